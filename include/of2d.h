@@ -1,0 +1,144 @@
+/*
+ * of2d.h — C-ABI of the MI355X-native OpticalFlow2d registration library
+ * (libof2d.so).  Plain pointers and sizes only; every entry point returns an
+ * int status (OF2D_OK = 0) and never throws across the boundary.
+ *
+ * The boundary replaces the reference's MEX entry point and the operator
+ * plug-in point underneath it:
+ *
+ *   reference                                   replaced by
+ *   -----------------------------------------   ---------------------------------
+ *   mexFunction (WrapperOpticalFlow2d.cpp:18-20) of2d_gateway (same 5 modes)
+ *   init branch            (:23-83)              of2d_create
+ *   register branch        (:86-102)             of2d_set_images + of2d_estimate
+ *   get-motion branch      (:105-117)            of2d_get_motion
+ *   warp branch            (:120-137)            of2d_warp
+ *   close branch           (:140-147)            of2d_destroy
+ *   ImageRegistration::estimate_motion
+ *     (src/ImageRegistration.cpp:133-156) and every
+ *     IterativeSolver::get_update
+ *     (src/regularization/IterativeSolver.h:22)  of2d_estimate (device-resident)
+ *   enum Regularisation/Verbose/MotionAccumulation
+ *     (src/SolverOptions.h:4-8)                  OF2D_REG_* / OF2D_VERBOSE_* /
+ *                                                OF2D_ACCUM_* (same values)
+ *
+ * Array layout at the boundary is the reference's: column-major with x fast,
+ * idx = i + j*dimx (src/Field.tpp:13; MATLAB [dimx, dimy]); images are double
+ * [dimx*dimy]; a motion field is planar double [dimx*dimy*2], x-plane first
+ * (src/Motion.cpp:23-39).
+ */
+#ifndef OF2D_H
+#define OF2D_H
+
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes ---- */
+#define OF2D_OK 0
+#define OF2D_ERR_INVALID_ARGUMENT 1 /* std::invalid_argument / mexErrMsgTxt on bad input */
+#define OF2D_ERR_RUNTIME 2          /* std::runtime_error, e.g. "Divide by zero exception" */
+#define OF2D_ERR_DEVICE 3           /* HIP / RCCL failure */
+#define OF2D_ERR_STATE 4            /* call sequence not allowed (mexErrMsgTxt :149-151) */
+
+/* ---- SolverOptions.h:4-8, identical integer values ---- */
+enum of2d_regularisation {
+    OF2D_REG_DIFFUSION = 0,
+    OF2D_REG_CURVATURE = 1,
+    OF2D_REG_ELASTIC = 2,
+    OF2D_REG_THIRIONS_DEMONS = 3,
+    OF2D_REG_DIFFEOMORPHIC_DEMONS = 4,
+    OF2D_REG_FLUID = 5
+};
+enum of2d_verbose { OF2D_VERBOSE_OFF = 0, OF2D_VERBOSE_ON = 1 };
+enum of2d_motion_accumulation { OF2D_ACCUM_COMPOSITION = 0, OF2D_ACCUM_ADDITION = 1 };
+
+typedef struct of2d_ctx of2d_ctx;
+
+/* Text the reference prints with mexPrintf (parameter banner
+ * ImageRegistration.cpp:6-47, Logger lines Logger.cpp:62-69, Fluid lines
+ * OpticalFlowFluid.cpp:94, ImageRegistrationFluid.cpp:110) goes through this
+ * hook; NULL restores the default (stdout).  Process-global. */
+typedef void (*of2d_print_fn)(const char *text, void *user);
+void of2d_set_print_hook(of2d_print_fn fn, void *user);
+
+/* ---- registration object (replaces the init branch, :23-83) ----
+ * niter has nscales+1 entries (finest level first, :35-38); regparams has
+ * nparams entries whose meaning follows the reference per regularisation
+ * (ImageRegistrationOpticalFlow.cpp:8-68, ImageRegistrationDemons.cpp:7-57,
+ * ImageRegistrationFluid.cpp:5-36).  Invalid nparams fails with
+ * OF2D_ERR_INVALID_ARGUMENT and the reference's message. */
+int of2d_create(of2d_ctx **out, int dimx, int dimy, const int *niter, int nscales, int reg,
+                const float *regparams, unsigned nparams, int nrefine, int verbose);
+/* register branch (:86-102): images are double [dimx*dimy] */
+int of2d_set_images(of2d_ctx *ctx, const double *Iref, const double *Imov);
+int of2d_estimate(of2d_ctx *ctx);
+/* get-motion branch (:105-117): out is double [dimx*dimy*2], planar */
+int of2d_get_motion(of2d_ctx *ctx, double *out);
+/* warp branch (:120-137): out is double [dimx*dimy] */
+int of2d_warp(of2d_ctx *ctx, const double *Imov, double *out);
+/* close branch (:140-147) */
+int of2d_destroy(of2d_ctx *ctx);
+const char *of2d_last_error(const of2d_ctx *ctx);
+/* iterations executed per (level, refine) of the last of2d_estimate, in
+ * execution order (coarsest level first); returns the number of entries */
+int of2d_iterations_executed(const of2d_ctx *ctx, int *out, int cap);
+/* per-iteration Logger error (Logger.cpp:32-51) of the last loop executed */
+int of2d_last_errors(const of2d_ctx *ctx, float *out, int cap);
+/* Options that the reference does not have (bench / deployment only):
+ *   "fixed_iters" (0/1): run every iteration, no convergence break
+ *   "chunk" (>=1): iterations enqueued between host convergence checks
+ *   "device" (>=0): HIP device ordinal, must be set before of2d_set_images */
+int of2d_set_option(of2d_ctx *ctx, const char *key, double value);
+
+/* ---- gateway: the process-global singleton of WrapperOpticalFlow2d.cpp:13.
+ * Mode is keyed on (nlhs, nrhs, singleton present) exactly like mexFunction:
+ *   init (0,8,no)  prhs = {[dimx dimy], niter, nscales, reg, regparams,
+ *                          nparams, nrefine, verbose}
+ *   register (0,2,yes) prhs = {Iref, Imov}
+ *   get (1,0,yes)  plhs[0] = double [dimx*dimy*2]
+ *   warp (1,1,yes) prhs = {Imov}, plhs[0] = double [dimx*dimy]
+ *   close (0,0,yes)
+ * anything else: OF2D_ERR_STATE with the reference's message (:149-151).
+ * plhs buffers are caller-allocated; of2d_gateway_output_numel tells the size. */
+int of2d_gateway(int nlhs, double **plhs, int nrhs, const double *const *prhs);
+size_t of2d_gateway_output_numel(int nlhs, int nrhs);
+int of2d_gateway_output_dims(int nlhs, int nrhs, size_t *dims, int *ndims);
+const char *of2d_gateway_last_error(void);
+
+/* ---- row-slab Horn-Schunck solver (multi-GPU north-star path) ----
+ * One process per GPU.  Global grid dimx x dimy is split into contiguous slabs
+ * of j-lines; rank r owns rows [row_begin, row_end) (of2d_slab_bounds).  The
+ * per-iteration halo (one j-line to each neighbour) travels over RCCL.
+ * nranks == 1 needs no unique id (pass NULL). */
+int of2d_slab_bounds(int dimy, int rank, int nranks, int *row_begin, int *row_end);
+int of2d_rccl_unique_id_size(void);
+int of2d_rccl_get_unique_id(void *out, int len);
+typedef struct of2d_slab of2d_slab;
+int of2d_slab_create(of2d_slab **out, int dimx, int dimy, float alpha, int rank, int nranks,
+                     int device, const void *rccl_unique_id, int id_len);
+/* images: rows [row_begin-1, row_end+1) clipped to [0, dimy), double, x fast */
+int of2d_slab_set_images(of2d_slab *s, const double *Iref_rows, const double *Imov_rows);
+/* runs niter Jacobi iterations (HS, Logger, convergence unless fixed_iters);
+ * *iters_done receives the iterations executed */
+int of2d_slab_run(of2d_slab *s, int niter, int fixed_iters, int *iters_done);
+/* owned rows of the motion, planar double [dimx*nrows*2] */
+int of2d_slab_get_motion(of2d_slab *s, double *out);
+/* average duration (microseconds) of the Jacobi kernel over nlaunch launches,
+ * timed with HIP events on the stream it is launched on */
+int of2d_slab_time_kernel(of2d_slab *s, int nlaunch, double *avg_us);
+/* wall time (ms, HIP events) of the last of2d_slab_run on this rank */
+int of2d_slab_last_run_ms(const of2d_slab *s, double *ms);
+int of2d_slab_destroy(of2d_slab *s);
+const char *of2d_slab_last_error(const of2d_slab *s);
+
+/* ---- library info ---- */
+const char *of2d_version(void);
+int of2d_device_count(int *count);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,94 @@
+// of2d_device.h — shared definitions for the gfx950 kernels and the host
+// driver of libof2d.so.
+//
+// HBM layout (DESIGN.md "Data layout"): every field of a pyramid level is a
+// pitched, row-major (j-line major, x fastest) array whose pitch P is dimx
+// rounded up to a multiple of 128 elements, with one zeroed ghost j-line above
+// row 0 and one below row dimy-1.  Images are float (4 B/px), motion fields
+// interleaved float2 (8 B/px) — the reference's layout (src/Field.tpp:13,
+// src/Motion.h:7) plus padding, so 2-px float4 loads of a motion row and 4-px
+// float4 loads of an image row are 16-B aligned.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <cstdint>
+#include <stdexcept>
+#include <string>
+
+namespace of2d {
+
+constexpr int kPitchAlign = 128;  // elements
+
+inline int pitch_for(int dimx) { return (dimx + kPitchAlign - 1) / kPitchAlign * kPitchAlign; }
+
+struct DeviceError : std::runtime_error {
+    using std::runtime_error::runtime_error;
+};
+
+#define OF2D_HIP(call)                                                                    \
+    do {                                                                                  \
+        hipError_t e_ = (call);                                                           \
+        if (e_ != hipSuccess)                                                             \
+            throw ::of2d::DeviceError(std::string("HIP error: ") + hipGetErrorString(e_) + \
+                                      " at " __FILE__ ":" + std::to_string(__LINE__));   \
+    } while (0)
+
+// status bits written by kernels (one word per context, zeroed per call)
+constexpr unsigned kStatusDivZero = 1u;
+
+// ---------------------------------------------------------------- HS Jacobi
+// Each wave marches kHsRows j-lines of a 128-px strip (2 px per lane); a block
+// is 4 waves stacked in y.
+constexpr int kHsRows = 16;
+constexpr int kHsStrip = 128;
+constexpr int kHsWaves = 4;
+inline dim3 hs_grid(int P, int nrows) {
+    return dim3(P / kHsStrip, (nrows + kHsRows * kHsWaves - 1) / (kHsRows * kHsWaves));
+}
+inline int hs_nblocks(int P, int nrows) {
+    dim3 g = hs_grid(P, nrows);
+    return int(g.x * g.y);
+}
+
+// One Jacobi step of OpticalFlowDiffusion::get_update with the Logger's norm
+// partials fused (sum ||u_new-u_old||, sum ||u_old|| per block, fp64).
+// Row pointers address the first owned row; rows -1 and nrows must be valid
+// memory (ghost j-lines).  row0 is the global j of the first owned row.
+void launch_hs_jacobi(const float2 *u_old, float2 *u_new, const float2 *dI, const float *It,
+                      int P, int dimx, int nrows, int row0, int dimy, float alphasq,
+                      double *partial, unsigned *status, hipStream_t st);
+// Sum C iterations' per-block partials in a fixed order: sums[2t+{0,1}] =
+// {sum ||diff||, sum ||prev||} for t < C.
+void launch_reduce_partials(const double *partial, int nblocks, int C, double *sums,
+                            hipStream_t st);
+
+// ---------------------------------------------------------------- fields
+void launch_d2f(const double *in, int dimx, int dimy, float *out, int P, int row_offset,
+                hipStream_t st);
+void launch_f2d(const float *in, int P, int dimx, int dimy, double *out, hipStream_t st);
+void launch_motion_to_planar(const float2 *m, int P, int dimx, int dimy, double *out,
+                             hipStream_t st);
+void launch_downsample_image(const float *in, int dxi, int dyi, int Pi, float *out, int dxo,
+                             int dyo, int Po, hipStream_t st);
+void launch_downsample_motion(const float2 *in, int dxi, int dyi, int Pi, float2 *out, int dxo,
+                              int dyo, int Po, hipStream_t st);
+void launch_upsample_motion(const float2 *in, int dxi, int dyi, int Pi, float2 *out, int dxo,
+                            int dyo, int Po, hipStream_t st);
+void launch_warp(const float *src, const float2 *u, float *dst, int dimx, int dimy, int P,
+                 hipStream_t st);
+void launch_gradients(const float *Iref, const float *Iaux, float2 *dI, float *It, int dimx,
+                      int dimy, int P, hipStream_t st);
+// slab variant: rows [0, nrows) of a slab whose first row is global j-line row0;
+// rows -1 and nrows are ghost j-lines holding the neighbours' image rows
+void launch_gradients_rows(const float *Iref, const float *Iaux, float2 *dI, float *It, int dimx,
+                           int nrows, int P, int row0, int dimy, hipStream_t st);
+void launch_accumulate(const float2 *m_old, const float2 *v, float2 *m_new, int dimx, int dimy,
+                       int P, hipStream_t st);
+void launch_compose_zero(const float2 *v, float2 *out, int dimx, int nrows, int P, int row0,
+                         int dimy, hipStream_t st);
+void launch_add_motion(const float2 *a, const float2 *b, float2 *out, int dimx, int dimy, int P,
+                       hipStream_t st);
+
+}  // namespace of2d

@@ -1,0 +1,149 @@
+// of2d_host.h — host-side driver of libof2d.so (C++ above the C-ABI).
+//
+// Registration mirrors the reference's ImageRegistration hierarchy
+// (src/ImageRegistration.{h,cpp}, src/ImageRegistration{OpticalFlow,Demons,
+// Fluid}.cpp): a pyramid of nscales+1 levels, nrefine warp-refine passes per
+// level, and an iteration loop per refine whose body is the solver's
+// get_update (src/regularization/**).  Everything below the C-ABI is device
+// resident: images, gradients, motion fields and Logger norms live in HBM and
+// the host only enqueues kernels and reads back a few bytes per chunk of
+// iterations to take the convergence decision.
+#pragma once
+
+#include <cstdarg>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "of2d_device.h"
+
+namespace of2d {
+
+void print(const char *fmt, ...) __attribute__((format(printf, 1, 2)));
+
+// ------------------------------------------------------------ device buffer
+// A pitched field with one ghost j-line above row 0 and one below the last
+// row; `p` points at row 0.  Zero-initialised like Field<T>::Field
+// (src/Field.tpp:15-18).
+template <class T>
+struct Field {
+    T *base = nullptr;
+    T *p = nullptr;
+    int dimx = 0, dimy = 0, P = 0;
+    size_t count = 0;
+    Field() = default;
+    Field(const Field &) = delete;
+    Field &operator=(const Field &) = delete;
+    Field(Field &&o) noexcept { *this = std::move(o); }
+    Field &operator=(Field &&o) noexcept {
+        std::swap(base, o.base);
+        std::swap(p, o.p);
+        std::swap(dimx, o.dimx);
+        std::swap(dimy, o.dimy);
+        std::swap(P, o.P);
+        std::swap(count, o.count);
+        return *this;
+    }
+    ~Field() { release(); }
+    void alloc(int dx, int dy, int ghost = 1) {
+        release();
+        dimx = dx;
+        dimy = dy;
+        P = pitch_for(dx);
+        count = (size_t)(dy + 2 * ghost) * P + kPitchAlign;
+        OF2D_HIP(hipMalloc(&base, count * sizeof(T)));
+        OF2D_HIP(hipMemset(base, 0, count * sizeof(T)));
+        p = base + (size_t)ghost * P;
+    }
+    void release() {
+        if (base) (void)hipFree(base);
+        base = p = nullptr;
+        count = 0;
+    }
+    void zero(hipStream_t st) { OF2D_HIP(hipMemsetAsync(base, 0, count * sizeof(T), st)); }
+    size_t bytes() const { return count * sizeof(T); }
+};
+
+// Pinned host scratch for the per-chunk read-back
+struct HostScratch {
+    double *sums = nullptr;
+    unsigned *status = nullptr;
+    float *flt = nullptr;
+    int cap = 0;
+    void ensure(int n);
+    ~HostScratch();
+};
+
+// Per-iteration Logger norms -> error, exactly the reference's float formula
+// (Logger.cpp:37-39, Motion.cpp:47) applied to fp64 sums.
+float logger_error(double sum_diff, double sum_prev, double npx);
+
+struct Level {
+    int dx = 0, dy = 0, P = 0;
+    Field<float> Iref, Imov, Iaux, It, Iwar, jac;
+    Field<float2> motion[2];
+    int mcur = 0;
+    Field<float2> dI;
+    Field<float2> est[3];
+    Field<float2> force, velocity, increment, corr, tmp;
+    Field<double> rhs;  // curvature spectral buffers (2 components)
+    float2 *cur_motion() { return motion[mcur].p; }
+};
+
+class Registration {
+   public:
+    Registration(int dimx, int dimy, int nscales, const int *niter, int nrefine, int reg,
+                 const float *params, unsigned nparams, int verbose);
+    ~Registration();
+    void set_images(const double *ref, const double *mov);
+    void estimate();
+    void get_motion(double *out);
+    void warp(const double *in, double *out);
+    void set_option(const std::string &key, double v);
+    const std::vector<int> &iterations() const { return iters_; }
+    const std::vector<float> &last_errors() const { return last_err_; }
+    int dimx() const { return dimx_; }
+    int dimy() const { return dimy_; }
+
+   private:
+    void ensure_device();
+    void estimate_level(int s);
+    int loop_hs(Level &L, int niter, float alpha, int &final_buf);
+    int loop_demons(Level &L, int niter, int &final_buf);
+    int loop_fluid(Level &L, int niter);
+    int loop_elastic(Level &L, int niter, int &final_buf);
+    int loop_curvature(Level &L, int niter, int &final_buf);
+    void check_status();
+
+    int dimx_, dimy_, nscales_, nrefine_, reg_, verbose_;
+    std::vector<int> niter_;
+    std::vector<float> params_;
+    std::vector<int> ldx_, ldy_;
+    std::vector<Level> lv_;
+    bool fixed_ = false;
+    int chunk_ = 32;
+    int device_ = -1;
+    bool ready_ = false;
+    hipStream_t st_ = nullptr;
+    double *d_stage_ = nullptr;  // double staging for boundary copies
+    size_t stage_count_ = 0;
+    double *d_partial_ = nullptr;
+    size_t partial_count_ = 0;
+    double *d_sums_ = nullptr;
+    unsigned *d_status_ = nullptr;
+    float *d_scalar_ = nullptr;
+    HostScratch hs_;
+    std::vector<int> iters_;
+    std::vector<float> last_err_;
+    // Demons kernels (Kernel::set_gaussian, src/Kernel.cpp:45-73)
+    std::vector<double> kdiff_, kfluid_;
+};
+
+// Validation of nparams per regularisation (ImageRegistrationOpticalFlow.cpp:8-12,
+// ImageRegistrationDemons.cpp:7-10, ImageRegistrationFluid.cpp:5-7)
+bool valid_regularisation_parameters(int reg, unsigned nparams);
+
+// Kernel::set_gaussian (src/Kernel.cpp:45-73): expf in float, normalised in double
+std::vector<double> gaussian_kernel(int kw, float sigma);
+
+}  // namespace of2d

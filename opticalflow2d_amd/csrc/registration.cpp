@@ -1,0 +1,331 @@
+// registration.cpp — device-resident registration driver (host C++ over HIP).
+//
+// Mirrors the control flow of the reference drivers:
+//   ImageRegistration::ImageRegistration / estimate_motion   src/ImageRegistration.cpp:49-156
+//   ImageRegistrationOpticalFlow::estimate_motion_at_current_resolution
+//                                                            src/ImageRegistrationOpticalFlow.cpp:97-151
+//   ImageRegistrationDemons::...                             src/ImageRegistrationDemons.cpp:86-137
+//   ImageRegistrationFluid::...                              src/ImageRegistrationFluid.cpp:67-142
+// The iteration loop is speculative: the host enqueues a chunk of iterations
+// without waiting, the fused Logger norms of the whole chunk come back in one
+// 16-B-per-iteration read, and the convergence test of Logger.cpp /
+// ImageRegistrationOpticalFlow.cpp:131-134 is evaluated on the host.  The
+// motion estimate rotates through three buffers, so the chunk's start state is
+// never overwritten: when the break fires inside a chunk the iterations up to
+// the break are replayed from that state (deterministic, bit-identical).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+
+#include "of2d_host.h"
+#include "of2d_solvers.h"
+
+namespace of2d {
+
+float logger_error(double sum_diff, double sum_prev, double npx) {
+    const float n = (float)npx;
+    const float prevnorm = (float)sum_prev / n;
+    const float diffnorm = (float)sum_diff / n;
+    return prevnorm == 0 ? 0.0f : diffnorm / prevnorm;
+}
+
+void HostScratch::ensure(int n) {
+    if (n <= cap) return;
+    if (sums) (void)hipHostFree(sums);
+    if (flt) (void)hipHostFree(flt);
+    if (!status) OF2D_HIP(hipHostMalloc(&status, 64 * sizeof(unsigned)));
+    OF2D_HIP(hipHostMalloc(&sums, sizeof(double) * 4 * n));
+    OF2D_HIP(hipHostMalloc(&flt, sizeof(float) * 4 * n));
+    cap = n;
+}
+HostScratch::~HostScratch() {
+    if (sums) (void)hipHostFree(sums);
+    if (flt) (void)hipHostFree(flt);
+    if (status) (void)hipHostFree(status);
+}
+
+bool valid_regularisation_parameters(int reg, unsigned np) {
+    switch (reg) {
+        case 0: return np == 1;
+        case 1: return np >= 1 && np <= 2;
+        case 2: return np >= 2 && np <= 3;
+        case 3: return np == 6;
+        case 4: return np == 5;
+        case 5: return np >= 2 && np <= 3;
+    }
+    return false;
+}
+
+std::vector<double> gaussian_kernel(int kw, float sigma) {
+    std::vector<double> k((size_t)kw * kw);
+    const int cx = (int)(((unsigned)kw - 1u) / 2u), cy = cx;
+    double weight = 0;
+    for (int i = 0; i < kw; i++)
+        for (int j = 0; j < kw; j++) {
+            const int idx = i + j * kw;
+            const float num = (float)(-((i - cx) * (i - cx) + (j - cy) * (j - cy)));
+            k[idx] = (double)expf(num / (2 * sigma * sigma));
+            weight += k[idx];
+        }
+    for (auto &v : k) v /= weight;
+    return k;
+}
+
+static const char kRule[] =
+    "%%%%%%%%%%%%%%%%%%%%%%%%%%%%%%%%%%%%%%%%%%%%%%%%%%%%%%%%%%%%%%%%%%%%%%%";  // 71 x '%'
+
+Registration::Registration(int dimx, int dimy, int nscales, const int *niter, int nrefine,
+                           int reg, const float *params, unsigned nparams, int verbose)
+    : dimx_(dimx), dimy_(dimy), nscales_(nscales), nrefine_(nrefine), reg_(reg),
+      verbose_(verbose) {
+    if (reg < 0 || reg > 5) throw std::invalid_argument("Error: invalid regularisation given\n");
+    if (dimx <= 0 || dimy <= 0 || nscales < 0)
+        throw std::invalid_argument("Error: invalid image dimensions\n");
+    niter_.assign(niter, niter + nscales + 1);
+    params_.assign(params, params + nparams);
+    // ImageRegistration.cpp:56-61: dim(dimin.x/scale, dimin.y/scale) with float scale
+    ldx_.resize(nscales + 1);
+    ldy_.resize(nscales + 1);
+    for (int s = nscales; s >= 0; s--) {
+        const float scale = (float)std::pow(2, s);
+        ldx_[s] = (int)(unsigned)((float)(unsigned)dimx / scale);
+        ldy_[s] = (int)(unsigned)((float)(unsigned)dimy / scale);
+    }
+    // ImageRegistration::display_registration_parameters (ImageRegistration.cpp:6-47),
+    // printed before the parameter check exactly like the reference (:80, then set_solver)
+    print("%s\n", kRule + 0);
+    print("Optical flow image registration started... (2D C++ implementation)...\n");
+    print("Registration parameters:\n");
+    print("dimensions:\t\t\t\t(%d %d)\n", ldx_[0], ldy_[0]);
+    print("niter:\t\t\t\t\t(%d", niter_[0]);
+    for (int s = 1; s < nscales + 1; s++) print(" %d", niter_[s]);
+    print(")\n");
+    print("nscales:\t\t\t\t%d\n", nscales);
+    print("nrefine:\t\t\t\t%d\n", nrefine);
+    static const char *names[] = {"Diffusion", "Curvature", "Elastic", "Thirions Demons",
+                                  "Diffeomorphic Demons", "Fluid"};
+    print("regularisation:\t\t\t\t%s\n", names[reg]);
+    if (nparams == 1) {
+        print("reg. param:\t\t\t\t%.2f\n", (double)params[0]);
+    } else if (nparams > 1) {
+        print("reg. params:\t\t\t\t(%.2f", (double)params[0]);
+        for (unsigned p = 1; p < nparams; p++) print(" %.2f", (double)params[p]);
+        print(")\n");
+    }
+    print("%s\n\n", kRule);
+    if (!valid_regularisation_parameters(reg, nparams))
+        throw std::invalid_argument(
+            "Invalid number of regularisation parameters for given regularisation method.\n");
+    for (int s = 0; s <= nscales; s++)
+        if (ldx_[s] <= 0 || ldy_[s] <= 0)
+            throw std::invalid_argument("Error: pyramid level with zero size\n");
+    if (reg == 3 || reg == 4) {  // Demons.cpp:19-23
+        const int kw = (int)(unsigned)params[4];
+        if (kw < 1) throw std::invalid_argument("Error: Demons kernel width must be >= 1\n");
+        kdiff_ = gaussian_kernel(kw, params[2]);
+        kfluid_ = gaussian_kernel(kw, params[3]);
+    }
+}
+
+Registration::~Registration() {
+    if (d_stage_) (void)hipFree(d_stage_);
+    if (d_partial_) (void)hipFree(d_partial_);
+    if (d_sums_) (void)hipFree(d_sums_);
+    if (d_status_) (void)hipFree(d_status_);
+    if (d_scalar_) (void)hipFree(d_scalar_);
+    lv_.clear();
+    if (st_) (void)hipStreamDestroy(st_);
+}
+
+void Registration::set_option(const std::string &key, double v) {
+    if (key == "fixed_iters")
+        fixed_ = v != 0;
+    else if (key == "chunk")
+        chunk_ = std::max(1, (int)v);
+    else if (key == "device") {
+        if (ready_) throw std::invalid_argument("option 'device' must be set before first use");
+        device_ = (int)v;
+    } else
+        throw std::invalid_argument("unknown option: " + key);
+}
+
+void Registration::ensure_device() {
+    if (ready_) return;
+    if (device_ >= 0) OF2D_HIP(hipSetDevice(device_));
+    OF2D_HIP(hipStreamCreateWithFlags(&st_, hipStreamNonBlocking));
+    lv_.resize(nscales_ + 1);
+    size_t maxnb = 1;
+    for (int s = 0; s <= nscales_; s++) {
+        Level &L = lv_[s];
+        L.dx = ldx_[s];
+        L.dy = ldy_[s];
+        L.P = pitch_for(L.dx);
+        L.Iref.alloc(L.dx, L.dy);
+        L.Imov.alloc(L.dx, L.dy);
+        L.Iaux.alloc(L.dx, L.dy);
+        L.It.alloc(L.dx, L.dy);
+        L.motion[0].alloc(L.dx, L.dy);
+        L.motion[1].alloc(L.dx, L.dy);
+        L.dI.alloc(L.dx, L.dy);
+        for (auto &e : L.est) e.alloc(L.dx, L.dy);
+        solvers::alloc_level(L, reg_);
+        maxnb = std::max(maxnb, (size_t)solvers::max_partial_blocks(L, reg_));
+    }
+    stage_count_ = (size_t)dimx_ * dimy_ * 2;
+    OF2D_HIP(hipMalloc(&d_stage_, stage_count_ * sizeof(double)));
+    partial_count_ = (size_t)chunk_ * maxnb * 2;
+    OF2D_HIP(hipMalloc(&d_partial_, partial_count_ * sizeof(double)));
+    OF2D_HIP(hipMalloc(&d_sums_, sizeof(double) * 4 * (size_t)std::max(chunk_, 64)));
+    OF2D_HIP(hipMalloc(&d_status_, 64 * sizeof(unsigned)));
+    OF2D_HIP(hipMemset(d_status_, 0, 64 * sizeof(unsigned)));
+    OF2D_HIP(hipMalloc(&d_scalar_, 64 * sizeof(float)));
+    hs_.ensure(std::max(chunk_, 64));
+    ready_ = true;
+}
+
+// ImageRegistration::set_reference_image / set_moving_image (:103-121)
+void Registration::set_images(const double *ref, const double *mov) {
+    ensure_device();
+    const size_t n0 = (size_t)dimx_ * dimy_;
+    Level &L0 = lv_[0];
+    for (int which = 0; which < 2; which++) {
+        const double *src = which ? mov : ref;
+        OF2D_HIP(hipMemcpyAsync(d_stage_, src, n0 * sizeof(double), hipMemcpyHostToDevice, st_));
+        Field<float> &dst0 = which ? L0.Imov : L0.Iref;
+        launch_d2f(d_stage_, dimx_, dimy_, dst0.p, L0.P, 0, st_);
+        for (int s = nscales_; s >= 1; s--) {
+            Field<float> &dst = which ? lv_[s].Imov : lv_[s].Iref;
+            launch_downsample_image(dst0.p, L0.dx, L0.dy, L0.P, dst.p, lv_[s].dx, lv_[s].dy,
+                                    lv_[s].P, st_);
+        }
+    }
+    OF2D_HIP(hipStreamSynchronize(st_));
+}
+
+void Registration::check_status() {
+    OF2D_HIP(hipMemcpyAsync(hs_.status, d_status_, sizeof(unsigned), hipMemcpyDeviceToHost, st_));
+    OF2D_HIP(hipStreamSynchronize(st_));
+    if (hs_.status[0] & kStatusDivZero) {
+        OF2D_HIP(hipMemsetAsync(d_status_, 0, sizeof(unsigned), st_));
+        throw std::runtime_error("Divide by zero exception");
+    }
+}
+
+// ImageRegistration::estimate_motion (:133-156)
+void Registration::estimate() {
+    ensure_device();
+    iters_.clear();
+    OF2D_HIP(hipMemsetAsync(d_status_, 0, 64 * sizeof(unsigned), st_));
+    Level &L0 = lv_[0];
+    for (int s = nscales_; s >= 0; s--) {
+        Level &L = lv_[s];
+        if (s > 0 && s < nscales_)
+            launch_downsample_motion(L0.cur_motion(), L0.dx, L0.dy, L0.P, L.cur_motion(), L.dx,
+                                     L.dy, L.P, st_);
+        estimate_level(s);
+        if (s > 0)
+            launch_upsample_motion(L.cur_motion(), L.dx, L.dy, L.P, L0.cur_motion(), L0.dx,
+                                   L0.dy, L0.P, st_);
+    }
+    OF2D_HIP(hipStreamSynchronize(st_));
+}
+
+// estimate_motion_at_current_resolution of the three drivers
+void Registration::estimate_level(int s) {
+    Level &L = lv_[s];
+    const int niter = niter_[s];
+    const bool demons = (reg_ == 3 || reg_ == 4);
+    for (int refine = 0; refine < nrefine_; refine++) {
+        // *Iaux = *Imov; Iaux->warp2d(*motion)
+        launch_warp(L.Imov.p, L.cur_motion(), L.Iaux.p, L.dx, L.dy, L.P, st_);
+        if (!demons) launch_gradients(L.Iref.p, L.Iaux.p, L.dI.p, L.It.p, L.dx, L.dy, L.P, st_);
+        L.est[0].zero(st_);  // motion_est starts at zero (reset() at :141 / new Motion)
+        int fin = 0, it = 0;
+        switch (reg_) {
+            case 0: it = loop_hs(L, niter, params_[0], fin); break;
+            case 1: it = loop_curvature(L, niter, fin); break;
+            case 2: it = loop_elastic(L, niter, fin); break;
+            case 3:
+            case 4: it = loop_demons(L, niter, fin); break;
+            case 5: it = loop_fluid(L, niter); break;
+        }
+        iters_.push_back(it);
+        // motion->accumulate(*motion_est)
+        launch_accumulate(L.motion[L.mcur].p, L.est[fin].p, L.motion[1 - L.mcur].p, L.dx, L.dy,
+                          L.P, st_);
+        L.mcur ^= 1;
+    }
+}
+
+// HS iteration loop (ImageRegistrationOpticalFlow.cpp:117-135) with fused Logger
+int Registration::loop_hs(Level &L, int niter, float alpha, int &final_buf) {
+    const float alphasq = alpha * alpha;  // OpticalFlowDiffusion.cpp:70
+    const int nb = hs_nblocks(L.P, L.dy);
+    const double npx = (double)L.dx * L.dy;
+    last_err_.clear();
+    int a = 0, k0 = 0;
+    auto seq_src = [](int a_, int t) { return t == 0 ? a_ : (t % 2 == 1 ? (a_ + 1) % 3 : (a_ + 2) % 3); };
+    auto seq_dst = [](int a_, int t) { return t % 2 == 0 ? (a_ + 1) % 3 : (a_ + 2) % 3; };
+    while (k0 < niter) {
+        const int C = std::min(chunk_, niter - k0);
+        for (int t = 0; t < C; t++)
+            launch_hs_jacobi(L.est[seq_src(a, t)].p, L.est[seq_dst(a, t)].p, L.dI.p, L.It.p, L.P,
+                             L.dx, L.dy, 0, L.dy, alphasq, d_partial_ + (size_t)t * nb * 2,
+                             d_status_, st_);
+        launch_reduce_partials(d_partial_, nb, C, d_sums_, st_);
+        OF2D_HIP(hipMemcpyAsync(hs_.sums, d_sums_, sizeof(double) * 2 * C, hipMemcpyDeviceToHost,
+                                st_));
+        check_status();  // synchronises the stream
+        for (int t = 0; t < C; t++) {
+            const int k = k0 + t;
+            const float err = logger_error(hs_.sums[2 * t], hs_.sums[2 * t + 1], npx);
+            last_err_.push_back(err);
+            if (verbose_) print("Iteration: %d\tError:%.4f\n", k, (double)err);
+            if (!fixed_ && err < 0.001f && k > 1) {
+                if (t + 2 <= C - 1) {  // dst(t) was overwritten by iteration t+2: replay
+                    for (int r = 0; r <= t; r++)
+                        launch_hs_jacobi(L.est[seq_src(a, r)].p, L.est[seq_dst(a, r)].p, L.dI.p,
+                                         L.It.p, L.P, L.dx, L.dy, 0, L.dy, alphasq, d_partial_,
+                                         d_status_, st_);
+                }
+                final_buf = seq_dst(a, t);
+                return k + 1;
+            }
+        }
+        a = seq_dst(a, C - 1);
+        k0 += C;
+    }
+    final_buf = a;
+    return niter;
+}
+
+// WrapperOpticalFlow2d.cpp:105-117 -> Motion::copy_motion_to_input
+void Registration::get_motion(double *out) {
+    ensure_device();
+    Level &L0 = lv_[0];
+    launch_motion_to_planar(L0.cur_motion(), L0.P, dimx_, dimy_, d_stage_, st_);
+    OF2D_HIP(hipMemcpyAsync(out, d_stage_, sizeof(double) * 2 * dimx_ * dimy_,
+                            hipMemcpyDeviceToHost, st_));
+    OF2D_HIP(hipStreamSynchronize(st_));
+}
+
+// WrapperOpticalFlow2d.cpp:120-137: Imov.set_image; Imov.warp2d(motion[0])
+void Registration::warp(const double *in, double *out) {
+    ensure_device();
+    Level &L0 = lv_[0];
+    const size_t n0 = (size_t)dimx_ * dimy_;
+    OF2D_HIP(hipMemcpyAsync(d_stage_, in, n0 * sizeof(double), hipMemcpyHostToDevice, st_));
+    Field<float> a, b;
+    a.alloc(dimx_, dimy_);
+    b.alloc(dimx_, dimy_);
+    launch_d2f(d_stage_, dimx_, dimy_, a.p, L0.P, 0, st_);
+    launch_warp(a.p, L0.cur_motion(), b.p, dimx_, dimy_, L0.P, st_);
+    launch_f2d(b.p, L0.P, dimx_, dimy_, d_stage_, st_);
+    OF2D_HIP(hipMemcpyAsync(out, d_stage_, n0 * sizeof(double), hipMemcpyDeviceToHost, st_));
+    OF2D_HIP(hipStreamSynchronize(st_));
+}
+
+}  // namespace of2d

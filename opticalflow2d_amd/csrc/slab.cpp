@@ -1,0 +1,317 @@
+// slab.cpp — row-slab Horn-Schunck over RCCL (the multi-GPU north-star path).
+//
+// The global dimx x dimy grid is cut into contiguous slabs of j-lines (the
+// memory-slow axis), one per process/GPU.  A Jacobi step of
+// OpticalFlowDiffusion::get_update (OpticalFlowDiffusion.cpp:43-55) at j-line
+// j reads u at j-1 and j+1, so each slab keeps one ghost j-line above and one
+// below and, before every step, sends its first owned j-line to the rank above
+// and its last to the rank below (ncclSend/ncclRecv of 8*dimx bytes each, one
+// group).  The Logger's norms (Logger.cpp:32-51) are fused into the stencil
+// kernel per block, reduced per rank, and all-reduced once per chunk of
+// iterations (two doubles per iteration) — the host then applies the
+// reference's break test (ImageRegistrationOpticalFlow.cpp:131-134).
+// The border rule of gradients::qlaplacian uses the GLOBAL j (gradients.h:73),
+// so the slab result equals the single-grid result bit for bit.
+//
+// The slab path registers with zero initial motion, one level, one refine:
+// warp2d by a zero field is the identity (src/Image.cpp:144-173 with fx=fy=0),
+// so Iaux == Imov and the gradients are taken of Imov directly.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cstring>
+#include <string>
+
+#include "../../include/of2d.h"
+#include "of2d_host.h"
+
+#define OF2D_NCCL(call)                                                                   \
+    do {                                                                                  \
+        ncclResult_t r_ = (call);                                                         \
+        if (r_ != ncclSuccess)                                                            \
+            throw ::of2d::DeviceError(std::string("RCCL error: ") + ncclGetErrorString(r_)); \
+    } while (0)
+
+struct of2d_slab {
+    int dimx = 0, dimy = 0, rank = 0, nranks = 1, rb = 0, re = 0, nrows = 0, P = 0;
+    int device = 0;
+    float alpha = 0.0f;
+    hipStream_t st = nullptr;
+    ncclComm_t comm = nullptr;
+    of2d::Field<float2> u[3];
+    of2d::Field<float2> dI;
+    of2d::Field<float> It, Iref, Imov;
+    double *d_partial = nullptr, *d_sums = nullptr, *d_stage = nullptr;
+    unsigned *d_status = nullptr;
+    of2d::HostScratch hs;
+    int chunk = 32;
+    int fin = 0;  // buffer holding the final motion
+    double last_ms = 0.0;
+    std::vector<float> errs;
+    std::string err;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+};
+
+namespace {
+thread_local std::string g_create_err;
+
+template <class F>
+int sguard(of2d_slab *s, F &&f) {
+    try {
+        f();
+        if (s) s->err.clear();
+        return OF2D_OK;
+    } catch (const std::invalid_argument &e) {
+        if (s) s->err = e.what();
+        return OF2D_ERR_INVALID_ARGUMENT;
+    } catch (const of2d::DeviceError &e) {
+        if (s) s->err = e.what();
+        return OF2D_ERR_DEVICE;
+    } catch (const std::exception &e) {
+        if (s) s->err = e.what();
+        return OF2D_ERR_RUNTIME;
+    }
+}
+
+void halo_exchange(of2d_slab *s, float2 *u) {
+    if (s->nranks == 1) return;
+    const size_t cnt = 2 * (size_t)s->dimx;  // one j-line of float2
+    const long P = s->P;
+    OF2D_NCCL(ncclGroupStart());
+    if (s->rank > 0) {
+        OF2D_NCCL(ncclSend(u, cnt, ncclFloat, s->rank - 1, s->comm, s->st));
+        OF2D_NCCL(ncclRecv(u - P, cnt, ncclFloat, s->rank - 1, s->comm, s->st));
+    }
+    if (s->rank < s->nranks - 1) {
+        OF2D_NCCL(ncclSend(u + (long)(s->nrows - 1) * P, cnt, ncclFloat, s->rank + 1, s->comm,
+                           s->st));
+        OF2D_NCCL(ncclRecv(u + (long)s->nrows * P, cnt, ncclFloat, s->rank + 1, s->comm, s->st));
+    }
+    OF2D_NCCL(ncclGroupEnd());
+}
+}  // namespace
+
+extern "C" {
+
+int of2d_slab_bounds(int dimy, int rank, int nranks, int *row_begin, int *row_end) {
+    if (dimy <= 0 || nranks <= 0 || rank < 0 || rank >= nranks || !row_begin || !row_end)
+        return OF2D_ERR_INVALID_ARGUMENT;
+    const int base = dimy / nranks, rem = dimy % nranks;
+    *row_begin = rank * base + std::min(rank, rem);
+    *row_end = *row_begin + base + (rank < rem ? 1 : 0);
+    return OF2D_OK;
+}
+
+int of2d_rccl_unique_id_size(void) { return (int)sizeof(ncclUniqueId); }
+
+int of2d_rccl_get_unique_id(void *out, int len) {
+    if (!out || len < (int)sizeof(ncclUniqueId)) return OF2D_ERR_INVALID_ARGUMENT;
+    ncclUniqueId id;
+    if (ncclGetUniqueId(&id) != ncclSuccess) return OF2D_ERR_DEVICE;
+    std::memcpy(out, &id, sizeof id);
+    return OF2D_OK;
+}
+
+int of2d_slab_create(of2d_slab **out, int dimx, int dimy, float alpha, int rank, int nranks,
+                     int device, const void *uid, int id_len) {
+    if (!out) return OF2D_ERR_INVALID_ARGUMENT;
+    *out = nullptr;
+    auto *s = new of2d_slab();
+    int rc = sguard(s, [&] {
+        if (dimx < 3 || dimy < 3) throw std::invalid_argument("slab: grid too small");
+        if (of2d_slab_bounds(dimy, rank, nranks, &s->rb, &s->re) != OF2D_OK)
+            throw std::invalid_argument("slab: bad rank/nranks");
+        s->nrows = s->re - s->rb;
+        if (s->nrows < 1) throw std::invalid_argument("slab: more ranks than j-lines");
+        s->dimx = dimx;
+        s->dimy = dimy;
+        s->rank = rank;
+        s->nranks = nranks;
+        s->alpha = alpha;
+        s->device = device;
+        s->P = of2d::pitch_for(dimx);
+        OF2D_HIP(hipSetDevice(device));
+        OF2D_HIP(hipStreamCreateWithFlags(&s->st, hipStreamNonBlocking));
+        OF2D_HIP(hipEventCreate(&s->ev0));
+        OF2D_HIP(hipEventCreate(&s->ev1));
+        for (auto &f : s->u) f.alloc(dimx, s->nrows);
+        s->dI.alloc(dimx, s->nrows);
+        s->It.alloc(dimx, s->nrows);
+        s->Iref.alloc(dimx, s->nrows);
+        s->Imov.alloc(dimx, s->nrows);
+        const int nb = of2d::hs_nblocks(s->P, s->nrows);
+        OF2D_HIP(hipMalloc(&s->d_partial, sizeof(double) * 2 * (size_t)nb * s->chunk));
+        OF2D_HIP(hipMalloc(&s->d_sums, sizeof(double) * 2 * s->chunk));
+        OF2D_HIP(hipMalloc(&s->d_status, 64 * sizeof(unsigned)));
+        OF2D_HIP(hipMemset(s->d_status, 0, 64 * sizeof(unsigned)));
+        OF2D_HIP(hipMalloc(&s->d_stage, sizeof(double) * 2 * (size_t)dimx * (s->nrows + 2)));
+        s->hs.ensure(s->chunk);
+        if (nranks > 1) {
+            if (!uid || id_len < (int)sizeof(ncclUniqueId))
+                throw std::invalid_argument("slab: RCCL unique id required for nranks > 1");
+            ncclUniqueId id;
+            std::memcpy(&id, uid, sizeof id);
+            OF2D_NCCL(ncclCommInitRank(&s->comm, nranks, id, rank));
+        }
+    });
+    if (rc != OF2D_OK) {
+        g_create_err = s->err;
+        of2d_slab_destroy(s);
+        return rc;
+    }
+    *out = s;
+    return OF2D_OK;
+}
+
+int of2d_slab_set_images(of2d_slab *s, const double *Iref_rows, const double *Imov_rows) {
+    if (!s || !Iref_rows || !Imov_rows) return OF2D_ERR_INVALID_ARGUMENT;
+    return sguard(s, [&] {
+        // rows [rb-1, re+1) clipped to [0, dimy) -> local rows [-has_up, nrows+has_dn)
+        const int has_up = s->rb > 0 ? 1 : 0, has_dn = s->re < s->dimy ? 1 : 0;
+        const int rows = s->nrows + has_up + has_dn;
+        for (int which = 0; which < 2; which++) {
+            const double *src = which ? Imov_rows : Iref_rows;
+            of2d::Field<float> &dst = which ? s->Imov : s->Iref;
+            OF2D_HIP(hipMemcpyAsync(s->d_stage, src, sizeof(double) * s->dimx * rows,
+                                    hipMemcpyHostToDevice, s->st));
+            of2d::launch_d2f(s->d_stage, s->dimx, rows, dst.p - (long)has_up * s->P, s->P, 0,
+                             s->st);
+        }
+        // IterativeSolver::set_derivatives(Iref, Iaux = Imov) on the owned rows
+        of2d::launch_gradients_rows(s->Iref.p, s->Imov.p, s->dI.p, s->It.p, s->dimx, s->nrows,
+                                    s->P, s->rb, s->dimy, s->st);
+        for (auto &f : s->u) f.zero(s->st);
+        s->fin = 0;
+        OF2D_HIP(hipStreamSynchronize(s->st));
+    });
+}
+
+int of2d_slab_run(of2d_slab *s, int niter, int fixed_iters, int *iters_done) {
+    if (!s) return OF2D_ERR_INVALID_ARGUMENT;
+    return sguard(s, [&] {
+        const float alphasq = s->alpha * s->alpha;
+        const int nb = of2d::hs_nblocks(s->P, s->nrows);
+        const double npx = (double)s->dimx * s->dimy;
+        auto src_of = [](int a, int t) { return t == 0 ? a : (t % 2 == 1 ? (a + 1) % 3 : (a + 2) % 3); };
+        auto dst_of = [](int a, int t) { return t % 2 == 0 ? (a + 1) % 3 : (a + 2) % 3; };
+        auto step = [&](int a, int t, double *partial) {
+            float2 *uin = s->u[src_of(a, t)].p;
+            halo_exchange(s, uin);
+            of2d::launch_hs_jacobi(uin, s->u[dst_of(a, t)].p, s->dI.p, s->It.p, s->P, s->dimx,
+                                   s->nrows, s->rb, s->dimy, alphasq, partial, s->d_status, s->st);
+        };
+        for (auto &f : s->u) f.zero(s->st);  // motion_est starts at zero
+        OF2D_HIP(hipMemsetAsync(s->d_status, 0, sizeof(unsigned), s->st));
+        s->errs.clear();
+        OF2D_HIP(hipEventRecord(s->ev0, s->st));
+        int a = 0, k0 = 0, done = -1;
+        while (k0 < niter && done < 0) {
+            const int C = std::min(s->chunk, niter - k0);
+            for (int t = 0; t < C; t++) step(a, t, s->d_partial + (size_t)t * nb * 2);
+            of2d::launch_reduce_partials(s->d_partial, nb, C, s->d_sums, s->st);
+            if (s->nranks > 1)
+                OF2D_NCCL(ncclAllReduce(s->d_sums, s->d_sums, 2 * (size_t)C, ncclDouble, ncclSum,
+                                        s->comm, s->st));
+            OF2D_HIP(hipMemcpyAsync(s->hs.sums, s->d_sums, sizeof(double) * 2 * C,
+                                    hipMemcpyDeviceToHost, s->st));
+            OF2D_HIP(hipMemcpyAsync(s->hs.status, s->d_status, sizeof(unsigned),
+                                    hipMemcpyDeviceToHost, s->st));
+            OF2D_HIP(hipStreamSynchronize(s->st));
+            if (s->hs.status[0] & of2d::kStatusDivZero)
+                throw std::runtime_error("Divide by zero exception");
+            for (int t = 0; t < C; t++) {
+                const int k = k0 + t;
+                const float e = of2d::logger_error(s->hs.sums[2 * t], s->hs.sums[2 * t + 1], npx);
+                s->errs.push_back(e);
+                if (!fixed_iters && e < 0.001f && k > 1) {
+                    if (t + 2 <= C - 1)  // replay up to the break (all ranks agree: sums are global)
+                        for (int r = 0; r <= t; r++) step(a, r, s->d_partial);
+                    s->fin = dst_of(a, t);
+                    done = k + 1;
+                    break;
+                }
+            }
+            if (done < 0) {
+                a = dst_of(a, C - 1);
+                k0 += C;
+            }
+        }
+        if (done < 0) {
+            s->fin = a;
+            done = niter;
+        }
+        OF2D_HIP(hipEventRecord(s->ev1, s->st));
+        OF2D_HIP(hipEventSynchronize(s->ev1));
+        float ms = 0.0f;
+        OF2D_HIP(hipEventElapsedTime(&ms, s->ev0, s->ev1));
+        s->last_ms = ms;
+        if (iters_done) *iters_done = done;
+    });
+}
+
+int of2d_slab_get_motion(of2d_slab *s, double *out) {
+    if (!s || !out) return OF2D_ERR_INVALID_ARGUMENT;
+    return sguard(s, [&] {
+        // motion->accumulate(*motion_est) onto the zero initial motion, then planar
+        // output (Motion::copy_motion_to_input); the scratch buffer is one not holding fin
+        float2 *tmp = s->u[(s->fin + 1) % 3].p;
+        of2d::launch_compose_zero(s->u[s->fin].p, tmp, s->dimx, s->nrows, s->P, s->rb, s->dimy,
+                                  s->st);
+        of2d::launch_motion_to_planar(tmp, s->P, s->dimx, s->nrows, s->d_stage, s->st);
+        OF2D_HIP(hipMemcpyAsync(out, s->d_stage, sizeof(double) * 2 * s->dimx * s->nrows,
+                                hipMemcpyDeviceToHost, s->st));
+        OF2D_HIP(hipStreamSynchronize(s->st));
+    });
+}
+
+int of2d_slab_time_kernel(of2d_slab *s, int nlaunch, double *avg_us) {
+    if (!s || nlaunch <= 0 || !avg_us) return OF2D_ERR_INVALID_ARGUMENT;
+    return sguard(s, [&] {
+        const float alphasq = s->alpha * s->alpha;
+        // warm-up launch, then nlaunch back-to-back launches between two events
+        of2d::launch_hs_jacobi(s->u[1].p, s->u[2].p, s->dI.p, s->It.p, s->P, s->dimx, s->nrows,
+                               s->rb, s->dimy, alphasq, s->d_partial, s->d_status, s->st);
+        OF2D_HIP(hipEventRecord(s->ev0, s->st));
+        for (int k = 0; k < nlaunch; k++)
+            of2d::launch_hs_jacobi(s->u[1 + (k & 1)].p, s->u[2 - (k & 1)].p, s->dI.p, s->It.p,
+                                   s->P, s->dimx, s->nrows, s->rb, s->dimy, alphasq, s->d_partial,
+                                   s->d_status, s->st);
+        OF2D_HIP(hipEventRecord(s->ev1, s->st));
+        OF2D_HIP(hipEventSynchronize(s->ev1));
+        float ms = 0.0f;
+        OF2D_HIP(hipEventElapsedTime(&ms, s->ev0, s->ev1));
+        *avg_us = 1000.0 * ms / nlaunch;
+    });
+}
+
+int of2d_slab_last_run_ms(const of2d_slab *s, double *ms) {
+    if (!s || !ms) return OF2D_ERR_INVALID_ARGUMENT;
+    *ms = s->last_ms;
+    return OF2D_OK;
+}
+
+int of2d_slab_destroy(of2d_slab *s) {
+    if (!s) return OF2D_ERR_INVALID_ARGUMENT;
+    if (s->comm) ncclCommDestroy(s->comm);
+    if (s->d_partial) (void)hipFree(s->d_partial);
+    if (s->d_sums) (void)hipFree(s->d_sums);
+    if (s->d_status) (void)hipFree(s->d_status);
+    if (s->d_stage) (void)hipFree(s->d_stage);
+    if (s->ev0) (void)hipEventDestroy(s->ev0);
+    if (s->ev1) (void)hipEventDestroy(s->ev1);
+    for (auto &f : s->u) f.release();
+    s->dI.release();
+    s->It.release();
+    s->Iref.release();
+    s->Imov.release();
+    if (s->st) (void)hipStreamDestroy(s->st);
+    delete s;
+    return OF2D_OK;
+}
+
+const char *of2d_slab_last_error(const of2d_slab *s) {
+    return s ? s->err.c_str() : g_create_err.c_str();
+}
+
+}  // extern "C"

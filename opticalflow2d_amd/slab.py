@@ -1,0 +1,108 @@
+"""Row-slab Horn-Schunck across GPUs (one process per GPU, RCCL halo).
+
+Python handle on the ``of2d_slab_*`` part of the C-ABI.  The decomposition is
+``of2d_slab_bounds``: rank r of N owns j-lines [row_begin, row_end) of the
+global grid; the RCCL unique id is created by rank 0 with
+``of2d_rccl_get_unique_id`` and handed to the other ranks by the caller (for
+example over ``torch.distributed`` with the gloo backend).
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Optional, Tuple
+
+import numpy as np
+
+from . import _lib
+from ._lib import check
+
+
+def slab_bounds(dimy: int, rank: int, nranks: int) -> Tuple[int, int]:
+    """[row_begin, row_end) of rank's slab (contiguous j-lines, remainder to the
+    lowest ranks)."""
+    b, e = C.c_int(), C.c_int()
+    st = _lib.lib().of2d_slab_bounds(int(dimy), int(rank), int(nranks), C.byref(b), C.byref(e))
+    check(st, "slab_bounds: invalid arguments")
+    return b.value, e.value
+
+
+def halo_rows(dimy: int, rank: int, nranks: int) -> Tuple[int, int]:
+    """Image rows a rank must supply: [row_begin-1, row_end+1) clipped."""
+    b, e = slab_bounds(dimy, rank, nranks)
+    return max(b - 1, 0), min(e + 1, dimy)
+
+
+def rccl_unique_id() -> bytes:
+    L = _lib.lib()
+    n = L.of2d_rccl_unique_id_size()
+    buf = (C.c_char * n)()
+    check(L.of2d_rccl_get_unique_id(buf, n), "ncclGetUniqueId failed")
+    return bytes(buf)
+
+
+class SlabSolver:
+    """One rank's slab of a global HS registration (zero initial motion, one
+    level, one refine — see opticalflow2d_amd/csrc/slab.cpp)."""
+
+    def __init__(self, dimx: int, dimy: int, alpha: float, rank: int = 0, nranks: int = 1,
+                 device: int = 0, unique_id: Optional[bytes] = None):
+        L = _lib.lib()
+        self.dimx, self.dimy, self.rank, self.nranks = int(dimx), int(dimy), rank, nranks
+        self.row_begin, self.row_end = slab_bounds(dimy, rank, nranks)
+        h = C.c_void_p()
+        uid = None
+        n = 0
+        if unique_id is not None:
+            uid = C.create_string_buffer(unique_id, len(unique_id))
+            n = len(unique_id)
+        st = L.of2d_slab_create(C.byref(h), self.dimx, self.dimy, float(alpha), rank, nranks,
+                                device, uid, n)
+        check(st, L.of2d_slab_last_error(None).decode())
+        self._h = h
+
+    def _chk(self, st):
+        check(st, _lib.lib().of2d_slab_last_error(self._h).decode())
+
+    def set_images(self, Iref_rows: np.ndarray, Imov_rows: np.ndarray) -> None:
+        """Rows [row_begin-1, row_end+1) (clipped) of the global images as
+        arrays of shape [dimx, rows] (column-major, x fastest)."""
+        lo, hi = halo_rows(self.dimy, self.rank, self.nranks)
+        n = self.dimx * (hi - lo)
+        r = np.ascontiguousarray(np.asarray(Iref_rows, np.float64).reshape(-1, order="F"))
+        m = np.ascontiguousarray(np.asarray(Imov_rows, np.float64).reshape(-1, order="F"))
+        if r.size != n or m.size != n:
+            raise ValueError(f"expected {n} values (rows {lo}..{hi})")
+        self._chk(_lib.lib().of2d_slab_set_images(self._h, r, m))
+
+    def run(self, niter: int, fixed_iters: bool = False) -> int:
+        done = C.c_int(0)
+        self._chk(_lib.lib().of2d_slab_run(self._h, int(niter), int(bool(fixed_iters)),
+                                           C.byref(done)))
+        return done.value
+
+    def motion(self) -> np.ndarray:
+        rows = self.row_end - self.row_begin
+        out = np.zeros(self.dimx * rows * 2, np.float64)
+        self._chk(_lib.lib().of2d_slab_get_motion(self._h, out))
+        return out.reshape((self.dimx, rows, 2), order="F")
+
+    def time_kernel(self, nlaunch: int = 50) -> float:
+        us = C.c_double(0.0)
+        self._chk(_lib.lib().of2d_slab_time_kernel(self._h, int(nlaunch), C.byref(us)))
+        return us.value
+
+    def last_run_ms(self) -> float:
+        ms = C.c_double(0.0)
+        self._chk(_lib.lib().of2d_slab_last_run_ms(self._h, C.byref(ms)))
+        return ms.value
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            _lib.lib().of2d_slab_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -1,0 +1,195 @@
+"""Horn-Schunck on the MI355X through the C-ABI, against the oracle.
+
+Bar: bit-exact motion fields and equal iteration counts (the HIP kernels keep
+the reference's fp32 operation order with -ffp-contract=off and IEEE
+division).  The Logger error is an fp64 tree sum on the GPU against the
+reference's sequential fp32 sum, so errors agree to a tolerance (stated per
+test) and iteration counts are compared on cases whose error is not within
+that tolerance of the 0.001 threshold.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, golden
+from opticalflow2d_amd import ImageRegistration, OpticalFlow2d, SlabSolver
+from opticalflow2d_amd import synthetic as S
+
+pytestmark = pytest.mark.gpu
+
+ERR_RTOL = 1e-4  # fp64 tree sum vs the reference's fp32 sequential sum (<= 256^2 px)
+
+
+def oracle_run(oracle, dims, niter, nscales, reg, params, nrefine, ref, mov, verbose=0,
+               fixed=False):
+    r = oracle.Registration(dims, niter, nscales, reg, params, nrefine, verbose,
+                            fixed_iters=fixed)
+    r.register(ref, mov)
+    out = dict(motion=r.motion(), warped=r.warp(mov), iters=r.iterations(),
+               errs=r.last_errors())
+    r.close()
+    return out
+
+
+def test_config1_gateway_call_sequence(gpu, oracle):
+    """BASELINE config 1 through the MEX-equivalent gateway, in the order of
+    test_opticalflow2d.m:42-59: init -> register -> get -> warp -> close."""
+    ka = json.load(open(os.path.join(GOLDEN, "reference_known_answers.json")))["hs_square256"]
+    ref, mov = S.translated_square(256)
+    OpticalFlow2d([256, 256], [200], 0, 0, [0.1], 1, 1, 0)
+    try:
+        OpticalFlow2d(ref, mov)
+        motion = OpticalFlow2d(nargout=1)
+        warped = OpticalFlow2d(mov, nargout=1)
+    finally:
+        OpticalFlow2d()
+    assert motion.shape == (256, 256, 2) and warped.shape == (256, 256)
+    o = oracle_run(oracle, (256, 256), [200], 0, 0, [0.1], 1, ref, mov)
+    assert np.array_equal(motion, o["motion"])
+    assert np.array_equal(warped, o["warped"])
+    run = ka["runs"][0]
+    assert round(float(motion.sum()), 6) == run["sum_motion"]
+    assert round(float(np.abs(motion).max()), 6) == run["max_abs_motion"]
+
+
+def test_early_exit_iteration_count(gpu, oracle):
+    ref, mov = S.translated_square(256)
+    with ImageRegistration((256, 256), [1000], 0, 0, [0.1]) as r:
+        r.register(ref, mov)
+        assert r.iterations() == [490]  # reference_known_answers.json
+        m = r.motion()
+        errs = r.last_errors()
+    o = oracle_run(oracle, (256, 256), [1000], 0, 0, [0.1], 1, ref, mov)
+    assert np.array_equal(m, o["motion"])
+    np.testing.assert_allclose(errs, o["errs"], rtol=ERR_RTOL, atol=1e-7)
+
+
+@pytest.mark.parametrize("chunk", [1, 7, 32])
+def test_chunked_speculation_is_exact(gpu, oracle, chunk):
+    """The break replay (registration.cpp loop_hs) lands on the same iterate
+    whatever the chunk size."""
+    ref, mov = S.translated_square(128)
+    with ImageRegistration((128, 128), [1000], 0, 0, [0.1], chunk=chunk) as r:
+        r.register(ref, mov)
+        m, it = r.motion(), r.iterations()
+    o = oracle_run(oracle, (128, 128), [1000], 0, 0, [0.1], 1, ref, mov)
+    assert it == o["iters"]
+    assert np.array_equal(m, o["motion"])
+
+
+@pytest.mark.parametrize("dims", [(37, 23), (129, 65), (255, 130), (64, 300), (3, 3)])
+def test_ragged_sizes(gpu, oracle, dims):
+    nx, ny = dims
+    rng = np.random.default_rng(nx * 1000 + ny)
+    ref = rng.random((nx, ny))
+    mov = np.roll(ref, 1, axis=0) * 0.9 + 0.05
+    with ImageRegistration(dims, [25], 0, 0, [0.3], fixed_iters=1) as r:
+        r.register(ref, mov)
+        m = r.motion()
+        w = r.warp(mov)
+    o = oracle_run(oracle, dims, [25], 0, 0, [0.3], 1, ref, mov, fixed=True)
+    assert np.array_equal(m, o["motion"])
+    assert np.array_equal(w, o["warped"])
+
+
+def test_pyramid_and_refine_fixture(gpu):
+    g = golden("oracle_paths.npz")
+    for name, niter, nscales, params, nrefine in [("hs_square64", [60], 0, [0.1], 1),
+                                                  ("hs_texture64_pyr", [40, 30], 1, [0.2], 2)]:
+        with ImageRegistration((64, 64), niter, nscales, 0, params, nrefine) as r:
+            r.register(g[f"{name}/ref"], g[f"{name}/mov"])
+            assert r.iterations() == g[f"{name}/iters"].tolist(), name
+            assert np.array_equal(r.motion(), g[f"{name}/motion"]), name
+            assert np.array_equal(r.warp(g[f"{name}/mov"]), g[f"{name}/warped"]), name
+
+
+def test_texture_three_levels_two_refines(gpu, oracle):
+    ref, mov = S.texture_pair(200, seed=11, ny=136)
+    args = ((200, 136), [30, 25, 20], 2, 0, [0.15], 2)
+    with ImageRegistration(*args) as r:
+        r.register(ref, mov)
+        m, it = r.motion(), r.iterations()
+    o = oracle_run(oracle, *args, ref, mov)
+    assert it == o["iters"]
+    assert np.array_equal(m, o["motion"])
+
+
+def test_warm_start_second_register_call(gpu, oracle):
+    """The singleton keeps motion[] across register calls
+    (ImageRegistration.cpp:133-156): a second call continues from the first."""
+    ref, mov = S.texture_pair(96, seed=5)
+    args = ((96, 96), [20, 15], 1, 0, [0.2], 1)
+    with ImageRegistration(*args) as r:
+        r.register(ref, mov)
+        r.register(ref, mov)
+        m = r.motion()
+    o = oracle.Registration(*args, 0)
+    o.register(ref, mov)
+    o.register(ref, mov)
+    assert np.array_equal(m, o.motion())
+    o.close()
+
+
+def test_verbose_logger_lines(gpu, oracle):
+    ref, mov = S.translated_square(64)
+    gpu.clear()
+    with ImageRegistration((64, 64), [40], 0, 0, [0.1], 1, 1) as r:
+        r.register(ref, mov)
+    text = "".join(gpu)
+    lines = [l for l in text.splitlines() if l.startswith("Iteration:")]
+    assert len(lines) == 40
+    L = oracle.lib()
+    L.oracle_clear_output()
+    oracle_run(oracle, (64, 64), [40], 0, 0, [0.1], 1, ref, mov, verbose=1)
+    olines = [l for l in L.oracle_captured_output().decode().splitlines()
+              if l.startswith("Iteration:")]
+    assert [l.split("\t")[0] for l in lines] == [l.split("\t")[0] for l in olines]
+    for a, b in zip(lines, olines):
+        assert abs(float(a.split(":")[-1]) - float(b.split(":")[-1])) <= 1.01e-4
+
+
+def test_divide_by_zero_raises(gpu):
+    from opticalflow2d_amd import Of2dError
+    flat = np.zeros((32, 32))
+    with ImageRegistration((32, 32), [5], 0, 0, [0.0]) as r:
+        with pytest.raises(Of2dError, match="Divide by zero exception"):
+            r.register(flat, flat)
+
+
+# ---------------------------------------------------------------- slab path
+def test_slab_single_rank_equals_registration(gpu):
+    ref, mov = S.texture_pair(256, seed=2)
+    with ImageRegistration((256, 256), [300], 0, 0, [0.1]) as r:
+        r.register(ref, mov)
+        m, it = r.motion(), r.iterations()
+    s = SlabSolver(256, 256, 0.1)
+    s.set_images(ref, mov)
+    assert s.run(300) == it[0]
+    assert np.array_equal(s.motion(), m)
+    s.close()
+
+
+def test_slab_full_size_4096_bitwise(gpu, oracle):
+    """BASELINE config 2 grid (4096^2): a few Jacobi iterations bit for bit
+    against the oracle's HS loop on the same gradients."""
+    n, iters = 4096, 4
+    ref, mov = S.texture_pair(n, seed=0)
+    s = SlabSolver(n, n, 0.1)
+    s.set_images(ref, mov)
+    assert s.run(iters, fixed_iters=True) == iters
+    m = s.motion()
+    s.close()
+    L = oracle.lib()
+    I = np.ascontiguousarray(mov.reshape(-1, order="F").astype(np.float32))
+    Ir = np.ascontiguousarray(ref.reshape(-1, order="F").astype(np.float32))
+    dI = np.zeros(2 * n * n, np.float32)
+    It = np.zeros(n * n, np.float32)
+    L.oracle_spatial_derivative(I, n, n, dI)
+    L.oracle_temporal_derivative(Ir, I, n * n, It)
+    u = np.zeros(2 * n * n, np.float32)
+    errs = np.zeros(iters, np.float32)
+    assert L.oracle_hs_loop(u, dI, It, n, n, 0.1, iters, 1, errs) == iters
+    got = np.stack([m[:, :, 0].reshape(-1, order="F"), m[:, :, 1].reshape(-1, order="F")], 1)
+    assert np.array_equal(got.astype(np.float32).reshape(-1), u)
