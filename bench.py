@@ -178,7 +178,7 @@ def main():
             },
             "roofline": {
                 "bound": "hbm",
-                "kernel": "hs_jacobi_kernel",
+                "kernel": "of2d::hs::jacobi_kernel<32,2,4,true,true,false>",
                 "achieved": round(achieved, 1),
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",

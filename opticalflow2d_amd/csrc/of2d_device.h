@@ -39,10 +39,11 @@ struct DeviceError : std::runtime_error {
 constexpr unsigned kStatusDivZero = 1u;
 
 // ---------------------------------------------------------------- HS Jacobi
-// Each wave marches kHsRows j-lines of a 128-px strip (2 px per lane); a block
-// is 4 waves stacked in y.
-constexpr int kHsRows = 16;
-constexpr int kHsStrip = 128;
+// Each wave marches kHsRows j-lines of a kHsStrip-px strip (kHsPxl px per
+// lane); a block is kHsWaves waves stacked in y (hs_jacobi_impl.h).
+constexpr int kHsRows = 32;
+constexpr int kHsPxl = 2;
+constexpr int kHsStrip = 64 * kHsPxl;
 constexpr int kHsWaves = 4;
 inline dim3 hs_grid(int P, int nrows) {
     return dim3(P / kHsStrip, (nrows + kHsRows * kHsWaves - 1) / (kHsRows * kHsWaves));

@@ -33,7 +33,7 @@ def test_library_is_gfx950_code_object():
     path = os.path.join(ROOT, "opticalflow2d_amd", "libof2d.so")
     blob = open(path, "rb").read()
     assert b"gfx950" in blob
-    assert b"hs_jacobi_kernel" in blob
+    assert b"jacobi_kernel" in blob
 
 
 def test_solver_options_values():

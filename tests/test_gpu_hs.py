@@ -191,5 +191,8 @@ def test_slab_full_size_4096_bitwise(gpu, oracle):
     u = np.zeros(2 * n * n, np.float32)
     errs = np.zeros(iters, np.float32)
     assert L.oracle_hs_loop(u, dI, It, n, n, 0.1, iters, 1, errs) == iters
+    # end of the refine: motion (zero) -> accumulate(motion_est) (ImageRegistrationOpticalFlow.cpp:138)
+    motion = np.zeros_like(u)
+    L.oracle_accumulate(motion, u, n, n)
     got = np.stack([m[:, :, 0].reshape(-1, order="F"), m[:, :, 1].reshape(-1, order="F")], 1)
-    assert np.array_equal(got.astype(np.float32).reshape(-1), u)
+    assert np.array_equal(got.astype(np.float32).reshape(-1), motion)

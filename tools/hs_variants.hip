@@ -1,0 +1,181 @@
+// hs_variants.hip — tuning harness for the HS Jacobi kernel (not part of the
+// product).  Times template variants of of2d::hs::jacobi_kernel on a 4096^2
+// grid with HIP events, checks every variant bit-identical to the first, and
+// times a copy probe with the same traffic mix (read 8+8+4 B, write 8 B per
+// px, no stencil) as the achievable ceiling.
+//   hipcc --offload-arch=gfx950 -O3 -ffp-contract=off -std=c++17 \
+//         -I opticalflow2d_amd/csrc tools/hs_variants.hip -o tools/hs_variants
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#include "hs_jacobi_impl.h"
+
+using namespace of2d;
+
+#define CK(x)                                                                   \
+    do {                                                                        \
+        hipError_t e = (x);                                                     \
+        if (e != hipSuccess) {                                                  \
+            fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e)); \
+            exit(1);                                                            \
+        }                                                                       \
+    } while (0)
+
+__global__ void probe_kernel(const float4 *__restrict__ u, const float4 *__restrict__ g,
+                             const float2 *__restrict__ t, float4 *__restrict__ o, long n2) {
+    long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    const long stride = (long)gridDim.x * blockDim.x;
+    for (; i < n2; i += stride) {
+        const float4 a = u[i], b = g[i];
+        const float2 c = t[i];
+        o[i] = make_float4(a.x + b.x * c.x, a.y + b.y, a.z + b.z * c.y, a.w + b.w);
+    }
+}
+
+struct Bufs {
+    float2 *u0, *u1, *dI;
+    float *It;
+    double *partial;
+    unsigned *status;
+    int P, dimx, dimy;
+};
+
+template <int ROWS, int PXL, int WAVES, bool NTL, bool NTS, bool NTG = NTL>
+float run(const Bufs &b, int iters, float2 *out_host, const char *name, double bytes) {
+    dim3 g = hs::grid_for<ROWS, PXL, WAVES>(b.P, b.dimy);
+    auto k = hs::jacobi_kernel<ROWS, PXL, WAVES, NTL, NTS, NTG>;
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    CK(hipMemset(b.u0 - b.P, 0, sizeof(float2) * (size_t)b.P * (b.dimy + 2)));
+    // warm-up
+    for (int it = 0; it < 3; it++)
+        hipLaunchKernelGGL(k, g, dim3(64 * WAVES), 0, 0, (it & 1) ? b.u1 : b.u0,
+                           (it & 1) ? b.u0 : b.u1, b.dI, b.It, b.P, b.dimx, b.dimy, 0, b.dimy,
+                           0.01f, b.partial, b.status);
+    CK(hipEventRecord(e0, 0));
+    for (int it = 0; it < iters; it++)
+        hipLaunchKernelGGL(k, g, dim3(64 * WAVES), 0, 0, (it & 1) ? b.u1 : b.u0,
+                           (it & 1) ? b.u0 : b.u1, b.dI, b.It, b.P, b.dimx, b.dimy, 0, b.dimy,
+                           0.01f, b.partial, b.status);
+    CK(hipEventRecord(e1, 0));
+    CK(hipEventSynchronize(e1));
+    float ms;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    const double us = 1000.0 * ms / iters;
+    // deterministic check run: 5 iterations from zero
+    CK(hipMemset(b.u0 - b.P, 0, sizeof(float2) * (size_t)b.P * (b.dimy + 2)));
+    CK(hipMemset(b.u1 - b.P, 0, sizeof(float2) * (size_t)b.P * (b.dimy + 2)));
+    for (int it = 0; it < 5; it++)
+        hipLaunchKernelGGL(k, g, dim3(64 * WAVES), 0, 0, (it & 1) ? b.u1 : b.u0,
+                           (it & 1) ? b.u0 : b.u1, b.dI, b.It, b.P, b.dimx, b.dimy, 0, b.dimy,
+                           0.01f, b.partial, b.status);
+    CK(hipMemcpy(out_host, b.u1, sizeof(float2) * (size_t)b.P * b.dimy, hipMemcpyDeviceToHost));
+    printf("%-28s grid=%5ux%-4u  %8.2f us  %7.1f GB/s  %5.1f%% of 8 TB/s\n", name, g.x, g.y, us,
+           bytes / us / 1e3, bytes / us / 1e3 / 80.0);
+    return (float)us;
+}
+
+int main(int argc, char **argv) {
+    const int n = argc > 1 ? atoi(argv[1]) : 4096;
+    const int iters = argc > 2 ? atoi(argv[2]) : 200;
+    Bufs b;
+    b.dimx = b.dimy = n;
+    b.P = (n + 255) / 256 * 256;
+    const size_t rows = (size_t)n + 2;
+    float2 *base0, *base1, *based;
+    float *baset;
+    CK(hipMalloc(&base0, sizeof(float2) * b.P * rows + 4096));
+    CK(hipMalloc(&base1, sizeof(float2) * b.P * rows + 4096));
+    CK(hipMalloc(&based, sizeof(float2) * b.P * rows + 4096));
+    CK(hipMalloc(&baset, sizeof(float) * b.P * rows + 4096));
+    b.u0 = base0 + b.P;
+    b.u1 = base1 + b.P;
+    b.dI = based + b.P;
+    b.It = baset + b.P;
+    CK(hipMalloc(&b.partial, sizeof(double) * 2 * 65536));
+    CK(hipMalloc(&b.status, 64));
+    std::vector<float> h((size_t)b.P * rows * 2);
+    srand(1);
+    for (auto &v : h) v = (rand() / (float)RAND_MAX) - 0.5f;
+    CK(hipMemcpy(based, h.data(), sizeof(float2) * b.P * rows, hipMemcpyHostToDevice));
+    CK(hipMemcpy(baset, h.data(), sizeof(float) * b.P * rows, hipMemcpyHostToDevice));
+    const double bytes = 28.0 * n * n;
+    printf("grid %d^2, %d launches per variant, %.1f MB per launch\n", n, iters, bytes / 1e6);
+
+    // probe: same traffic mix, no stencil
+    {
+        const long n2 = (long)b.P * n / 2;
+        hipEvent_t e0, e1;
+        CK(hipEventCreate(&e0));
+        CK(hipEventCreate(&e1));
+        for (int grid : {2048, 4096, 8192}) {
+            hipLaunchKernelGGL(probe_kernel, dim3(grid), dim3(256), 0, 0, (const float4 *)b.u0,
+                               (const float4 *)b.dI, (const float2 *)b.It, (float4 *)b.u1, n2);
+            CK(hipEventRecord(e0, 0));
+            for (int it = 0; it < iters; it++)
+                hipLaunchKernelGGL(probe_kernel, dim3(grid), dim3(256), 0, 0,
+                                   (const float4 *)((it & 1) ? b.u1 : b.u0), (const float4 *)b.dI,
+                                   (const float2 *)b.It, (float4 *)((it & 1) ? b.u0 : b.u1), n2);
+            CK(hipEventRecord(e1, 0));
+            CK(hipEventSynchronize(e1));
+            float ms;
+            CK(hipEventElapsedTime(&ms, e0, e1));
+            const double us = 1000.0 * ms / iters;
+            printf("probe grid=%-6d                   %8.2f us  %7.1f GB/s  %5.1f%% of 8 TB/s\n",
+                   grid, us, bytes / us / 1e3, bytes / us / 1e3 / 80.0);
+        }
+    }
+
+    const size_t cnt = (size_t)b.P * n;
+    std::vector<float2> ref(cnt), got(cnt);
+    int bad = 0;
+#define V(R, X, W, NL, NS)                                                                 \
+    do {                                                                                   \
+        run<R, X, W, NL, NS>(b, iters, got.data(), #R "r " #X "px " #W "w nl" #NL " ns" #NS, \
+                             bytes);                                                      \
+        if (first) {                                                                       \
+            ref = got;                                                                     \
+            first = false;                                                                 \
+        } else if (memcmp(ref.data(), got.data(), cnt * sizeof(float2)) != 0) {            \
+            printf("   ^^^ MISMATCH\n");                                                   \
+            bad++;                                                                         \
+        }                                                                                  \
+    } while (0)
+    bool first = true;
+#define V3(R, X, W, NL, NS, NG)                                                            \
+    do {                                                                                   \
+        run<R, X, W, NL, NS, NG>(b, iters, got.data(),                                     \
+                                 #R "r " #X "px " #W "w u" #NL " st" #NS " g" #NG, bytes); \
+        if (first) {                                                                       \
+            ref = got;                                                                     \
+            first = false;                                                                 \
+        } else if (memcmp(ref.data(), got.data(), cnt * sizeof(float2)) != 0) {            \
+            printf("   ^^^ MISMATCH\n");                                                  \
+            bad++;                                                                         \
+        }                                                                                  \
+    } while (0)
+    const bool product_only = argc > 3 && strcmp(argv[3], "product") == 0;
+    V3(32, 2, 4, true, true, false);  // the product configuration (hs_kernels.hip)
+    if (product_only) return 0;
+    V3(32, 2, 4, false, true, false);
+    V3(24, 2, 4, false, true, false);
+    V3(40, 2, 4, false, true, false);
+    V3(48, 2, 4, false, true, false);
+    V3(32, 2, 2, false, true, false);
+    V3(32, 2, 8, false, true, false);
+    V3(24, 4, 2, false, true, false);
+    V3(48, 4, 2, false, true, false);
+    V3(32, 2, 4, true, true, false);
+    V3(32, 2, 4, false, true, true);
+    V3(32, 2, 4, true, false, false);
+    V3(32, 4, 4, true, true, false);
+    V3(64, 2, 2, false, true, false);
+    V3(32, 2, 1, false, true, false);
+    printf("%s\n", bad ? "SOME VARIANTS MISMATCH" : "all variants bit-identical");
+    return bad ? 1 : 0;
+}

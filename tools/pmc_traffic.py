@@ -1,0 +1,68 @@
+#!/usr/bin/env python3
+"""HBM traffic of the HS Jacobi kernel from rocprofv3 PMC counters.
+
+Two separate --pmc passes over `tools/hs_variants 4096 N product` (FETCH_SIZE,
+then WRITE_SIZE; they do not fit one pass on gfx950).  The probe kernel in the
+same binary moves a KNOWN byte count with the same access mix (16-B u and dI
+loads, 8-B It loads, 16-B stores), so it calibrates the counters for this
+pattern (MI355X_MICROARCH.md: FETCH_SIZE under-reports wide streaming reads
+by 2x on gfx950; other widths are uncalibrated).  Writes
+profiles/hs_traffic.json with the corrected bytes per launch.
+usage: pmc_traffic.py <fetch_counter_collection.csv> <write_counter_collection.csv> [n]
+"""
+import csv
+import json
+import os
+import sys
+from collections import defaultdict
+
+
+def per_kernel(path, counter):
+    acc = defaultdict(list)
+    with open(path) as f:
+        for row in csv.DictReader(f):
+            if row.get("Counter_Name") != counter:
+                continue
+            acc[row["Kernel_Name"]].append(float(row["Counter_Value"]))
+    return {k: sum(v) / len(v) for k, v in acc.items()}
+
+
+def main():
+    fetch_csv, write_csv = sys.argv[1], sys.argv[2]
+    n = int(sys.argv[3]) if len(sys.argv) > 3 else 4096
+    P = (n + 255) // 256 * 256
+    fetch = per_kernel(fetch_csv, "FETCH_SIZE")  # KB
+    write = per_kernel(write_csv, "WRITE_SIZE")  # KB
+    probe = [k for k in fetch if "probe_kernel" in k][0]
+    jac = [k for k in fetch if "jacobi_kernel" in k][0]
+    px = P * n  # the probe sweeps the pitched rows
+    probe_read_true = 20.0 * px
+    probe_write_true = 8.0 * px
+    fcal = probe_read_true / (fetch[probe] * 1024.0)
+    wcal = probe_write_true / (write[probe] * 1024.0)
+    rd = fetch[jac] * 1024.0 * fcal
+    wr = write[jac] * 1024.0 * wcal
+    alg = 28.0 * n * n
+    out = {
+        "kernel": jac,
+        "grid": [n, n],
+        "fetch_raw_bytes": fetch[jac] * 1024.0,
+        "write_raw_bytes": write[jac] * 1024.0,
+        "fetch_calibration": fcal,
+        "write_calibration": wcal,
+        "read_bytes_per_launch": rd,
+        "write_bytes_per_launch": wr,
+        "bytes_per_launch": rd + wr,
+        "algorithmic_bytes_per_launch": alg,
+        "traffic_over_algorithmic": (rd + wr) / alg,
+        "source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes) on tools/hs_variants, "
+                  "calibrated on the probe kernel's known bytes",
+    }
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    with open(os.path.join(root, "profiles", "hs_traffic.json"), "w") as f:
+        json.dump(out, f, indent=1)
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
