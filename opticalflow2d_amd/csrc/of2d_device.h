@@ -37,6 +37,7 @@ struct DeviceError : std::runtime_error {
 
 // status bits written by kernels (one word per context, zeroed per call)
 constexpr unsigned kStatusDivZero = 1u;
+constexpr unsigned kStatusExpBound = 2u;  // scaling-and-squaring count above the host bound
 
 // ---------------------------------------------------------------- HS Jacobi
 // Each wave marches kHsRows j-lines of a kHsStrip-px strip (kHsPxl px per
@@ -91,5 +92,23 @@ void launch_compose_zero(const float2 *v, float2 *out, int dimx, int nrows, int 
                          int dimy, hipStream_t st);
 void launch_add_motion(const float2 *a, const float2 *b, float2 *out, int dimx, int dimy, int P,
                        hipStream_t st);
+
+// ---------------------------------------------------------------- Demons
+void launch_demons_force(const float *Iref, const float *Imov, const float2 *u, float2 *corr,
+                         int dimx, int dimy, int P, float sigma_isq, float sigma_xsq,
+                         unsigned *status, hipStream_t st);
+dim3 conv_grid(int dimx, int dimy);
+int conv_nblocks(int dimx, int dimy);
+// mode 0 Composition, 1 Addition, 2 no update, 3 store the smoothed corr only
+void launch_smooth_compose(const float2 *corr, const float2 *u, float2 *out, int dimx, int dimy,
+                           int P, const float *kf, const double *kd, int kw, double wfull,
+                           int mode, hipStream_t st);
+void launch_smooth_norm(const float2 *umid, const float2 *prev, float2 *out, int dimx, int dimy,
+                        int P, const float *kf, const double *kd, int kw, double wfull,
+                        double *partial, hipStream_t st);
+// Motion::exp (Motion.cpp:253-277) on f; *result is f or scratch
+void launch_motion_exp(float2 *f, float2 *scratch, int dimx, int dimy, int P, int nsq_max,
+                       float *d_part, int nparts, int *d_nsq, float *d_maxabs, unsigned *status,
+                       float2 **result, hipStream_t st);
 
 }  // namespace of2d

@@ -11,6 +11,7 @@
 #pragma once
 
 #include <cstdarg>
+#include <functional>
 #include <memory>
 #include <string>
 #include <vector>
@@ -19,6 +20,7 @@
 
 namespace of2d {
 
+struct DemonsKernels;
 void print(const char *fmt, ...) __attribute__((format(printf, 1, 2)));
 
 // ------------------------------------------------------------ device buffer
@@ -105,7 +107,10 @@ class Registration {
     int dimx() const { return dimx_; }
     int dimy() const { return dimy_; }
 
+    using StepFn = std::function<void(const float2 *src, float2 *dst, double *partial)>;
+
    private:
+    int run_chunked(Level &L, int niter, int nb, const StepFn &step, int &final_buf);
     void ensure_device();
     void estimate_level(int s);
     int loop_hs(Level &L, int niter, float alpha, int &final_buf);
@@ -137,6 +142,7 @@ class Registration {
     std::vector<float> last_err_;
     // Demons kernels (Kernel::set_gaussian, src/Kernel.cpp:45-73)
     std::vector<double> kdiff_, kfluid_;
+    std::shared_ptr<DemonsKernels> demons_k_;
 };
 
 // Validation of nparams per regularisation (ImageRegistrationOpticalFlow.cpp:8-12,

@@ -143,8 +143,10 @@ Registration::~Registration() {
 void Registration::set_option(const std::string &key, double v) {
     if (key == "fixed_iters")
         fixed_ = v != 0;
-    else if (key == "chunk")
+    else if (key == "chunk") {
+        if (ready_) throw std::invalid_argument("option 'chunk' must be set before first use");
         chunk_ = std::max(1, (int)v);
+    }
     else if (key == "device") {
         if (ready_) throw std::invalid_argument("option 'device' must be set before first use");
         device_ = (int)v;
@@ -181,7 +183,7 @@ void Registration::ensure_device() {
     OF2D_HIP(hipMalloc(&d_sums_, sizeof(double) * 4 * (size_t)std::max(chunk_, 64)));
     OF2D_HIP(hipMalloc(&d_status_, 64 * sizeof(unsigned)));
     OF2D_HIP(hipMemset(d_status_, 0, 64 * sizeof(unsigned)));
-    OF2D_HIP(hipMalloc(&d_scalar_, 64 * sizeof(float)));
+    OF2D_HIP(hipMalloc(&d_scalar_, (16 + 256) * sizeof(float)));
     hs_.ensure(std::max(chunk_, 64));
     ready_ = true;
 }
@@ -260,46 +262,55 @@ void Registration::estimate_level(int s) {
     }
 }
 
-// HS iteration loop (ImageRegistrationOpticalFlow.cpp:117-135) with fused Logger
-int Registration::loop_hs(Level &L, int niter, float alpha, int &final_buf) {
-    const float alphasq = alpha * alpha;  // OpticalFlowDiffusion.cpp:70
-    const int nb = hs_nblocks(L.P, L.dy);
+// Speculative chunked iteration loop shared by every solver whose iteration
+// reads motion_est from one buffer and writes the next iterate to another
+// (HS, Demons, Elastic, Curvature).  step(src, dst, partial) enqueues one
+// get_update plus the fused Logger partials (nb blocks x {diff, prev}).
+int Registration::run_chunked(Level &L, int niter, int nb, const StepFn &step, int &final_buf) {
     const double npx = (double)L.dx * L.dy;
     last_err_.clear();
     int a = 0, k0 = 0;
-    auto seq_src = [](int a_, int t) { return t == 0 ? a_ : (t % 2 == 1 ? (a_ + 1) % 3 : (a_ + 2) % 3); };
-    auto seq_dst = [](int a_, int t) { return t % 2 == 0 ? (a_ + 1) % 3 : (a_ + 2) % 3; };
+    auto src_of = [](int a_, int t) { return t == 0 ? a_ : (t % 2 == 1 ? (a_ + 1) % 3 : (a_ + 2) % 3); };
+    auto dst_of = [](int a_, int t) { return t % 2 == 0 ? (a_ + 1) % 3 : (a_ + 2) % 3; };
     while (k0 < niter) {
         const int C = std::min(chunk_, niter - k0);
         for (int t = 0; t < C; t++)
-            launch_hs_jacobi(L.est[seq_src(a, t)].p, L.est[seq_dst(a, t)].p, L.dI.p, L.It.p, L.P,
-                             L.dx, L.dy, 0, L.dy, alphasq, d_partial_ + (size_t)t * nb * 2,
-                             d_status_, st_);
+            step(L.est[src_of(a, t)].p, L.est[dst_of(a, t)].p, d_partial_ + (size_t)t * nb * 2);
         launch_reduce_partials(d_partial_, nb, C, d_sums_, st_);
         OF2D_HIP(hipMemcpyAsync(hs_.sums, d_sums_, sizeof(double) * 2 * C, hipMemcpyDeviceToHost,
                                 st_));
-        check_status();  // synchronises the stream
+        check_status();  // synchronises the stream; throws the reference's runtime_error
         for (int t = 0; t < C; t++) {
             const int k = k0 + t;
             const float err = logger_error(hs_.sums[2 * t], hs_.sums[2 * t + 1], npx);
             last_err_.push_back(err);
             if (verbose_) print("Iteration: %d\tError:%.4f\n", k, (double)err);
-            if (!fixed_ && err < 0.001f && k > 1) {
-                if (t + 2 <= C - 1) {  // dst(t) was overwritten by iteration t+2: replay
+            if (!fixed_ && err < 0.001f && k > 1) {  // ImageRegistrationOpticalFlow.cpp:131-134
+                if (t + 2 <= C - 1)  // dst(t) was overwritten by iteration t+2: replay from a
                     for (int r = 0; r <= t; r++)
-                        launch_hs_jacobi(L.est[seq_src(a, r)].p, L.est[seq_dst(a, r)].p, L.dI.p,
-                                         L.It.p, L.P, L.dx, L.dy, 0, L.dy, alphasq, d_partial_,
-                                         d_status_, st_);
-                }
-                final_buf = seq_dst(a, t);
+                        step(L.est[src_of(a, r)].p, L.est[dst_of(a, r)].p, d_partial_);
+                final_buf = dst_of(a, t);
                 return k + 1;
             }
         }
-        a = seq_dst(a, C - 1);
+        a = dst_of(a, C - 1);
         k0 += C;
     }
     final_buf = a;
     return niter;
+}
+
+// HS iteration loop (ImageRegistrationOpticalFlow.cpp:117-135) with fused Logger
+int Registration::loop_hs(Level &L, int niter, float alpha, int &final_buf) {
+    const float alphasq = alpha * alpha;  // OpticalFlowDiffusion.cpp:70
+    const int nb = hs_nblocks(L.P, L.dy);
+    return run_chunked(
+        L, niter, nb,
+        [&](const float2 *src, float2 *dst, double *partial) {
+            launch_hs_jacobi(src, dst, L.dI.p, L.It.p, L.P, L.dx, L.dy, 0, L.dy, alphasq, partial,
+                             d_status_, st_);
+        },
+        final_buf);
 }
 
 // WrapperOpticalFlow2d.cpp:105-117 -> Motion::copy_motion_to_input
