@@ -38,6 +38,7 @@ struct DeviceError : std::runtime_error {
 // status bits written by kernels (one word per context, zeroed per call)
 constexpr unsigned kStatusDivZero = 1u;
 constexpr unsigned kStatusExpBound = 2u;  // scaling-and-squaring count above the host bound
+constexpr unsigned kStatusSpinTimeout = 4u;  // a bounded inter-workgroup wait gave up
 
 // ---------------------------------------------------------------- HS Jacobi
 // Each wave marches kHsRows j-lines of a kHsStrip-px strip (kHsPxl px per
@@ -110,5 +111,28 @@ void launch_smooth_norm(const float2 *umid, const float2 *prev, float2 *out, int
 void launch_motion_exp(float2 *f, float2 *scratch, int dimx, int dimy, int P, int nsq_max,
                        float *d_part, int nparts, int *d_nsq, float *d_maxabs, unsigned *status,
                        float2 **result, hipStream_t st);
+
+// ---------------------------------------------------------------- Fluid / Elastic
+int sor_nstrips(int dimx);
+// in-place Gauss-Seidel SOR sweep (OpticalFlowFluid.cpp:7-41), wavefront-exact.
+// fused: b = force(u_or_b = motion, dI, It) per pixel; else u_or_b is b.
+// H: nstrips*dimy*2 granules (zeroed once); epoch: > every earlier epoch on H;
+// ticket: per-H counter, a multiple of nstrips before the launch.
+void launch_sor(float2 *v, const float2 *u_or_b, const float2 *dI, const float *It, bool fused,
+                int dimx, int dimy, int P, float mu, float lambda, float omega,
+                unsigned long long *H, unsigned epoch, unsigned *ticket, unsigned *status,
+                hipStream_t st);
+void launch_force(const float2 *u, const float2 *dI, const float *It, float2 *f, int dimx,
+                  int dimy, int P, hipStream_t st);
+int increment_nblocks(int dimx, int dimy);
+// R and scal[0] = maxabs(R), scal[1] = 0.65f / maxabs
+void launch_increment(const float2 *u, const float2 *vel, float2 *R, int dimx, int dimy, int P,
+                      float *part, float *scal, hipStream_t st);
+void launch_integrate_logger(float2 *u, const float2 *R, float2 *prev, const float *scal,
+                             int dimx, int dimy, int P, double *partial, hipStream_t st);
+void launch_logger(const float2 *u, float2 *prev, int dimx, int dimy, int P, double *partial,
+                   hipStream_t st);
+void launch_jacobian_min(const float2 *u, int dimx, int dimy, int P, float *part, float *out,
+                         hipStream_t st);
 
 }  // namespace of2d

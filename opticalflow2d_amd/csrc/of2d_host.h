@@ -66,6 +66,31 @@ struct Field {
     size_t bytes() const { return count * sizeof(T); }
 };
 
+// A plain device array (no ghost lines)
+template <class T>
+struct DevArray {
+    T *p = nullptr;
+    size_t n = 0;
+    DevArray() = default;
+    DevArray(const DevArray &) = delete;
+    DevArray &operator=(const DevArray &) = delete;
+    DevArray(DevArray &&o) noexcept { *this = std::move(o); }
+    DevArray &operator=(DevArray &&o) noexcept {
+        std::swap(p, o.p);
+        std::swap(n, o.n);
+        return *this;
+    }
+    ~DevArray() {
+        if (p) (void)hipFree(p);
+    }
+    void alloc(size_t count) {
+        if (p) (void)hipFree(p);
+        n = count;
+        OF2D_HIP(hipMalloc(&p, sizeof(T) * (count ? count : 1)));
+        OF2D_HIP(hipMemset(p, 0, sizeof(T) * (count ? count : 1)));
+    }
+};
+
 // Pinned host scratch for the per-chunk read-back
 struct HostScratch {
     double *sums = nullptr;
@@ -89,6 +114,9 @@ struct Level {
     Field<float2> est[3];
     Field<float2> force, velocity, increment, corr, tmp;
     Field<double> rhs;  // curvature spectral buffers (2 components)
+    DevArray<unsigned long long> sorH;  // SOR strip hand-off granules
+    DevArray<unsigned> sorTicket;       // SOR strip ticket (multiple of nstrips between sweeps)
+    DevArray<float> part;               // per-block float partials (max / min reductions)
     float2 *cur_motion() { return motion[mcur].p; }
 };
 
@@ -143,6 +171,7 @@ class Registration {
     // Demons kernels (Kernel::set_gaussian, src/Kernel.cpp:45-73)
     std::vector<double> kdiff_, kfluid_;
     std::shared_ptr<DemonsKernels> demons_k_;
+    unsigned epoch_ = 0;  // SOR hand-off epoch, strictly increasing per sweep
 };
 
 // Validation of nparams per regularisation (ImageRegistrationOpticalFlow.cpp:8-12,

@@ -210,10 +210,13 @@ void Registration::set_images(const double *ref, const double *mov) {
 void Registration::check_status() {
     OF2D_HIP(hipMemcpyAsync(hs_.status, d_status_, sizeof(unsigned), hipMemcpyDeviceToHost, st_));
     OF2D_HIP(hipStreamSynchronize(st_));
-    if (hs_.status[0] & kStatusDivZero) {
-        OF2D_HIP(hipMemsetAsync(d_status_, 0, sizeof(unsigned), st_));
-        throw std::runtime_error("Divide by zero exception");
-    }
+    const unsigned st = hs_.status[0];
+    if (st) OF2D_HIP(hipMemsetAsync(d_status_, 0, sizeof(unsigned), st_));
+    if (st & kStatusDivZero) throw std::runtime_error("Divide by zero exception");
+    if (st & kStatusSpinTimeout)
+        throw DeviceError("internal error: SOR strip hand-off timed out (results discarded)");
+    if (st & kStatusExpBound)
+        throw DeviceError("internal error: scaling-and-squaring count above its bound");
 }
 
 // ImageRegistration::estimate_motion (:133-156)

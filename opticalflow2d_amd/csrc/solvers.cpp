@@ -22,15 +22,17 @@ void alloc_level(Level &L, int reg) {
                 L.increment.alloc(L.dx, L.dy);  // u o exp(c)
             }
             break;
-        case 2:
+        case 2:  // OpticalFlow::force + Logger prev; SOR hand-off buffers
+        case 5:  // + OpticalFlowFluid velocity / increment (OpticalFlowFluid.cpp:50-51)
             L.force.alloc(L.dx, L.dy);
-            break;
-        case 5:
-            L.force.alloc(L.dx, L.dy);
-            L.velocity.alloc(L.dx, L.dy);
-            L.increment.alloc(L.dx, L.dy);
-            L.jac.alloc(L.dx, L.dy);
             L.tmp.alloc(L.dx, L.dy);
+            L.sorH.alloc((size_t)std::max(sor_nstrips(L.dx), 1) * L.dy * 2);
+            L.sorTicket.alloc(1);
+            L.part.alloc((size_t)increment_nblocks(L.dx, L.dy));
+            if (reg == 5) {
+                L.velocity.alloc(L.dx, L.dy);
+                L.increment.alloc(L.dx, L.dy);
+            }
             break;
         case 1:
             L.force.alloc(L.dx, L.dy);
@@ -42,6 +44,7 @@ void alloc_level(Level &L, int reg) {
 
 int max_partial_blocks(const Level &L, int reg) {
     if (reg == 3 || reg == 4) return conv_nblocks(L.dx, L.dy);
+    if (reg == 2 || reg == 5) return increment_nblocks(L.dx, L.dy);
     return hs_nblocks(L.P, L.dy);
 }
 
@@ -143,12 +146,110 @@ int Registration::loop_demons(Level &L, int niter, int &final_buf) {
         final_buf);
 }
 
-int Registration::loop_fluid(Level &, int) {
-    throw std::runtime_error("Fluid: not implemented yet");
+// ImageRegistrationFluid::estimate_motion_at_current_resolution loop body
+// (ImageRegistrationFluid.cpp:94-125) with OpticalFlowFluid::get_update
+// (OpticalFlowFluid.cpp:123-140).  The reference prints a line every
+// iteration and may regrid after any iteration, so this loop takes its
+// decisions per iteration: one small read-back (Logger sums, maxabs, dt,
+// min Jacobian, status) per iteration.
+int Registration::loop_fluid(Level &L, int niter) {
+    const float mu = params_[0], lambda = params_[1];
+    const float omega = params_.size() == 3 ? params_[2] : (float)0.66;  // OpticalFlowFluid.h:10
+    float2 *est = L.est[0].p;
+    float2 *prev = L.tmp.p;
+    L.tmp.zero(st_);  // Logger::prev starts at zero (Logger.cpp:13, new per refine)
+    float *scal = d_scalar_ + 8;  // [0] maxabs, [1] dt, [2] min jacobian
+    const int nb = increment_nblocks(L.dx, L.dy);
+    const double npx = (double)L.dx * L.dy;
+    last_err_.clear();
+    int iter;
+    for (iter = 0; iter < niter; iter++) {
+        launch_sor(L.velocity.p, est, L.dI.p, L.It.p, true, L.dx, L.dy, L.P, mu, lambda, omega,
+                   L.sorH.p, ++epoch_, L.sorTicket.p, d_status_, st_);
+        launch_increment(est, L.velocity.p, L.increment.p, L.dx, L.dy, L.P, L.part.p, scal, st_);
+        launch_integrate_logger(est, L.increment.p, prev, scal, L.dx, L.dy, L.P, d_partial_, st_);
+        launch_reduce_partials(d_partial_, nb, 1, d_sums_, st_);
+        launch_jacobian_min(est, L.dx, L.dy, L.P, L.part.p, scal + 2, st_);
+        OF2D_HIP(hipMemcpyAsync(hs_.sums, d_sums_, sizeof(double) * 2, hipMemcpyDeviceToHost, st_));
+        OF2D_HIP(hipMemcpyAsync(hs_.flt, scal, sizeof(float) * 3, hipMemcpyDeviceToHost, st_));
+        check_status();
+        const float maxabs = hs_.flt[0], dt = hs_.flt[1], jmin = hs_.flt[2];
+        print("Dumax: %.3f\tMaxabs increment: %.3f\t Timestep: %.3f\n", (double)0.65f,
+              (double)maxabs, (double)dt);
+        const float err = logger_error(hs_.sums[0], hs_.sums[1], npx);
+        last_err_.push_back(err);
+        if (verbose_) print("Iteration: %d\tError:%.4f\n", iter, (double)err);
+        if (!fixed_ && err < 0.001f && iter > 1) {
+            iter++;
+            break;
+        }
+        if (jmin < 0.5) {  // regridding (ImageRegistrationFluid.cpp:108-124)
+            print("Regridding on iteration: %d\tMin Jacobian: %.3f\n", iter, (double)jmin);
+            launch_accumulate(L.motion[L.mcur].p, est, L.motion[1 - L.mcur].p, L.dx, L.dy, L.P,
+                              st_);
+            L.mcur ^= 1;
+            L.est[0].zero(st_);
+            launch_warp(L.Imov.p, L.cur_motion(), L.Iaux.p, L.dx, L.dy, L.P, st_);
+            launch_gradients(L.Iref.p, L.Iaux.p, L.dI.p, L.It.p, L.dx, L.dy, L.P, st_);
+        }
+    }
+    return iter;
 }
-int Registration::loop_elastic(Level &, int, int &) {
-    throw std::runtime_error("Elastic: not implemented yet");
+
+// ImageRegistrationOpticalFlow loop (:123-135) with OpticalFlowElastic::get_update
+// (OpticalFlowElastic.cpp:13-19): force from the motion, then the SOR sweep of
+// the motion itself (in place).  Chunked like HS; the chunk's start state is
+// snapshot so a break inside the chunk is replayed from it.
+int Registration::loop_elastic(Level &L, int niter, int &final_buf) {
+    const float mu = params_[0], lambda = params_[1];
+    const float omega = params_.size() == 3 ? params_[2] : 0.66f;  // OpticalFlowElastic.h:9
+    float2 *est = L.est[0].p;
+    float2 *snap = L.est[1].p;
+    float2 *prev = L.tmp.p;
+    L.tmp.zero(st_);
+    const int nb = increment_nblocks(L.dx, L.dy);
+    const double npx = (double)L.dx * L.dy;
+    auto update = [&]() {
+        launch_force(est, L.dI.p, L.It.p, L.force.p, L.dx, L.dy, L.P, st_);
+        launch_sor(est, L.force.p, L.dI.p, L.It.p, false, L.dx, L.dy, L.P, mu, lambda, omega,
+                   L.sorH.p, ++epoch_, L.sorTicket.p, d_status_, st_);
+    };
+    last_err_.clear();
+    final_buf = 0;
+    int k0 = 0;
+    while (k0 < niter) {
+        const int C = std::min(chunk_, niter - k0);
+        OF2D_HIP(hipMemcpyAsync(L.est[1].base, L.est[0].base, L.est[0].bytes(),
+                                hipMemcpyDeviceToDevice, st_));
+        for (int t = 0; t < C; t++) {
+            update();
+            launch_logger(est, prev, L.dx, L.dy, L.P, d_partial_ + (size_t)t * nb * 2, st_);
+        }
+        launch_reduce_partials(d_partial_, nb, C, d_sums_, st_);
+        OF2D_HIP(hipMemcpyAsync(hs_.sums, d_sums_, sizeof(double) * 2 * C, hipMemcpyDeviceToHost,
+                                st_));
+        check_status();
+        for (int t = 0; t < C; t++) {
+            const int k = k0 + t;
+            const float err = logger_error(hs_.sums[2 * t], hs_.sums[2 * t + 1], npx);
+            last_err_.push_back(err);
+            if (verbose_) print("Iteration: %d\tError:%.4f\n", k, (double)err);
+            if (!fixed_ && err < 0.001f && k > 1) {
+                if (t < C - 1) {  // replay up to the break from the chunk's start state
+                    OF2D_HIP(hipMemcpyAsync(L.est[0].base, L.est[1].base, L.est[0].bytes(),
+                                            hipMemcpyDeviceToDevice, st_));
+                    for (int r = 0; r <= t; r++) update();
+                    check_status();
+                }
+                (void)snap;
+                return k + 1;
+            }
+        }
+        k0 += C;
+    }
+    return niter;
 }
+
 int Registration::loop_curvature(Level &, int, int &) {
     throw std::runtime_error("Curvature: not implemented yet");
 }

@@ -1,0 +1,98 @@
+"""Viscous fluid and elastic registration on the MI355X against the oracle.
+
+The SOR sweep runs as an exact wavefront of the reference's in-place
+Gauss-Seidel order (fluid_kernels.hip), so the bar is bit-exact motion fields,
+identical iteration counts and identical printed Dumax / Regridding lines.
+"""
+import numpy as np
+import pytest
+
+from conftest import golden
+from opticalflow2d_amd import ImageRegistration
+from opticalflow2d_amd import synthetic as S
+
+pytestmark = pytest.mark.gpu
+
+
+def run_both(gpu, oracle, dims, niter, nscales, reg, params, nrefine, ref, mov, calls=1,
+             **opt):
+    gpu.clear()
+    with ImageRegistration(dims, niter, nscales, reg, params, nrefine, **opt) as r:
+        for _ in range(calls):
+            r.register(ref, mov)
+        g = dict(motion=r.motion(), warped=r.warp(mov), iters=r.iterations())
+    gtext = "".join(gpu)
+    L = oracle.lib()
+    L.oracle_clear_output()
+    o = oracle.Registration(dims, niter, nscales, reg, params, nrefine, 0,
+                            fixed_iters=bool(opt.get("fixed_iters", 0)))
+    for _ in range(calls):
+        o.register(ref, mov)
+    w = dict(motion=o.motion(), warped=o.warp(mov), iters=o.iterations())
+    o.close()
+    otext = L.oracle_captured_output().decode()
+    return g, w, gtext, otext
+
+
+def body(text):
+    """Printed lines after the banner (Dumax / Regridding / Iteration)."""
+    return [l for l in text.splitlines()
+            if l.startswith(("Dumax", "Regridding", "Iteration"))]
+
+
+def test_fluid_and_elastic_fixtures(gpu):
+    g = golden("oracle_paths.npz")
+    for name, niter, nscales, reg, params in [("fluid_disk64", [30, 30], 1, 5, [0.25, 0.0]),
+                                              ("elastic_texture64", [25], 0, 2, [0.5, 0.25])]:
+        with ImageRegistration((64, 64), niter, nscales, reg, params, 1) as r:
+            r.register(g[f"{name}/ref"], g[f"{name}/mov"])
+            assert r.iterations() == g[f"{name}/iters"].tolist(), name
+            assert np.array_equal(r.motion(), g[f"{name}/motion"]), name
+            assert np.array_equal(r.warp(g[f"{name}/mov"]), g[f"{name}/warped"]), name
+
+
+@pytest.mark.parametrize("dims", [(70, 37), (130, 50), (64, 64), (125, 300), (5, 4)])
+def test_fluid_printed_lines_and_motion(gpu, oracle, dims):
+    ref, mov = S.shifted_disk(max(dims))
+    ref, mov = ref[: dims[0], : dims[1]], mov[: dims[0], : dims[1]]
+    g, w, gt, ot = run_both(gpu, oracle, dims, [20], 0, 5, [0.25, 0.0], 1, ref, mov)
+    assert g["iters"] == w["iters"]
+    assert np.array_equal(g["motion"], w["motion"])
+    assert body(gt) == body(ot)
+
+
+def test_fluid_regridding_and_warm_start(gpu, oracle):
+    """Large shift -> Jacobian drops below 0.5 -> regridding; the velocity field
+    persists across register calls (OpticalFlowFluid.cpp:50)."""
+    ref, mov = S.shifted_disk(96, shift=(9, 5))
+    g, w, gt, ot = run_both(gpu, oracle, (96, 96), [60, 40], 1, 5, [0.25, 0.0, 0.9], 1, ref, mov,
+                            calls=2)
+    assert g["iters"] == w["iters"]
+    assert np.array_equal(g["motion"], w["motion"])
+    assert body(gt) == body(ot)
+
+
+def test_fluid_many_strips_512(gpu, oracle):
+    """8 wavefront strips with hand-offs; 3 pyramid levels as in config 4."""
+    ref, mov = S.shifted_disk(512)
+    g, w, gt, ot = run_both(gpu, oracle, (512, 512), [6, 6, 6], 2, 5, [0.25, 0.0], 1, ref, mov)
+    assert g["iters"] == w["iters"]
+    assert np.array_equal(g["motion"], w["motion"])
+    assert body(gt) == body(ot)
+
+
+@pytest.mark.parametrize("chunk", [1, 5, 32])
+def test_elastic_chunked_with_break(gpu, oracle, chunk):
+    ref, mov = S.texture_pair(90, seed=12, ny=77)
+    g, w, _, _ = run_both(gpu, oracle, (90, 77), [1000], 0, 2, [0.1, 0.0], 1, ref, mov,
+                          chunk=chunk)
+    assert g["iters"] == w["iters"] == [413]
+    assert np.array_equal(g["motion"], w["motion"])
+
+
+def test_elastic_wide_sweep(gpu, oracle):
+    """One SOR sweep over 1100 x 300 (18 strips), fixed iterations."""
+    ref, mov = S.texture_pair(1100, seed=3, ny=300)
+    g, w, _, _ = run_both(gpu, oracle, (1100, 300), [3], 0, 2, [0.3, 0.1], 1, ref, mov,
+                          fixed_iters=1)
+    assert np.array_equal(g["motion"], w["motion"])
