@@ -1,0 +1,167 @@
+#!/usr/bin/env python3
+"""Secondary BASELINE.json configurations on one MI355X (bench.py is the
+headline).  One JSON line per configuration:
+
+  cfg1  HS 256^2 translated square, 200 iterations, MEX call sequence
+        (init -> register -> get -> warp -> close) through the gateway
+  cfg3  Thirion's Demons 4096^2 (params [1, 0.25, 2, 2, 5, Composition])
+  cfg4  viscous fluid 8192^2, 3-level pyramid (params [0.25, 0.0])
+  cfg5  HS 16384^2 on one GPU (the 1-GPU point of the row-slab config)
+
+Each GPU line carries the oracle's single-core time on a bounded sample of the
+same work (`cpu_baseline`).  Iteration counts are fixed (no convergence break)
+so the work is well defined; `--iters` scales them down for a quick run.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+
+def oracle_time(dims, niter, nscales, reg, params, ref, mov, fixed=True):
+    from oracle import oracle as O
+    O.lib().oracle_capture_output(1)
+    O.lib().oracle_set_reference_loop_order(1)
+    r = O.Registration(dims, niter, nscales, reg, params, 1, 0, fixed_iters=fixed)
+    t0 = time.perf_counter()
+    r.register(ref, mov)
+    dt = time.perf_counter() - t0
+    it = r.iterations()
+    r.close()
+    O.lib().oracle_set_reference_loop_order(0)
+    O.lib().oracle_clear_output()
+    return dt, it
+
+
+def gpu_time(dims, niter, nscales, reg, params, ref, mov, reps=1):
+    from opticalflow2d_amd import ImageRegistration
+    with ImageRegistration(dims, niter, nscales, reg, params, 1, fixed_iters=1) as r:
+        r.register(ref, mov)  # warm-up (allocation, first launches)
+        best = 1e30
+        for _ in range(reps):
+            # images go up untimed; the timed region is the device pyramid
+            r.set_images(ref, mov)
+            t0 = time.perf_counter()
+            r.estimate()
+            best = min(best, time.perf_counter() - t0)
+        it = r.iterations()
+    return best, it
+
+
+def level_px(dims, nscales, niter):
+    tot = 0
+    for s in range(nscales + 1):
+        sc = np.float32(2.0 ** s)
+        dx = int(np.float32(dims[0]) / sc)
+        dy = int(np.float32(dims[1]) / sc)
+        tot += dx * dy * niter[s]
+    return tot
+
+
+def cfg1():
+    from opticalflow2d_amd import OpticalFlow2d
+    from opticalflow2d_amd import synthetic as S
+    ref, mov = S.translated_square(256)
+    OpticalFlow2d([256, 256], [200], 0, 0, [0.1], 1, 1, 0)  # warm-up object
+    OpticalFlow2d(ref, mov)
+    OpticalFlow2d()
+    t0 = time.perf_counter()
+    OpticalFlow2d([256, 256], [200], 0, 0, [0.1], 1, 1, 0)
+    OpticalFlow2d(ref, mov)
+    m = OpticalFlow2d(nargout=1)
+    OpticalFlow2d(mov, nargout=1)
+    OpticalFlow2d()
+    dt = time.perf_counter() - t0
+    cdt, _ = oracle_time((256, 256), [200], 0, 0, [0.1], ref, mov, fixed=False)
+    return {"config": "cfg1 HS 256^2 square, 200 iters, init->register->get->warp->close",
+            "gpu_wall_s": round(dt, 5), "cpu_wall_s": round(cdt, 4),
+            "sum_motion": float(m.sum()), "cpu_baseline": {"cores": 1, "kind": "port"}}
+
+
+def cfg3(iters):
+    from opticalflow2d_amd import synthetic as S
+    n = 4096
+    ref, mov = S.procedural_pair(n, 0, n)
+    params = [1.0, 0.25, 2.0, 2.0, 5, 0]
+    dt, it = gpu_time((n, n), [iters], 0, 3, params, ref, mov, reps=2)
+    px_it = n * n * it[0]
+    # CPU sample: 512^2, 3 iterations of the same solver (extrapolated per px-it)
+    rs, ms = S.procedural_pair(512, 0, 512)
+    cdt, cit = oracle_time((512, 512), [3], 0, 3, params, rs, ms)
+    cpu = 512 * 512 * cit[0] / cdt / 1e6
+    return {"config": f"cfg3 Thirion Demons {n}^2, {it[0]} iterations (fixed)",
+            "value": round(px_it / dt / 1e6, 1), "unit": "Mpx-it/s", "gpu_wall_s": round(dt, 4),
+            "ms_per_iter": round(1000 * dt / it[0], 4),
+            "cpu_baseline": {"value": round(cpu, 2), "unit": "Mpx-it/s", "cores": 1,
+                             "kind": "port", "sample": "oracle 512^2 x 3 iterations"}}
+
+
+def cfg4(iters):
+    from opticalflow2d_amd import synthetic as S
+    n = 8192
+    ref, mov = S.shifted_disk(n)
+    niter = [iters, iters, iters]
+    params = [0.25, 0.0]
+    dt, it = gpu_time((n, n), niter, 2, 5, params, ref, mov, reps=1)
+    px_it = level_px((n, n), 2, [it[2], it[1], it[0]])
+    rs, ms = S.shifted_disk(1024)
+    cdt, cit = oracle_time((1024, 1024), [2, 2, 2], 2, 5, params, rs, ms)
+    cpu = level_px((1024, 1024), 2, [cit[2], cit[1], cit[0]]) / cdt / 1e6
+    return {"config": f"cfg4 viscous fluid {n}^2, 3 levels x {iters} iterations (fixed)",
+            "value": round(px_it / dt / 1e6, 1), "unit": "Mpx-it/s", "gpu_wall_s": round(dt, 3),
+            "iterations": it,
+            "cpu_baseline": {"value": round(cpu, 2), "unit": "Mpx-it/s", "cores": 1,
+                             "kind": "port", "sample": "oracle 1024^2, 3 levels x 2 iterations"}}
+
+
+def cfg5(iters):
+    from opticalflow2d_amd import SlabSolver
+    from opticalflow2d_amd import synthetic as S
+    n = 16384
+    ref, mov = S.procedural_pair(n, 0, n)
+    s = SlabSolver(n, n, 0.1)
+    s.set_images(ref, mov)
+    del ref, mov
+    s.run(20, fixed_iters=True)
+    t0 = time.perf_counter()
+    s.run(iters, fixed_iters=True)
+    dt = time.perf_counter() - t0
+    us = s.time_kernel(20)
+    s.close()
+    return {"config": f"cfg5 HS {n}^2 on 1 GPU, {iters} iterations",
+            "value": round(n * n * iters / dt / 1e6, 1), "unit": "Mpx-it/s",
+            "ms_per_iter": round(1000 * dt / iters, 4), "kernel_us": round(us, 2),
+            "kernel_GBps": round(28.0 * n * n / us / 1e3, 1)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--configs", default="1,3,4,5")
+    ap.add_argument("--iters", type=int, default=0, help="override iteration counts")
+    a = ap.parse_args()
+    from opticalflow2d_amd import set_print_sink
+    set_print_sink(lambda s: None)
+    for c in a.configs.split(","):
+        if c == "1":
+            r = cfg1()
+        elif c == "3":
+            r = cfg3(a.iters or 100)
+        elif c == "4":
+            r = cfg4(a.iters or 200)
+        elif c == "5":
+            r = cfg5(a.iters or 1000)
+        else:
+            continue
+        print(json.dumps(r), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -21,9 +21,10 @@
 //     neighbour's three upcoming OLD values arrive by cross-lane shuffles —
 //     a step costs no LDS and no barrier;
 //   * lane 0 is a ghost of the previous strip's last column: it receives those
-//     NEW values from the previous strip through 8-byte {epoch, value}
-//     granules (agent-scope release/acquire-free hand-off, MI355X guide §6
-//     G16 R2), prefetched a few steps ahead; lane 63 is a ghost of the next
+//     NEW values from the previous strip through 16-byte {x, epoch, y, epoch}
+//     granules written and read with single sc1 dwordx4 accesses (a tag-checked
+//     hand-off that needs no release/acquire fence, MI355X guide §6 G16 R2),
+//     prefetched 8-16 steps ahead; lane 63 is a ghost of the next
 //     strip's first column (OLD values, which that strip cannot overwrite
 //     before this strip has published the rows that depend on them);
 //   * strips are claimed in order through a ticket counter, so a strip only
@@ -35,209 +36,390 @@
 namespace of2d {
 
 namespace {
-constexpr int kStripCols = 62;
-constexpr int kPre = 8;    // rows of OLD values prefetched ahead of the window
-constexpr int kGPre = 8;   // granule rows prefetched ahead by lane 0
 constexpr unsigned kSpinLimit = 1u << 24;
 
 typedef unsigned long long u64;
 
-__device__ __forceinline__ u64 gload(const u64 *p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void gstore(u64 *p, u64 v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ u64 granule(unsigned epoch, float v) {
-    return ((u64)epoch << 32) | (u64)__float_as_uint(v);
-}
+// rows per block of the element-wise field kernels (64 x 4 threads, 8 rows
+// each): few enough partials that the single-block final reductions are short
+constexpr int kFieldRows = 32;
 
-struct Px {  // what one lane needs at one row
-    float2 v;     // OLD velocity
-    float2 g;     // dI
-    float2 u;     // motion (fused force) or force b
-    float it;     // It (fused force)
+struct Grad2 {
+    float2 dx, dy;
 };
-
-template <bool FUSED>
-__device__ __forceinline__ Px load_px(const float2 *v, const float2 *u, const float2 *dI,
-                                      const float *It, int c, int r, int dimx, int dimy, int P) {
-    Px p;
-    const int cc = min(max(c, 0), dimx - 1), rr = min(max(r, 0), dimy - 1);
-    const long idx = (long)rr * P + cc;
-    p.v = v[idx];
-    p.u = u[idx];
-    if constexpr (FUSED) {
-        p.g = dI[idx];
-        p.it = It[idx];
+// partial_x / partial_y of the motion on coord2d (gradients.h:9-32): one-sided
+// at the borders, (a - b) / 2 inside
+__device__ __forceinline__ Grad2 motion_gradients(const float2 *__restrict__ u, long idx, int i,
+                                                  int j, int dimx, int dimy, int P) {
+    Grad2 d;
+    if (i == 0) {
+        const float2 a = u[idx + 1], b = u[idx];
+        d.dx = make_float2(a.x - b.x, a.y - b.y);
+    } else if (i == dimx - 1) {
+        const float2 a = u[idx], b = u[idx - 1];
+        d.dx = make_float2(a.x - b.x, a.y - b.y);
     } else {
-        p.g = make_float2(0.0f, 0.0f);
-        p.it = 0.0f;
+        const float2 a = u[idx + 1], b = u[idx - 1];
+        d.dx = make_float2((a.x - b.x) / 2.0f, (a.y - b.y) / 2.0f);
     }
-    return p;
+    if (j == 0) {
+        const float2 a = u[idx + P], b = u[idx];
+        d.dy = make_float2(a.x - b.x, a.y - b.y);
+    } else if (j == dimy - 1) {
+        const float2 a = u[idx], b = u[idx - P];
+        d.dy = make_float2(a.x - b.x, a.y - b.y);
+    } else {
+        const float2 a = u[idx + P], b = u[idx - P];
+        d.dy = make_float2((a.x - b.x) / 2.0f, (a.y - b.y) / 2.0f);
+    }
+    return d;
 }
 
-__device__ __forceinline__ float2 shfl_up2(float2 a) {
-    return make_float2(__shfl_up(a.x, 1), __shfl_up(a.y, 1));
+// max / min over a 64 x 4 block (result valid in thread (0,0)); the order of a
+// max or min does not change its value
+__device__ __forceinline__ float block_max(float m) {
+    for (int off = 32; off > 0; off >>= 1) {
+        const float o = __shfl_down(m, off);
+        m = (m < o) ? o : m;
+    }
+    __shared__ float red[4];
+    if (threadIdx.x == 0) red[threadIdx.y] = m;
+    __syncthreads();
+    for (int w = 1; w < 4; w++) m = (m < red[w]) ? red[w] : m;
+    return m;
 }
-__device__ __forceinline__ float2 shfl_down2(float2 a) {
-    return make_float2(__shfl_down(a.x, 1), __shfl_down(a.y, 1));
+__device__ __forceinline__ float block_min(float m) {
+    for (int off = 32; off > 0; off >>= 1) {
+        const float o = __shfl_down(m, off);
+        m = (o < m) ? o : m;
+    }
+    __shared__ float red[4];
+    if (threadIdx.x == 0) red[threadIdx.y] = m;
+    __syncthreads();
+    for (int w = 1; w < 4; w++) m = (red[w] < m) ? red[w] : m;
+    return m;
+}
+// fp64 Logger partials of a 64 x 4 block, fixed order, written by thread (0,0)
+__device__ __forceinline__ void block_sum2(double sd, double sp, double *__restrict__ partial) {
+    for (int off = 32; off > 0; off >>= 1) {
+        sd += __shfl_down(sd, off);
+        sp += __shfl_down(sp, off);
+    }
+    __shared__ double red[2][4];
+    if (threadIdx.x == 0) {
+        red[0][threadIdx.y] = sd;
+        red[1][threadIdx.y] = sp;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0 && threadIdx.y == 0) {
+        const long blk = (long)blockIdx.y * gridDim.x + blockIdx.x;
+        partial[2 * blk] = ((red[0][0] + red[0][1]) + red[0][2]) + red[0][3];
+        partial[2 * blk + 1] = ((red[1][0] + red[1][1]) + red[1][2]) + red[1][3];
+    }
+}
+// max / min over a 1024-thread block (result valid in thread 0)
+__device__ __forceinline__ float wide_max(float m) {
+    for (int off = 32; off > 0; off >>= 1) {
+        const float o = __shfl_down(m, off);
+        m = (m < o) ? o : m;
+    }
+    __shared__ float red[16];
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+    __syncthreads();
+    for (int w = 1; w < 16; w++) m = (m < red[w]) ? red[w] : m;
+    return m;
+}
+__device__ __forceinline__ float wide_min(float m) {
+    for (int off = 32; off > 0; off >>= 1) {
+        const float o = __shfl_down(m, off);
+        m = (o < m) ? o : m;
+    }
+    __shared__ float red[16];
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+    __syncthreads();
+    for (int w = 1; w < 16; w++) m = (red[w] < m) ? red[w] : m;
+    return m;
 }
 }  // namespace
 
-// FUSED: b = force computed from (u, dI, It) of the same pixel (Fluid: u is not
-// modified by the sweep).  !FUSED: b read from `u` (Elastic: the force is
-// computed before the sweep and the sweep updates the motion itself).
-template <bool FUSED>
-__global__ __launch_bounds__(64) void sor_strip_kernel(
-    float2 *__restrict__ v, const float2 *__restrict__ u, const float2 *__restrict__ dI,
-    const float *__restrict__ It, int dimx, int dimy, int P, float A, float B, float M, float ML,
-    u64 *__restrict__ H, unsigned epoch, unsigned *__restrict__ ticket, int nstrips,
-    unsigned *__restrict__ status) {
+// The sweep works on a packed array vb = {v.x, v.y, b.x, b.y}: the field being
+// relaxed and its right-hand side, stored SKEWED along the wavefront: pixel
+// (i, j) lives at row t = 2i + j, column i (sor_index).  Every lane of a strip
+// then works on the same row t at each step, so a step's load is one
+// contiguous 1-KB row segment and its store one 512-B half-interleaved segment
+// (row-major storage would make both 64 separate transactions).  Cells of the
+// skewed array that are no pixel (j outside [0, dimy)) are padding: a lane
+// whose wavefront row lies outside the image reads and writes back its own
+// padding cell instead of branching.
+//
+// Lane l (0..62) owns column c0 + l and at step s works on row s + 1 - 2l;
+// lane 63 is a ghost of the next strip's first column (OLD values only).
+// Per step and wave:
+//   * two DPP wave_shr:1 move the left neighbours' newest outputs one lane to
+//     the right; lane 0, which has no left lane, takes the DPP `old` operand,
+//     i.e. the ghost column's value (the previous strip's last column, or the
+//     image column 0 for strip 0) — the hand-off costs no select;
+//   * two DPP wave_shl:1 bring the right neighbour's newest OLD row; older
+//     neighbour values slide through registers (L <- LU, R <- RU ...);
+//   * the update itself runs on packed fp32 (v_pk_add/v_pk_mul, no
+//     contraction: the reference's float operation order, OpticalFlowFluid.cpp:27-35);
+//   * one 8-B store of the new value, one 16-B granule store by lane 62; the
+//     stores of lanes that own no interior column are dropped by the buffer
+//     range check (voffset past num_records), not masked.
+// Loads run one group (4 batches of 8 rows) ahead; granules (lane k of a
+// vector = ghost row q + k, {epoch, x, y, epoch}: both 8-B halves carry the
+// tag) two batches ahead, are tag-checked once per batch and rotated one lane
+// per step by DPP.  Groups whose rows are interior for every lane skip the
+// boundary-row select.
+namespace {
+constexpr int kSorCols = 63;  // real columns per strip (lanes 0..62)
+constexpr int kSorB = 8;      // rows per batch
+constexpr int kSorNB = 4;     // batches per group
+constexpr int kSorG = kSorB * kSorNB;
+constexpr int kSorGLead = 2;  // granule vectors are loaded this many batches ahead
+constexpr unsigned kOob = 0x40000000u;   // voffset beyond num_records: the access is dropped
+constexpr int kNumRecords = 0x20000000;  // bytes addressable from a moving rsrc base
+constexpr int kRsrcFlags = 0x00020000;
+
+typedef float v2f __attribute__((ext_vector_type(2)));
+typedef unsigned v2u __attribute__((ext_vector_type(2)));
+typedef unsigned v4u __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ float dpp_shr_old(float old, float x) {  // lane i <- i-1, lane 0 <- old
+    return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(old), __float_as_int(x), 0x138,
+                                                      0xF, 0xF, false));
+}
+__device__ __forceinline__ float dpp_shl(float x) {  // lane i <- lane i+1 (lane 63 <- 0)
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x130, 0xF, 0xF, true));
+}
+__device__ __forceinline__ v2f lo2(v4u q) { return v2f{__uint_as_float(q.x), __uint_as_float(q.y)}; }
+__device__ __forceinline__ v2f hi2(v4u q) { return v2f{__uint_as_float(q.z), __uint_as_float(q.w)}; }
+__device__ __forceinline__ v2f mid2(v4u q) { return v2f{__uint_as_float(q.y), __uint_as_float(q.z)}; }
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_at(const void *p) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), 0, kNumRecords, kRsrcFlags);
+}
+
+// lanes 0..7 of a granule vector: tagged with this sweep's epoch, or a ghost
+// row outside the image (never published, never used for an interior pixel)
+__device__ __forceinline__ bool granules_ready(v4u g, int row0, int dimy, unsigned epoch) {
+    const int lane = threadIdx.x;
+    const bool ok = lane >= kSorB || (g.x == epoch && g.w == epoch) ||
+                    (unsigned)(row0 + lane) >= (unsigned)dimy;
+    return __builtin_amdgcn_ballot_w64(ok) == ~0ull;
+}
+
+// Slow path of the hand-off: some granule of the batch was not yet published
+// when it was prefetched; poll the batch until it is.  Out of line, so the
+// fast path's counted vmcnt is not turned into a drain at a loop preheader.
+__device__ __attribute__((noinline)) v4u granule_poll(__amdgpu_buffer_rsrc_t rs, unsigned voff,
+                                                      int soff, int row0, int dimy,
+                                                      unsigned epoch, unsigned *status) {
+    v4u g = v4u{0u, 0u, 0u, 0u};
+    for (unsigned spins = 0; spins < kSpinLimit; spins++) {
+        __builtin_amdgcn_s_sleep(1);
+        g = __builtin_amdgcn_raw_buffer_load_b128(rs, voff, soff, 16 /* sc1 */);
+        if (granules_ready(g, row0, dimy, epoch)) return g;
+    }
+    atomicOr(status, kStatusSpinTimeout);
+    return g;
+}
+
+template <bool B>
+struct Flag {
+    static constexpr bool value = B;
+};
+}  // namespace
+
+__global__ __launch_bounds__(64) void sor_strip_kernel(float4 *__restrict__ vb, int dimx, int dimy,
+                                                       int P, float A, float B, float M, float ML,
+                                                       v4u *__restrict__ H, long Hstride,
+                                                       unsigned epoch,
+                                                       unsigned *__restrict__ ticket, int nstrips,
+                                                       unsigned *__restrict__ status,
+                                                       unsigned long long *__restrict__ trace) {
     const int lane = threadIdx.x;
     __shared__ int s_strip;
     if (lane == 0) s_strip = (int)(atomicAdd(ticket, 1u) % (unsigned)nstrips);
     __syncthreads();
-    const int I = s_strip;
-    const int c0 = kStripCols * I;  // lane 0 = column c0 (previous strip's last column)
+    const int I = __builtin_amdgcn_readfirstlane(s_strip);
+    // optional timeline (tools/sor_harness.hip): start, end, polled batches
+    const unsigned long long t_start = trace ? __builtin_amdgcn_s_memrealtime() : 0;
+    unsigned npoll = 0;
+    const int c0 = 1 + kSorCols * I;  // lane 0's column
     const int c = c0 + lane;
-    const bool active = lane >= 1 && lane <= kStripCols && c <= dimx - 2;
-    // this strip publishes its last column when a next strip exists
-    const bool publisher = (lane == kStripCols) && active && (c + 1 <= dimx - 2);
-    const bool consumer = (lane == 0) && (I > 0);
-    u64 *Hout = H + (size_t)I * dimy * 2;          // our column c0 + 62
-    const u64 *Hin = H + (size_t)(I - 1) * dimy * 2;  // previous strip's column c0
+    const bool active = lane < kSorCols && c <= dimx - 2;
+    // vb addressing: at step s every lane is on skewed row 2 c0 + s + 1; a
+    // batch rsrc points at (that row for the batch's first step, column c0)
+    const unsigned P16 = (unsigned)P * 16u;
+    const unsigned voff_ld = (unsigned)lane * 16u;  // lanes past dimx read padding cells
+    const unsigned voff_st = active ? (unsigned)lane * 16u : kOob;
+    const char *vbc0 = reinterpret_cast<const char *>(vb + c0);
+    // granules: region I (ghost column of this strip), region I+1 (published)
+    const char *gin = reinterpret_cast<const char *>(H + (long)I * Hstride + kSorPadRows);
+    const char *gout = reinterpret_cast<const char *>(H + (long)(I + 1) * Hstride + kSorPadRows);
+    const unsigned voff_gin = lane < kSorB ? (unsigned)lane * 16u : kOob;
+    const unsigned voff_pub = lane == kSorCols - 1 ? 0u : kOob;
 
-    // row of this lane at step s: r = s - 2(lane-1) + 1 (lane 0: s + 3)
-    const int rofs = 3 - 2 * lane;  // r = s + rofs
     const int s0 = -3;
-    const int s1 = (dimy - 2) - 1 + 2 * (kStripCols - 1);  // last step of lane 62
+    const int s1 = dimy + 122;  // lane 62 publishes ghost row dimy - 1 at this step
+    // skewed row of the first step of batch b of the group starting at step g
+    auto vrs = [&](int g, int b) {
+        return rsrc_at(vbc0 + (long)(2 * c0 + g + kSorB * b + 1) * P16);
+    };
+    auto grs = [&](int g) { return rsrc_at(gin + (long)(g + 2) * 16); };
 
-    // window of OLD values rows r..r+3 and a prefetch FIFO rows r+4..r+3+kPre
-    float2 w[4];
-    Px fifo[kPre];
-    Px cur[4];  // Px for rows r..r+3 (v, force inputs)
+    // window rows r..r+3 of the first step, batches of the first group
+    v4u W0, W1, W2, W3, X[kSorNB][kSorB], GV[kSorNB];
     {
-        const int r = s0 + rofs;
+        const auto rs = vrs(s0, 0);
+        W0 = __builtin_amdgcn_raw_buffer_load_b128(rs, voff_ld, 0, 0);
+        W1 = __builtin_amdgcn_raw_buffer_load_b128(rs, voff_ld, (int)P16, 0);
+        W2 = __builtin_amdgcn_raw_buffer_load_b128(rs, voff_ld, 2 * (int)P16, 0);
+        W3 = __builtin_amdgcn_raw_buffer_load_b128(rs, voff_ld, 3 * (int)P16, 0);
 #pragma unroll
-        for (int k = 0; k < 4; k++) {
-            cur[k] = load_px<FUSED>(v, u, dI, It, c, r + k, dimx, dimy, P);
-            w[k] = cur[k].v;
-        }
+        for (int b = 0; b < kSorNB; b++)
 #pragma unroll
-        for (int k = 0; k < kPre; k++) fifo[k] = load_px<FUSED>(v, u, dI, It, c, r + 4 + k, dimx, dimy, P);
+            for (int j = 0; j < kSorB; j++)
+                X[b][j] = __builtin_amdgcn_raw_buffer_load_b128(rs, voff_ld,
+                                                                (4 + kSorB * b + j) * (int)P16, 0);
+        const auto gr = grs(s0);
+#pragma unroll
+        for (int b = 0; b < kSorGLead; b++)
+            GV[b] = __builtin_amdgcn_raw_buffer_load_b128(gr, voff_gin, kSorB * b * 16, 16);
     }
-    // lane 0: granule prefetch FIFO for rows q..q+kGPre-1, q = s + 3
-    u64 gx[kGPre], gy[kGPre];
-    if (consumer) {
-#pragma unroll
-        for (int k = 0; k < kGPre; k++) {
-            const int q = s0 + 3 + k;
-            const int qq = min(max(q, 0), dimy - 1);
-            gx[k] = gload(Hin + 2 * (size_t)qq);
-            gy[k] = gload(Hin + 2 * (size_t)qq + 1);
-        }
-    }
-    float2 h1 = w[0], h2 = w[0], h3 = w[0];  // own outputs at s-1, s-2, s-3
-    unsigned bad = 0;
+    v2f RD = v2f{dpp_shl(__uint_as_float(W1.x)), dpp_shl(__uint_as_float(W1.y))};
+    v2f R = v2f{dpp_shl(__uint_as_float(W2.x)), dpp_shl(__uint_as_float(W2.y))};
+    v2f RU = v2f{dpp_shl(__uint_as_float(W3.x)), dpp_shl(__uint_as_float(W3.y))};
+    v2f LU = v2f{0.0f, 0.0f}, L = LU, D = lo2(W0);
+    v2f G = LU;  // lane k: ghost row (step + 2 + k) of the current batch
 
-    for (int s = s0; s <= s1; s++) {
-        const int r = s + rofs;
-        // ---- this lane's output at step s (before the shuffles of step s+1)
-        float2 out = w[0];  // boundary rows / inactive: the OLD value
-        // ---- left neighbour NEW values: its outputs at s-1, s-2, s-3
-        const float2 LU = shfl_up2(h1), L = shfl_up2(h2), LD = shfl_up2(h3);
-        // ---- right neighbour OLD values rows r-1, r, r+1 = its window w1..w3
-        const float2 RD = shfl_down2(w[1]), R = shfl_down2(w[2]), RU = shfl_down2(w[3]);
-        if (lane == 0) {
-            // ghost of column c0: NEW value at row q = r
-            const int q = r;
-            if (consumer && q >= 1 && q <= dimy - 2) {
-                u64 a = gx[0], b = gy[0];
-                unsigned spins = 0;
-                while ((unsigned)(a >> 32) != epoch || (unsigned)(b >> 32) != epoch) {
-                    if (++spins > kSpinLimit) {
-                        atomicOr(status, kStatusSpinTimeout);
-                        break;
-                    }
-                    __builtin_amdgcn_s_sleep(1);
-                    a = gload(Hin + 2 * (size_t)q);
-                    b = gload(Hin + 2 * (size_t)q + 1);
-                }
-                out = make_float2(__uint_as_float((unsigned)a), __uint_as_float((unsigned)b));
-            }
-        } else if (active && r >= 1 && r <= dimy - 2) {
-            const Px &p = cur[0];
-            float2 b;
-            if constexpr (FUSED) {
-                // OpticalFlow.cpp:33: dI * (It + u.x*dI.x + u.y*dI.y)
-                const float sc = (p.it + p.u.x * p.g.x) + p.u.y * p.g.y;
-                b = make_float2(p.g.x * sc, p.g.y * sc);
-            } else {
-                b = p.u;
-            }
-            const float2 C = w[0], U = w[1], D = h1;
-            // OpticalFlowFluid.cpp:27-35 (same association, no contraction)
-            const float s1x = ((R.x + L.x) + U.x) + D.x;
-            const float s2x = (R.x + L.x) + 0.25f * (((RU.y - LU.y) - RD.y) + LD.y);
-            const float nx = A * C.x + B * ((b.x - M * s1x) - ML * s2x);
-            const float s1y = ((R.y + L.y) + U.y) + D.y;
-            const float s2y = (R.y + L.y) + 0.25f * (((RU.x - LU.x) - RD.x) + LD.x);
-            const float ny = A * C.y + B * ((b.y - M * s1y) - ML * s2y);
-            out = make_float2(nx, ny);
-            v[(long)r * P + c] = out;
-            if (publisher) {
-                gstore(Hout + 2 * (size_t)r, granule(epoch, nx));
-                gstore(Hout + 2 * (size_t)r + 1, granule(epoch, ny));
-            }
+    auto step = [&](auto chk, int s, int j, __amdgpu_buffer_rsrc_t rs,
+                    __amdgpu_buffer_rsrc_t ps, v4u xin) {
+        const v2f C = lo2(W0), b = hi2(W0), U = lo2(W1);
+        // left neighbours' NEW values at rows r+1, r, r-1 (ghost column in lane 0)
+        const v2f LD = L;
+        L = LU;
+        const v2f Gn = v2f{dpp_shl(G.x), dpp_shl(G.y)};  // next step's ghost row in lane 0
+        LU = v2f{dpp_shr_old(G.x, D.x), dpp_shr_old(G.y, D.y)};
+        G = Gn;
+        // OpticalFlowFluid.cpp:27-35, same association, no contraction
+        const v2f RL = R + L;
+        const v2f s1v = (RL + U) + D;
+        const v2f t = ((RU - LU) - RD) + LD;
+        const v2f s2v = RL + 0.25f * t.yx;
+        const v2f n = A * C + B * ((b - M * s1v) - ML * s2v);
+        v2f out = n;
+        if constexpr (decltype(chk)::value) {
+            const int r = s + 1 - 2 * lane;
+            if ((unsigned)(r - 1) >= (unsigned)(dimy - 2)) out = C;  // boundary row: OLD value
         }
-        // ---- shift histories, window and prefetch queues
-        h3 = h2;
-        h2 = h1;
-        h1 = out;
+        __builtin_amdgcn_raw_buffer_store_b64(
+            v2u{__float_as_uint(out.x), __float_as_uint(out.y)}, rs, voff_st, j * (int)P16, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(
+            v4u{epoch, __float_as_uint(out.x), __float_as_uint(out.y), epoch}, ps,
+            voff_pub + (unsigned)j * 16u, 0, 16 /* sc1 */);
+        D = out;
+        W0 = W1;
+        W1 = W2;
+        W2 = W3;
+        W3 = xin;
+        RD = R;
+        R = RU;
+        RU = v2f{dpp_shl(__uint_as_float(W3.x)), dpp_shl(__uint_as_float(W3.y))};
+    };
+
+    auto group = [&](auto chk, int g) {
 #pragma unroll
-        for (int k = 0; k < 3; k++) {
-            cur[k] = cur[k + 1];
-            w[k] = w[k + 1];
-        }
-        cur[3] = fifo[0];
-        w[3] = fifo[0].v;
-#pragma unroll
-        for (int k = 0; k < kPre - 1; k++) fifo[k] = fifo[k + 1];
-        fifo[kPre - 1] = load_px<FUSED>(v, u, dI, It, c, r + 4 + kPre, dimx, dimy, P);
-        if (consumer) {
-#pragma unroll
-            for (int k = 0; k < kGPre - 1; k++) {
-                gx[k] = gx[k + 1];
-                gy[k] = gy[k + 1];
+        for (int b = 0; b < kSorNB; b++) {
+            const int sb = g + kSorB * b;
+            // ghost rows sb+2 .. sb+9: check the tags, start the lead batch's load
+            v4u gv = GV[b];
+            if (!granules_ready(gv, sb + 2, dimy, epoch)) {
+                gv = granule_poll(grs(g), voff_gin, kSorB * b * 16, sb + 2, dimy, epoch, status);
+                npoll++;
             }
-            const int qn = r + 1 + (kGPre - 1);
-            const int qq = min(max(qn, 0), dimy - 1);
-            gx[kGPre - 1] = gload(Hin + 2 * (size_t)qq);
-            gy[kGPre - 1] = gload(Hin + 2 * (size_t)qq + 1);
+            G = mid2(gv);
+            {
+                const int bl = b + kSorGLead;  // batch index counted from this group
+                GV[bl % kSorNB] = __builtin_amdgcn_raw_buffer_load_b128(grs(g), voff_gin,
+                                                                        kSorB * bl * 16, 16);
+            }
+            const auto rs = vrs(g, b);
+            const auto ps = rsrc_at(gout + (long)(sb - 123) * 16);
+#pragma unroll
+            for (int j = 0; j < kSorB; j++) step(chk, sb + j, j, rs, ps, X[b][j]);
+            // batch b of the next group: rows 32 further down
+#pragma unroll
+            for (int j = 0; j < kSorB; j++)
+                X[b][j] = __builtin_amdgcn_raw_buffer_load_b128(rs, voff_ld,
+                                                                (4 + kSorG + j) * (int)P16, 0);
         }
+    };
+
+    for (int g = s0; g <= s1; g += kSorG) {
+        if (g >= 124 && g + kSorG - 1 <= dimy - 3)
+            group(Flag<false>{}, g);
+        else
+            group(Flag<true>{}, g);
     }
-    (void)bad;
+    if (trace && lane == 0) {
+        trace[3 * I] = t_start;
+        trace[3 * I + 1] = __builtin_amdgcn_s_memrealtime();
+        trace[3 * I + 2] = npoll;
+    }
 }
 
-int sor_nstrips(int dimx) { return dimx < 3 ? 0 : (dimx - 2 + kStripCols - 1) / kStripCols; }
+int sor_nstrips(int dimx) { return dimx < 3 ? 0 : (dimx - 2 + kSorCols - 1) / kSorCols; }
+long sor_granule_stride(int dimy) { return (long)dimy + 2L * kSorPadRows; }
+size_t sor_granule_bytes(int dimx, int dimy) {
+    return (size_t)(sor_nstrips(dimx) + 1) * (size_t)sor_granule_stride(dimy) * 16u;
+}
 
-void launch_sor(float2 *v, const float2 *u_or_b, const float2 *dI, const float *It, bool fused,
-                int dimx, int dimy, int P, float mu, float lambda, float omega,
-                unsigned long long *H, unsigned epoch, unsigned *ticket, unsigned *status,
-                hipStream_t st) {
+void launch_sor(float4 *vb, int dimx, int dimy, int P, float mu, float lambda, float omega,
+                void *H, unsigned epoch, unsigned *ticket, unsigned *status, hipStream_t st) {
     if (dimx < 3 || dimy < 3) return;  // no interior (OpticalFlowFluid.cpp:23-24)
     const int ns = sor_nstrips(dimx);
     // per-pixel constants of OpticalFlowFluid.cpp:27 evaluated once, same float ops
     const float A = 1.0f - omega;
     const float B = omega / (-6 * mu - 2 * lambda);
     const float ML = mu + lambda;
-    if (fused)
-        hipLaunchKernelGGL(sor_strip_kernel<true>, dim3(ns), dim3(64), 0, st, v, u_or_b, dI, It,
-                           dimx, dimy, P, A, B, mu, ML, (u64 *)H, epoch, ticket, ns, status);
-    else
-        hipLaunchKernelGGL(sor_strip_kernel<false>, dim3(ns), dim3(64), 0, st, v, u_or_b, dI, It,
-                           dimx, dimy, P, A, B, mu, ML, (u64 *)H, epoch, ticket, ns, status);
+    hipLaunchKernelGGL(sor_strip_kernel, dim3(ns), dim3(64), 0, st, vb, dimx, dimy, P, A, B, mu,
+                       ML, (v4u *)H, sor_granule_stride(dimy), epoch, ticket, ns, status,
+                       (unsigned long long *)nullptr);
+    OF2D_HIP(hipGetLastError());
+}
+
+// vb.zw <- force(u, dI, It) (OpticalFlow.cpp:15-39); with pack_v also vb.xy <- v.
+// Column 0 (never relaxed) is the ghost column of strip 0: its values go to
+// granule region 0 with this sweep's epoch.
+__global__ void sor_pack_kernel(float4 *__restrict__ vb, const float2 *__restrict__ u,
+                                const float2 *__restrict__ dI, const float *__restrict__ It,
+                                const float2 *__restrict__ v, int dimx, int dimy, int P,
+                                v4u *__restrict__ H, unsigned epoch) {
+    const int i = blockIdx.x * 64 + threadIdx.x, j = blockIdx.y * 4 + threadIdx.y;
+    if (i >= dimx || j >= dimy) return;
+    const long idx = (long)j * P + i;
+    const float2 m = u[idx], g = dI[idx];
+    const float sc = (It[idx] + m.x * g.x) + m.y * g.y;
+    const float2 b = make_float2(g.x * sc, g.y * sc);
+    const long sk = sor_index(i, j, P);
+    float2 x;
+    if (v) {
+        x = v[idx];
+        vb[sk] = make_float4(x.x, x.y, b.x, b.y);
+    } else {
+        reinterpret_cast<float2 *>(vb + sk)[1] = b;
+        x = reinterpret_cast<const float2 *>(vb + sk)[0];
+    }
+    if (i == 0 && H)
+        H[kSorPadRows + j] = v4u{epoch, __float_as_uint(x.x), __float_as_uint(x.y), epoch};
+}
+void launch_sor_pack(float4 *vb, const float2 *u, const float2 *dI, const float *It,
+                     const float2 *v, int dimx, int dimy, int P, void *H, unsigned epoch,
+                     hipStream_t st) {
+    hipLaunchKernelGGL(sor_pack_kernel, dim3((dimx + 63) / 64, (dimy + 3) / 4), dim3(64, 4), 0,
+                       st, vb, u, dI, It, v, dimx, dimy, P, (v4u *)H, epoch);
     OF2D_HIP(hipGetLastError());
 }
 
@@ -265,85 +447,57 @@ void launch_force(const float2 *u, const float2 *dI, const float *It, float2 *f,
 // motion (gradients.h:9-32 on coord2d), and per-block max of (float)(2 y^2)
 // (Motion::maxabs, Motion.cpp:51-58)
 __global__ __launch_bounds__(256) void increment_kernel(const float2 *__restrict__ u,
-                                                        const float2 *__restrict__ vel,
+                                                        const float4 *__restrict__ vel,
                                                         float2 *__restrict__ R, int dimx, int dimy,
                                                         int P, float *__restrict__ part) {
-    const int i = blockIdx.x * 64 + threadIdx.x, j = blockIdx.y * 4 + threadIdx.y;
+    const int i = blockIdx.x * 64 + threadIdx.x;
     float m = 0.0f;
-    if (i < dimx && j < dimy) {
+    for (int k = 0; k < kFieldRows / 4; k++) {
+        const int j = blockIdx.y * kFieldRows + 4 * k + threadIdx.y;
+        if (i >= dimx || j >= dimy) break;
         const long idx = (long)j * P + i;
-        const float2 v = vel[idx];
-        float2 dx, dy;
-        if (i == 0) {
-            const float2 a = u[idx + 1], b = u[idx];
-            dx = make_float2(a.x - b.x, a.y - b.y);
-        } else if (i == dimx - 1) {
-            const float2 a = u[idx], b = u[idx - 1];
-            dx = make_float2(a.x - b.x, a.y - b.y);
-        } else {
-            const float2 a = u[idx + 1], b = u[idx - 1];
-            dx = make_float2((a.x - b.x) / 2.0f, (a.y - b.y) / 2.0f);
-        }
-        if (j == 0) {
-            const float2 a = u[idx + P], b = u[idx];
-            dy = make_float2(a.x - b.x, a.y - b.y);
-        } else if (j == dimy - 1) {
-            const float2 a = u[idx], b = u[idx - P];
-            dy = make_float2(a.x - b.x, a.y - b.y);
-        } else {
-            const float2 a = u[idx + P], b = u[idx - P];
-            dy = make_float2((a.x - b.x) / 2.0f, (a.y - b.y) / 2.0f);
-        }
+        const float4 vq = vel[sor_index(i, j, P)];
+        const float2 v = make_float2(vq.x, vq.y);
+        const Grad2 d = motion_gradients(u, idx, i, j, dimx, dimy, P);
         // (v - dudx*v.x) - dudy*v.y
-        const float2 r = make_float2((v.x - dx.x * v.x) - dy.x * v.y, (v.y - dx.y * v.x) - dy.y * v.y);
+        const float2 r = make_float2((v.x - d.dx.x * v.x) - d.dy.x * v.y,
+                                     (v.y - d.dx.y * v.x) - d.dy.y * v.y);
         R[idx] = r;
         const double y = (double)r.y;
-        m = (float)(y * y + y * y);
+        const float q = (float)(y * y + y * y);
+        m = (m < q) ? q : m;
     }
-    for (int off = 32; off > 0; off >>= 1) {
-        const float o = __shfl_down(m, off);
-        m = (m < o) ? o : m;
-    }
-    __shared__ float red[4];
-    const int t = threadIdx.y * 64 + threadIdx.x;
-    if ((t & 63) == 0) red[t >> 6] = m;
-    __syncthreads();
-    if (t == 0) {
-        float a = red[0];
-        for (int w = 1; w < 4; w++) a = (a < red[w]) ? red[w] : a;
-        part[(long)blockIdx.y * gridDim.x + blockIdx.x] = a;
-    }
+    m = block_max(m);
+    if (threadIdx.x == 0 && threadIdx.y == 0) part[(long)blockIdx.y * gridDim.x + blockIdx.x] = m;
 }
 
 // maxabs = sqrt(max) (float), dt = 0.65f / maxabs; scal[0]=maxabs, scal[1]=dt
-__global__ void timestep_kernel(const float *__restrict__ part, int n, float *__restrict__ scal) {
-    __shared__ float red[256];
+__global__ __launch_bounds__(1024) void timestep_kernel(const float *__restrict__ part, int n,
+                                                        float *__restrict__ scal) {
     float m = 0.0f;
-    for (int k = threadIdx.x; k < n; k += 256) m = (m < part[k]) ? part[k] : m;
-    red[threadIdx.x] = m;
-    __syncthreads();
-    for (int w = 128; w > 0; w >>= 1) {
-        if (threadIdx.x < w) {
-            const float o = red[threadIdx.x + w];
-            red[threadIdx.x] = (red[threadIdx.x] < o) ? o : red[threadIdx.x];
-        }
-        __syncthreads();
-    }
+    for (int k = threadIdx.x; k < n; k += 1024) m = (m < part[k]) ? part[k] : m;
+    m = wide_max(m);
     if (threadIdx.x == 0) {
-        const float maxabs = sqrtf(red[0]);
+        const float maxabs = sqrtf(m);
         const float dumax = 0.65f;  // OpticalFlowFluid.h:32
         scal[0] = maxabs;
         scal[1] = dumax / maxabs;
     }
 }
 
-int increment_nblocks(int dimx, int dimy) { return ((dimx + 63) / 64) * ((dimy + 3) / 4); }
+dim3 field_grid(int dimx, int dimy) {
+    return dim3((dimx + 63) / 64, (dimy + kFieldRows - 1) / kFieldRows);
+}
+int increment_nblocks(int dimx, int dimy) {
+    const dim3 g = field_grid(dimx, dimy);
+    return int(g.x * g.y);
+}
 
-void launch_increment(const float2 *u, const float2 *vel, float2 *R, int dimx, int dimy, int P,
+void launch_increment(const float2 *u, const float4 *vel, float2 *R, int dimx, int dimy, int P,
                       float *part, float *scal, hipStream_t st) {
-    const dim3 g((dimx + 63) / 64, (dimy + 3) / 4);
+    const dim3 g = field_grid(dimx, dimy);
     hipLaunchKernelGGL(increment_kernel, g, dim3(64, 4), 0, st, u, vel, R, dimx, dimy, P, part);
-    hipLaunchKernelGGL(timestep_kernel, dim3(1), dim3(256), 0, st, part, (int)(g.x * g.y), scal);
+    hipLaunchKernelGGL(timestep_kernel, dim3(1), dim3(1024), 0, st, part, (int)(g.x * g.y), scal);
     OF2D_HIP(hipGetLastError());
 }
 
@@ -357,11 +511,13 @@ __global__ __launch_bounds__(256) void integrate_logger_kernel(float2 *__restric
                                                                const float *__restrict__ scal,
                                                                int dimx, int dimy, int P,
                                                                double *__restrict__ partial) {
-    const int i = blockIdx.x * 64 + threadIdx.x, j = blockIdx.y * 4 + threadIdx.y;
+    const int i = blockIdx.x * 64 + threadIdx.x;
+    const float dt = scal[1];
     double sd = 0.0, sp = 0.0;
-    if (i < dimx && j < dimy) {
+    for (int k = 0; k < kFieldRows / 4; k++) {
+        const int j = blockIdx.y * kFieldRows + 4 * k + threadIdx.y;
+        if (i >= dimx || j >= dimy) break;
         const long idx = (long)j * P + i;
-        const float dt = scal[1];
         float2 m = u[idx];
         if (dt < 65.0f) {
             const float2 r = R[idx];
@@ -370,72 +526,46 @@ __global__ __launch_bounds__(256) void integrate_logger_kernel(float2 *__restric
         }
         const float2 pv = prev[idx];
         const float ex = m.x - pv.x, ey = m.y - pv.y;
-        sd = (double)__builtin_sqrtf(ex * ex + ey * ey);
-        sp = (double)__builtin_sqrtf(pv.x * pv.x + pv.y * pv.y);
+        sd += (double)__builtin_sqrtf(ex * ex + ey * ey);
+        sp += (double)__builtin_sqrtf(pv.x * pv.x + pv.y * pv.y);
         prev[idx] = m;
     }
-    for (int off = 32; off > 0; off >>= 1) {
-        sd += __shfl_down(sd, off);
-        sp += __shfl_down(sp, off);
-    }
-    __shared__ double red[2][4];
-    const int t = threadIdx.y * 64 + threadIdx.x;
-    if ((t & 63) == 0) {
-        red[0][t >> 6] = sd;
-        red[1][t >> 6] = sp;
-    }
-    __syncthreads();
-    if (t == 0) {
-        const long blk = (long)blockIdx.y * gridDim.x + blockIdx.x;
-        partial[2 * blk] = ((red[0][0] + red[0][1]) + red[0][2]) + red[0][3];
-        partial[2 * blk + 1] = ((red[1][0] + red[1][1]) + red[1][2]) + red[1][3];
-    }
+    block_sum2(sd, sp, partial);
 }
 
 void launch_integrate_logger(float2 *u, const float2 *R, float2 *prev, const float *scal,
                              int dimx, int dimy, int P, double *partial, hipStream_t st) {
-    hipLaunchKernelGGL(integrate_logger_kernel, dim3((dimx + 63) / 64, (dimy + 3) / 4),
-                       dim3(64, 4), 0, st, u, R, prev, scal, dimx, dimy, P, partial);
+    hipLaunchKernelGGL(integrate_logger_kernel, field_grid(dimx, dimy), dim3(64, 4), 0, st, u, R, prev, scal, dimx, dimy, P, partial);
     OF2D_HIP(hipGetLastError());
 }
 
-// Logger only (Elastic / Curvature, whose update is in place): partials of
-// ||u - prev||, ||prev||; prev <- u
-__global__ __launch_bounds__(256) void logger_kernel(const float2 *__restrict__ u,
+// Logger only (Elastic, whose update is the in-place sweep): u <- vb.xy, partials
+// of ||u - prev||, ||prev||; prev <- u
+__global__ __launch_bounds__(256) void logger_kernel(const float4 *__restrict__ vb,
+                                                     float2 *__restrict__ u,
                                                      float2 *__restrict__ prev, int dimx,
                                                      int dimy, int P,
                                                      double *__restrict__ partial) {
-    const int i = blockIdx.x * 64 + threadIdx.x, j = blockIdx.y * 4 + threadIdx.y;
+    const int i = blockIdx.x * 64 + threadIdx.x;
     double sd = 0.0, sp = 0.0;
-    if (i < dimx && j < dimy) {
+    for (int k = 0; k < kFieldRows / 4; k++) {
+        const int j = blockIdx.y * kFieldRows + 4 * k + threadIdx.y;
+        if (i >= dimx || j >= dimy) break;
         const long idx = (long)j * P + i;
-        const float2 m = u[idx], pv = prev[idx];
+        const float4 q = vb[sor_index(i, j, P)];
+        const float2 m = make_float2(q.x, q.y), pv = prev[idx];
+        u[idx] = m;
         const float ex = m.x - pv.x, ey = m.y - pv.y;
-        sd = (double)__builtin_sqrtf(ex * ex + ey * ey);
-        sp = (double)__builtin_sqrtf(pv.x * pv.x + pv.y * pv.y);
+        sd += (double)__builtin_sqrtf(ex * ex + ey * ey);
+        sp += (double)__builtin_sqrtf(pv.x * pv.x + pv.y * pv.y);
         prev[idx] = m;
     }
-    for (int off = 32; off > 0; off >>= 1) {
-        sd += __shfl_down(sd, off);
-        sp += __shfl_down(sp, off);
-    }
-    __shared__ double red[2][4];
-    const int t = threadIdx.y * 64 + threadIdx.x;
-    if ((t & 63) == 0) {
-        red[0][t >> 6] = sd;
-        red[1][t >> 6] = sp;
-    }
-    __syncthreads();
-    if (t == 0) {
-        const long blk = (long)blockIdx.y * gridDim.x + blockIdx.x;
-        partial[2 * blk] = ((red[0][0] + red[0][1]) + red[0][2]) + red[0][3];
-        partial[2 * blk + 1] = ((red[1][0] + red[1][1]) + red[1][2]) + red[1][3];
-    }
+    block_sum2(sd, sp, partial);
 }
-void launch_logger(const float2 *u, float2 *prev, int dimx, int dimy, int P, double *partial,
-                   hipStream_t st) {
-    hipLaunchKernelGGL(logger_kernel, dim3((dimx + 63) / 64, (dimy + 3) / 4), dim3(64, 4), 0, st,
-                       u, prev, dimx, dimy, P, partial);
+void launch_logger(const float4 *vb, float2 *u, float2 *prev, int dimx, int dimy, int P,
+                   double *partial, hipStream_t st) {
+    hipLaunchKernelGGL(logger_kernel, field_grid(dimx, dimy), dim3(64, 4), 0, st,
+                       vb, u, prev, dimx, dimy, P, partial);
     OF2D_HIP(hipGetLastError());
 }
 
@@ -445,67 +575,31 @@ void launch_logger(const float2 *u, float2 *prev, int dimx, int dimy, int P, dou
 __global__ __launch_bounds__(256) void jacobian_min_kernel(const float2 *__restrict__ u,
                                                            int dimx, int dimy, int P,
                                                            float *__restrict__ part) {
-    const int i = blockIdx.x * 64 + threadIdx.x, j = blockIdx.y * 4 + threadIdx.y;
+    const int i = blockIdx.x * 64 + threadIdx.x;
     float m = __builtin_inff();
-    if (i < dimx && j < dimy) {
+    for (int k = 0; k < kFieldRows / 4; k++) {
+        const int j = blockIdx.y * kFieldRows + 4 * k + threadIdx.y;
+        if (i >= dimx || j >= dimy) break;
         const long idx = (long)j * P + i;
-        float2 dx, dy;
-        if (i == 0) {
-            const float2 a = u[idx + 1], b = u[idx];
-            dx = make_float2(a.x - b.x, a.y - b.y);
-        } else if (i == dimx - 1) {
-            const float2 a = u[idx], b = u[idx - 1];
-            dx = make_float2(a.x - b.x, a.y - b.y);
-        } else {
-            const float2 a = u[idx + 1], b = u[idx - 1];
-            dx = make_float2((a.x - b.x) / 2.0f, (a.y - b.y) / 2.0f);
-        }
-        if (j == 0) {
-            const float2 a = u[idx + P], b = u[idx];
-            dy = make_float2(a.x - b.x, a.y - b.y);
-        } else if (j == dimy - 1) {
-            const float2 a = u[idx], b = u[idx - P];
-            dy = make_float2(a.x - b.x, a.y - b.y);
-        } else {
-            const float2 a = u[idx + P], b = u[idx - P];
-            dy = make_float2((a.x - b.x) / 2.0f, (a.y - b.y) / 2.0f);
-        }
-        m = (1.0f + dx.x) * (1.0f + dy.y) - dx.y * dy.x;
+        const Grad2 d = motion_gradients(u, idx, i, j, dimx, dimy, P);
+        const float q = (1.0f + d.dx.x) * (1.0f + d.dy.y) - d.dx.y * d.dy.x;
+        m = (q < m) ? q : m;
     }
-    for (int off = 32; off > 0; off >>= 1) {
-        const float o = __shfl_down(m, off);
-        m = (o < m) ? o : m;
-    }
-    __shared__ float red[4];
-    const int t = threadIdx.y * 64 + threadIdx.x;
-    if ((t & 63) == 0) red[t >> 6] = m;
-    __syncthreads();
-    if (t == 0) {
-        float a = red[0];
-        for (int w = 1; w < 4; w++) a = (red[w] < a) ? red[w] : a;
-        part[(long)blockIdx.y * gridDim.x + blockIdx.x] = a;
-    }
+    m = block_min(m);
+    if (threadIdx.x == 0 && threadIdx.y == 0) part[(long)blockIdx.y * gridDim.x + blockIdx.x] = m;
 }
-__global__ void min_final_kernel(const float *__restrict__ part, int n, float *__restrict__ out) {
-    __shared__ float red[256];
+__global__ __launch_bounds__(1024) void min_final_kernel(const float *__restrict__ part, int n,
+                                                         float *__restrict__ out) {
     float m = __builtin_inff();
-    for (int k = threadIdx.x; k < n; k += 256) m = (part[k] < m) ? part[k] : m;
-    red[threadIdx.x] = m;
-    __syncthreads();
-    for (int w = 128; w > 0; w >>= 1) {
-        if (threadIdx.x < w) {
-            const float o = red[threadIdx.x + w];
-            red[threadIdx.x] = (o < red[threadIdx.x]) ? o : red[threadIdx.x];
-        }
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) *out = red[0];
+    for (int k = threadIdx.x; k < n; k += 1024) m = (part[k] < m) ? part[k] : m;
+    m = wide_min(m);
+    if (threadIdx.x == 0) *out = m;
 }
 void launch_jacobian_min(const float2 *u, int dimx, int dimy, int P, float *part, float *out,
                          hipStream_t st) {
-    const dim3 g((dimx + 63) / 64, (dimy + 3) / 4);
+    const dim3 g = field_grid(dimx, dimy);
     hipLaunchKernelGGL(jacobian_min_kernel, g, dim3(64, 4), 0, st, u, dimx, dimy, P, part);
-    hipLaunchKernelGGL(min_final_kernel, dim3(1), dim3(256), 0, st, part, (int)(g.x * g.y), out);
+    hipLaunchKernelGGL(min_final_kernel, dim3(1), dim3(1024), 0, st, part, (int)(g.x * g.y), out);
     OF2D_HIP(hipGetLastError());
 }
 

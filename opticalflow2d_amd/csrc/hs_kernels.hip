@@ -38,13 +38,15 @@ void launch_hs_jacobi(const float2 *u_old, float2 *u_new, const float2 *dI, cons
     OF2D_HIP(hipGetLastError());
 }
 
-// partial: [C][nblocks][2]; one block per iteration, fixed summation order.
-__global__ __launch_bounds__(256) void reduce_partials_kernel(const double *__restrict__ partial,
-                                                              int nblocks,
-                                                              double *__restrict__ sums) {
+// partial: [C][nblocks][2]; one 1024-thread block per iteration, fixed
+// summation order (strided per-thread sums, wave trees, then the 16 waves in
+// order).
+__global__ __launch_bounds__(1024) void reduce_partials_kernel(const double *__restrict__ partial,
+                                                               int nblocks,
+                                                               double *__restrict__ sums) {
     const double *p = partial + (size_t)blockIdx.x * nblocks * 2;
     double a = 0.0, b = 0.0;
-    for (int i = threadIdx.x; i < nblocks; i += 256) {
+    for (int i = threadIdx.x; i < nblocks; i += 1024) {
         a += p[2 * i];
         b += p[2 * i + 1];
     }
@@ -53,7 +55,7 @@ __global__ __launch_bounds__(256) void reduce_partials_kernel(const double *__re
         a += __shfl_down(a, off);
         b += __shfl_down(b, off);
     }
-    __shared__ double red[2][4];
+    __shared__ double red[2][16];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     if (lane == 0) {
         red[0][wave] = a;
@@ -61,15 +63,19 @@ __global__ __launch_bounds__(256) void reduce_partials_kernel(const double *__re
     }
     __syncthreads();
     if (threadIdx.x == 0) {
-        sums[2 * blockIdx.x] = ((red[0][0] + red[0][1]) + red[0][2]) + red[0][3];
-        sums[2 * blockIdx.x + 1] = ((red[1][0] + red[1][1]) + red[1][2]) + red[1][3];
+        for (int w = 1; w < 16; w++) {
+            a += red[0][w];
+            b += red[1][w];
+        }
+        sums[2 * blockIdx.x] = a;
+        sums[2 * blockIdx.x + 1] = b;
     }
 }
 
 void launch_reduce_partials(const double *partial, int nblocks, int C, double *sums,
                             hipStream_t st) {
     if (C <= 0) return;
-    hipLaunchKernelGGL(reduce_partials_kernel, dim3(C), dim3(256), 0, st, partial, nblocks, sums);
+    hipLaunchKernelGGL(reduce_partials_kernel, dim3(C), dim3(1024), 0, st, partial, nblocks, sums);
     OF2D_HIP(hipGetLastError());
 }
 

@@ -114,24 +114,39 @@ void launch_motion_exp(float2 *f, float2 *scratch, int dimx, int dimy, int P, in
 
 // ---------------------------------------------------------------- Fluid / Elastic
 int sor_nstrips(int dimx);
-// in-place Gauss-Seidel SOR sweep (OpticalFlowFluid.cpp:7-41), wavefront-exact.
-// fused: b = force(u_or_b = motion, dI, It) per pixel; else u_or_b is b.
-// H: nstrips*dimy*2 granules (zeroed once); epoch: > every earlier epoch on H;
+// The SOR working array vb is stored skewed along the Gauss-Seidel wavefront:
+// pixel (i, j) at row 2i + j, column i, pitch P (fluid_kernels.hip).  It has
+// sor_rows(dimx, dimy) rows; the last kSorPadRows are padding for lanes that
+// run past the image (as do the kSorPadRows above and below each granule region).
+constexpr int kSorPadRows = 256;
+__host__ __device__ inline long sor_index(int i, int j, int P) {
+    return (2L * i + j) * P + i;
+}
+inline int sor_rows(int dimx, int dimy) { return 2 * dimx + dimy + kSorPadRows; }
+long sor_granule_stride(int dimy);
+// (nstrips + 1) regions of 16-B granules, zeroed once
+size_t sor_granule_bytes(int dimx, int dimy);
+// in-place Gauss-Seidel SOR sweep (OpticalFlowFluid.cpp:7-41), wavefront-exact,
+// on the skewed vb = {v.x, v.y, b.x, b.y} (sor_rows rows of pitch P).
+// epoch: > every earlier epoch on H, the same epoch as the sor_pack before it;
 // ticket: per-H counter, a multiple of nstrips before the launch.
-void launch_sor(float2 *v, const float2 *u_or_b, const float2 *dI, const float *It, bool fused,
-                int dimx, int dimy, int P, float mu, float lambda, float omega,
-                unsigned long long *H, unsigned epoch, unsigned *ticket, unsigned *status,
-                hipStream_t st);
+void launch_sor(float4 *vb, int dimx, int dimy, int P, float mu, float lambda, float omega,
+                void *H, unsigned epoch, unsigned *ticket, unsigned *status, hipStream_t st);
+// vb.zw <- force(u, dI, It); if v != nullptr also vb.xy <- v; granule region 0
+// <- column 0 of vb.xy tagged with epoch
+void launch_sor_pack(float4 *vb, const float2 *u, const float2 *dI, const float *It,
+                     const float2 *v, int dimx, int dimy, int P, void *H, unsigned epoch,
+                     hipStream_t st);
 void launch_force(const float2 *u, const float2 *dI, const float *It, float2 *f, int dimx,
                   int dimy, int P, hipStream_t st);
 int increment_nblocks(int dimx, int dimy);
 // R and scal[0] = maxabs(R), scal[1] = 0.65f / maxabs
-void launch_increment(const float2 *u, const float2 *vel, float2 *R, int dimx, int dimy, int P,
+void launch_increment(const float2 *u, const float4 *vel, float2 *R, int dimx, int dimy, int P,
                       float *part, float *scal, hipStream_t st);
 void launch_integrate_logger(float2 *u, const float2 *R, float2 *prev, const float *scal,
                              int dimx, int dimy, int P, double *partial, hipStream_t st);
-void launch_logger(const float2 *u, float2 *prev, int dimx, int dimy, int P, double *partial,
-                   hipStream_t st);
+void launch_logger(const float4 *vb, float2 *u, float2 *prev, int dimx, int dimy, int P,
+                   double *partial, hipStream_t st);
 void launch_jacobian_min(const float2 *u, int dimx, int dimy, int P, float *part, float *out,
                          hipStream_t st);
 

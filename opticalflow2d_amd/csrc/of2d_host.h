@@ -114,6 +114,7 @@ struct Level {
     Field<float2> est[3];
     Field<float2> force, velocity, increment, corr, tmp;
     Field<double> rhs;  // curvature spectral buffers (2 components)
+    Field<float4> vb;                   // SOR working array {v, b} (Fluid: persistent velocity)
     DevArray<unsigned long long> sorH;  // SOR strip hand-off granules
     DevArray<unsigned> sorTicket;       // SOR strip ticket (multiple of nstrips between sweeps)
     DevArray<float> part;               // per-block float partials (max / min reductions)

@@ -26,13 +26,11 @@ void alloc_level(Level &L, int reg) {
         case 5:  // + OpticalFlowFluid velocity / increment (OpticalFlowFluid.cpp:50-51)
             L.force.alloc(L.dx, L.dy);
             L.tmp.alloc(L.dx, L.dy);
-            L.sorH.alloc((size_t)std::max(sor_nstrips(L.dx), 1) * L.dy * 2);
+            L.sorH.alloc(sor_granule_bytes(L.dx, L.dy) / sizeof(unsigned long long));
             L.sorTicket.alloc(1);
             L.part.alloc((size_t)increment_nblocks(L.dx, L.dy));
-            if (reg == 5) {
-                L.velocity.alloc(L.dx, L.dy);
-                L.increment.alloc(L.dx, L.dy);
-            }
+            L.vb.alloc(L.dx, sor_rows(L.dx, L.dy));  // skewed; Fluid: the velocity is vb.xy
+            if (reg == 5) L.increment.alloc(L.dx, L.dy);
             break;
         case 1:
             L.force.alloc(L.dx, L.dy);
@@ -164,9 +162,12 @@ int Registration::loop_fluid(Level &L, int niter) {
     last_err_.clear();
     int iter;
     for (iter = 0; iter < niter; iter++) {
-        launch_sor(L.velocity.p, est, L.dI.p, L.It.p, true, L.dx, L.dy, L.P, mu, lambda, omega,
-                   L.sorH.p, ++epoch_, L.sorTicket.p, d_status_, st_);
-        launch_increment(est, L.velocity.p, L.increment.p, L.dx, L.dy, L.P, L.part.p, scal, st_);
+        // get_force(force, motion) into vb.zw, then the SOR sweep of the velocity vb.xy
+        const unsigned ep = ++epoch_;
+        launch_sor_pack(L.vb.p, est, L.dI.p, L.It.p, nullptr, L.dx, L.dy, L.P, L.sorH.p, ep, st_);
+        launch_sor(L.vb.p, L.dx, L.dy, L.P, mu, lambda, omega, L.sorH.p, ep, L.sorTicket.p,
+                   d_status_, st_);
+        launch_increment(est, L.vb.p, L.increment.p, L.dx, L.dy, L.P, L.part.p, scal, st_);
         launch_integrate_logger(est, L.increment.p, prev, scal, L.dx, L.dy, L.P, d_partial_, st_);
         launch_reduce_partials(d_partial_, nb, 1, d_sums_, st_);
         launch_jacobian_min(est, L.dx, L.dy, L.P, L.part.p, scal + 2, st_);
@@ -209,10 +210,13 @@ int Registration::loop_elastic(Level &L, int niter, int &final_buf) {
     L.tmp.zero(st_);
     const int nb = increment_nblocks(L.dx, L.dy);
     const double npx = (double)L.dx * L.dy;
+    // get_force(force, motion) then the SOR sweep of the motion itself: pack
+    // {u, force} into vb, sweep, unpack (the unpack is fused into the Logger pass)
     auto update = [&]() {
-        launch_force(est, L.dI.p, L.It.p, L.force.p, L.dx, L.dy, L.P, st_);
-        launch_sor(est, L.force.p, L.dI.p, L.It.p, false, L.dx, L.dy, L.P, mu, lambda, omega,
-                   L.sorH.p, ++epoch_, L.sorTicket.p, d_status_, st_);
+        const unsigned ep = ++epoch_;
+        launch_sor_pack(L.vb.p, est, L.dI.p, L.It.p, est, L.dx, L.dy, L.P, L.sorH.p, ep, st_);
+        launch_sor(L.vb.p, L.dx, L.dy, L.P, mu, lambda, omega, L.sorH.p, ep, L.sorTicket.p,
+                   d_status_, st_);
     };
     last_err_.clear();
     final_buf = 0;
@@ -223,7 +227,8 @@ int Registration::loop_elastic(Level &L, int niter, int &final_buf) {
                                 hipMemcpyDeviceToDevice, st_));
         for (int t = 0; t < C; t++) {
             update();
-            launch_logger(est, prev, L.dx, L.dy, L.P, d_partial_ + (size_t)t * nb * 2, st_);
+            launch_logger(L.vb.p, est, prev, L.dx, L.dy, L.P, d_partial_ + (size_t)t * nb * 2,
+                          st_);
         }
         launch_reduce_partials(d_partial_, nb, C, d_sums_, st_);
         OF2D_HIP(hipMemcpyAsync(hs_.sums, d_sums_, sizeof(double) * 2 * C, hipMemcpyDeviceToHost,
@@ -238,7 +243,10 @@ int Registration::loop_elastic(Level &L, int niter, int &final_buf) {
                 if (t < C - 1) {  // replay up to the break from the chunk's start state
                     OF2D_HIP(hipMemcpyAsync(L.est[0].base, L.est[1].base, L.est[0].bytes(),
                                             hipMemcpyDeviceToDevice, st_));
-                    for (int r = 0; r <= t; r++) update();
+                    for (int r = 0; r <= t; r++) {
+                        update();
+                        launch_logger(L.vb.p, est, prev, L.dx, L.dy, L.P, d_partial_, st_);
+                    }
                     check_status();
                 }
                 (void)snap;

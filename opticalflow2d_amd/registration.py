@@ -162,11 +162,18 @@ class ImageRegistration:
         self._chk(_lib.lib().of2d_set_option(self._h, key.encode(), float(value)))
 
     def register(self, Iref, Imov) -> None:
+        self.set_images(Iref, Imov)
+        self.estimate()
+
+    def set_images(self, Iref, Imov) -> None:
+        """Upload the image pair (the first half of register)."""
         n = self.dimx * self.dimy
         r, m = _col(Iref, n), _col(Imov, n)
-        L = _lib.lib()
-        self._chk(L.of2d_set_images(self._h, r, m))
-        self._chk(L.of2d_estimate(self._h))
+        self._chk(_lib.lib().of2d_set_images(self._h, r, m))
+
+    def estimate(self) -> None:
+        """Run the pyramid on the images already on the device."""
+        self._chk(_lib.lib().of2d_estimate(self._h))
 
     def motion(self) -> np.ndarray:
         out = np.zeros(self.dimx * self.dimy * 2, np.float64)

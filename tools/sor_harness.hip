@@ -1,0 +1,83 @@
+// SOR wavefront timeline harness: runs sor_strip_kernel on a synthetic
+// {v, b} field and prints per-strip start/end times and polled batches.
+//   hipcc -O3 -ffp-contract=off --offload-arch=gfx950 -I opticalflow2d_amd/csrc \
+//         tools/sor_harness.hip -o tools/sor_harness
+//   tools/sor_harness DIMX DIMY [REPS]
+#include "../opticalflow2d_amd/csrc/fluid_kernels.hip"
+
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+using namespace of2d;
+
+int main(int argc, char **argv) {
+    const int dimx = argc > 1 ? atoi(argv[1]) : 8192, dimy = argc > 2 ? atoi(argv[2]) : 8192;
+    const int reps = argc > 3 ? atoi(argv[3]) : 5;
+    const int P = pitch_for(dimx), ns = sor_nstrips(dimx);
+    const size_t rows = (size_t)sor_rows(dimx, dimy) + 1;
+    std::vector<float4> h((size_t)rows * P);
+    unsigned x = 12345;
+    for (auto &q : h) {
+        auto rnd = [&]() { x = x * 1664525u + 1013904223u; return (x >> 8) * (1.0f / 16777216.0f) - 0.5f; };
+        q = make_float4(rnd(), rnd(), rnd(), rnd());
+    }
+    float4 *vb;
+    void *H;
+    unsigned *ticket, *status;
+    unsigned long long *trace;
+    OF2D_HIP(hipMalloc(&vb, h.size() * sizeof(float4)));
+    OF2D_HIP(hipMemcpy(vb, h.data(), h.size() * sizeof(float4), hipMemcpyHostToDevice));
+    OF2D_HIP(hipMalloc(&H, sor_granule_bytes(dimx, dimy)));
+    OF2D_HIP(hipMemset(H, 0, sor_granule_bytes(dimx, dimy)));
+    OF2D_HIP(hipMalloc(&ticket, 4));
+    OF2D_HIP(hipMalloc(&status, 4));
+    OF2D_HIP(hipMemset(ticket, 0, 4));
+    OF2D_HIP(hipMemset(status, 0, 4));
+    OF2D_HIP(hipMalloc(&trace, 24 * (size_t)ns));
+    float4 *vb0 = vb;
+    const float A = 1.0f - 0.66f, B = 0.66f / (-6 * 0.25f), M = 0.25f, ML = 0.25f;
+    hipEvent_t e0, e1;
+    hipEventCreate(&e0);
+    hipEventCreate(&e1);
+    std::vector<unsigned long long> tr(3 * (size_t)ns);
+    for (int r = 0; r < reps; r++) {
+        const unsigned epoch = r + 1;
+        // column-0 granules for strip 0 (what sor_pack writes)
+        hipLaunchKernelGGL(sor_pack_kernel, dim3((dimx + 63) / 64, (dimy + 3) / 4), dim3(64, 4), 0,
+                           0, vb0, (const float2 *)vb0, (const float2 *)vb0, (const float *)vb0,
+                           (const float2 *)nullptr, dimx, dimy, P, (v4u *)H, epoch);
+        hipEventRecord(e0, 0);
+        hipLaunchKernelGGL(sor_strip_kernel, dim3(ns), dim3(64), 0, 0, vb0, dimx, dimy, P, A, B,
+                           M, ML, (v4u *)H, sor_granule_stride(dimy), epoch, ticket, ns, status,
+                           trace);
+        hipEventRecord(e1, 0);
+        OF2D_HIP(hipDeviceSynchronize());
+        float ms;
+        hipEventElapsedTime(&ms, e0, e1);
+        unsigned st;
+        OF2D_HIP(hipMemcpy(&st, status, 4, hipMemcpyDeviceToHost));
+        OF2D_HIP(hipMemcpy(tr.data(), trace, tr.size() * 8, hipMemcpyDeviceToHost));
+        unsigned long long t0 = ~0ull, t1 = 0, polls = 0;
+        for (int i = 0; i < ns; i++) {
+            t0 = std::min(t0, tr[3 * i]);
+            t1 = std::max(t1, tr[3 * i + 1]);
+            polls += tr[3 * i + 2];
+        }
+        const double steps = dimy + 126.0;
+        const double lag = ns > 1 ? (tr[3 * (ns - 1)] - tr[0]) * 0.01 / (ns - 1) : 0;  // us
+        double dur = 0;
+        for (int i = 0; i < ns; i++) dur += (tr[3 * i + 1] - tr[3 * i]) * 0.01;
+        dur /= ns;
+        printf("%dx%d strips %d: %.3f ms (timeline %.3f ms)  start lag %.2f us/strip  strip %.1f us"
+               " = %.1f ns/step  polled batches %llu  status %u\n",
+               dimx, dimy, ns, ms, (t1 - t0) * 1e-5, lag, dur, dur * 1e3 / steps, polls, st);
+        if (r == reps - 1 && ns > 1) {
+            printf("  strip: start_us end_us polls\n");
+            for (int i = 0; i < ns; i += std::max(1, ns / 12))
+                printf("  %4d: %9.2f %9.2f %llu\n", i, (tr[3 * i] - t0) * 0.01,
+                       (tr[3 * i + 1] - t0) * 0.01, tr[3 * i + 2]);
+        }
+    }
+    return 0;
+}
