@@ -112,6 +112,20 @@ void launch_motion_exp(float2 *f, float2 *scratch, int dimx, int dimy, int P, in
                        float *d_part, int nparts, int *d_nsq, float *d_maxabs, unsigned *status,
                        float2 **result, hipStream_t st);
 
+// ---------------------------------------------------------------- Curvature
+// C = A B (column-major fp64, MFMA), times E elementwise when E != nullptr;
+// batch z offsets A, B, C by sA, sB, sC elements
+void launch_dgemm(int M, int N, int K, const double *A, long lda, long sA, const double *B,
+                  long ldb, long sB, double *C, long ldc, long sC, const double *E, long lde,
+                  int batch, hipStream_t st);
+// X planes (x at 0, y at `plane`, pitch P) <- (double)(u - tau * force(u))
+void launch_curv_rhs(const float2 *u, const float2 *dI, const float *It, float tau, int dimx,
+                     int dimy, int P, double *X, long plane, hipStream_t st);
+int curv_nblocks(int dimx, int dimy);
+// out <- (float)Z / div, Logger partials against u
+void launch_curv_construct(const double *Z, long plane, const float2 *u, float2 *out, float div,
+                           int dimx, int dimy, int P, double *partial, hipStream_t st);
+
 // ---------------------------------------------------------------- Fluid / Elastic
 int sor_nstrips(int dimx);
 // The SOR working array vb is stored skewed along the Gauss-Seidel wavefront:

@@ -54,7 +54,10 @@ struct Field {
         P = pitch_for(dx);
         count = (size_t)(dy + 2 * ghost) * P + kPitchAlign;
         OF2D_HIP(hipMalloc(&base, count * sizeof(T)));
+        // the null-stream memset is unordered with the driver's non-blocking
+        // stream: finish it before anything is enqueued there
         OF2D_HIP(hipMemset(base, 0, count * sizeof(T)));
+        OF2D_HIP(hipDeviceSynchronize());
         p = base + (size_t)ghost * P;
     }
     void release() {
@@ -88,6 +91,7 @@ struct DevArray {
         n = count;
         OF2D_HIP(hipMalloc(&p, sizeof(T) * (count ? count : 1)));
         OF2D_HIP(hipMemset(p, 0, sizeof(T) * (count ? count : 1)));
+        OF2D_HIP(hipDeviceSynchronize());  // see Field::alloc
     }
 };
 
@@ -113,7 +117,9 @@ struct Level {
     Field<float2> dI;
     Field<float2> est[3];
     Field<float2> force, velocity, increment, corr, tmp;
-    Field<double> rhs;  // curvature spectral buffers (2 components)
+    DevArray<double> cbuf[2];              // Curvature: two x|y double plane pairs (pitch P)
+    DevArray<double> cC1T, cC0, cD1T, cD0;  // Curvature: REDFT10 / REDFT01 matrices
+    DevArray<double> cE;                    // Curvature: eigenvalues (pitch P)
     Field<float4> vb;                   // SOR working array {v, b} (Fluid: persistent velocity)
     DevArray<unsigned long long> sorH;  // SOR strip hand-off granules
     DevArray<unsigned> sorTicket;       // SOR strip ticket (multiple of nstrips between sweeps)

@@ -184,6 +184,7 @@ void Registration::ensure_device() {
     OF2D_HIP(hipMalloc(&d_status_, 64 * sizeof(unsigned)));
     OF2D_HIP(hipMemset(d_status_, 0, 64 * sizeof(unsigned)));
     OF2D_HIP(hipMalloc(&d_scalar_, (16 + 256) * sizeof(float)));
+    OF2D_HIP(hipDeviceSynchronize());  // null-stream memset vs the non-blocking stream
     hs_.ensure(std::max(chunk_, 64));
     ready_ = true;
 }

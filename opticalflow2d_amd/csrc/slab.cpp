@@ -145,6 +145,7 @@ int of2d_slab_create(of2d_slab **out, int dimx, int dimy, float alpha, int rank,
         OF2D_HIP(hipMalloc(&s->d_sums, sizeof(double) * 2 * s->chunk));
         OF2D_HIP(hipMalloc(&s->d_status, 64 * sizeof(unsigned)));
         OF2D_HIP(hipMemset(s->d_status, 0, 64 * sizeof(unsigned)));
+        OF2D_HIP(hipDeviceSynchronize());  // null-stream memset vs the non-blocking stream
         OF2D_HIP(hipMalloc(&s->d_stage, sizeof(double) * 2 * (size_t)dimx * (s->nrows + 2)));
         s->hs.ensure(s->chunk);
         if (nranks > 1) {

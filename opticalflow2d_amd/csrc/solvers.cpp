@@ -4,6 +4,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <vector>
 
 #include "of2d_host.h"
 #include "of2d_solvers.h"
@@ -32,8 +33,9 @@ void alloc_level(Level &L, int reg) {
             L.vb.alloc(L.dx, sor_rows(L.dx, L.dy));  // skewed; Fluid: the velocity is vb.xy
             if (reg == 5) L.increment.alloc(L.dx, L.dy);
             break;
-        case 1:
-            L.force.alloc(L.dx, L.dy);
+        case 1:  // OpticalFlowCurvature.cpp:36-56 (the force is fused into the rhs kernel)
+            L.cbuf[0].alloc(2 * (size_t)L.P * L.dy);
+            L.cbuf[1].alloc(2 * (size_t)L.P * L.dy);
             break;
         default:
             break;
@@ -43,6 +45,7 @@ void alloc_level(Level &L, int reg) {
 int max_partial_blocks(const Level &L, int reg) {
     if (reg == 3 || reg == 4) return conv_nblocks(L.dx, L.dy);
     if (reg == 2 || reg == 5) return increment_nblocks(L.dx, L.dy);
+    if (reg == 1) return curv_nblocks(L.dx, L.dy);
     return hs_nblocks(L.P, L.dy);
 }
 
@@ -258,8 +261,83 @@ int Registration::loop_elastic(Level &L, int niter, int &final_buf) {
     return niter;
 }
 
-int Registration::loop_curvature(Level &, int, int &) {
-    throw std::runtime_error("Curvature: not implemented yet");
+// Curvature (OpticalFlowCurvature.cpp:144-167) inside the ImageRegistrationOpticalFlow
+// loop.  The transform matrices and eigenvalues depend only on the level's
+// dimensions and the parameters, so they are built once per level on the host
+// in double (the reference's eigenvalue expression, OpticalFlowCurvature.cpp:6-30;
+// the REDFT10 / REDFT01 definitions for the transforms) and uploaded.
+namespace {
+void build_curvature(Level &L, float alpha, float tau, hipStream_t st) {
+    if (L.cE.p) return;
+    const int n0 = L.dx, n1 = L.dy, P = L.P;
+    const double PI_ = 3.14159265;  // OpticalFlowCurvature.cpp:4
+    std::vector<double> h;
+    auto upload = [&](DevArray<double> &d) {
+        d.alloc(h.size());
+        OF2D_HIP(hipMemcpyAsync(d.p, h.data(), h.size() * sizeof(double), hipMemcpyHostToDevice,
+                                st));
+        OF2D_HIP(hipStreamSynchronize(st));
+    };
+    // REDFT10 along an axis of length n: Y_k = sum_j 2 cos(pi (j + 1/2) k / n) X_j
+    auto c10 = [](int k, int j, int n) {
+        return 2.0 * std::cos(M_PI * ((double)j + 0.5) * (double)k / (double)n);
+    };
+    // REDFT01: Y_k = X_0 + sum_{j>=1} 2 cos(pi j (k + 1/2) / n) X_j
+    auto c01 = [](int k, int j, int n) {
+        return j == 0 ? 1.0 : 2.0 * std::cos(M_PI * (double)j * ((double)k + 0.5) / (double)n);
+    };
+    // right factors (axis y), column-major n1 x n1: M^T[j][q] = M[q][j]
+    h.assign((size_t)n1 * n1, 0.0);
+    for (int q = 0; q < n1; q++)
+        for (int j = 0; j < n1; j++) h[j + (size_t)q * n1] = c10(q, j, n1);
+    upload(L.cC1T);
+    for (int q = 0; q < n1; q++)
+        for (int j = 0; j < n1; j++) h[j + (size_t)q * n1] = c01(q, j, n1);
+    upload(L.cD1T);
+    // left factors (axis x), column-major n0 x n0 with leading dimension P
+    h.assign((size_t)P * n0, 0.0);
+    for (int i = 0; i < n0; i++)
+        for (int k = 0; k < n0; k++) h[k + (size_t)i * P] = c10(k, i, n0);
+    upload(L.cC0);
+    for (int i = 0; i < n0; i++)
+        for (int k = 0; k < n0; k++) h[k + (size_t)i * P] = c01(k, i, n0);
+    upload(L.cD0);
+    // eigenvalues 1 / (1 + tau alpha (-4 + 2 cos(p pi / nx) + 2 cos(q pi / ny))^2)
+    h.assign((size_t)P * n1, 0.0);
+    const float ta = tau * alpha;
+    for (int p = 0; p < n0; p++)
+        for (int q = 0; q < n1; q++) {
+            const double lam = -4 + 2 * std::cos((unsigned)p * PI_ / (unsigned)n0) +
+                               2 * std::cos((unsigned)q * PI_ / (unsigned)n1);
+            h[p + (size_t)q * P] = 1.0f / (1.0f + ta * std::pow(lam, 2));
+        }
+    upload(L.cE);
+}
+}  // namespace
+
+int Registration::loop_curvature(Level &L, int niter, int &final_buf) {
+    const float alpha = params_[0];
+    const float tau = params_.size() == 1 ? 1.0f : params_[1];  // OpticalFlowCurvature.h:8
+    build_curvature(L, alpha, tau, st_);
+    const int n0 = L.dx, n1 = L.dy, P = L.P;
+    const long plane = (long)P * n1;
+    const float div = 4.0f * (float)((unsigned)n0 * (unsigned)n1);  // 4.0f*sizein
+    double *X = L.cbuf[0].p, *T = L.cbuf[1].p;
+    return run_chunked(
+        L, niter, curv_nblocks(n0, n1),
+        [&](const float2 *src, float2 *dst, double *partial) {
+            launch_curv_rhs(src, L.dI.p, L.It.p, tau, n0, n1, P, X, plane, st_);
+            // forward REDFT10 x REDFT10 (axis y, then axis x with the eigenvalues)
+            launch_dgemm(n0, n1, n1, X, P, plane, L.cC1T.p, n1, 0, T, P, plane, nullptr, 0, 2,
+                         st_);
+            launch_dgemm(n0, n1, n0, L.cC0.p, P, 0, T, P, plane, X, P, plane, L.cE.p, P, 2, st_);
+            // inverse REDFT01 x REDFT01
+            launch_dgemm(n0, n1, n1, X, P, plane, L.cD1T.p, n1, 0, T, P, plane, nullptr, 0, 2,
+                         st_);
+            launch_dgemm(n0, n1, n0, L.cD0.p, P, 0, T, P, plane, X, P, plane, nullptr, 0, 2, st_);
+            launch_curv_construct(X, plane, src, dst, div, n0, n1, P, partial, st_);
+        },
+        final_buf);
 }
 
 }  // namespace of2d

@@ -697,6 +697,13 @@ static void dct_axis(double *a, unsigned n0, unsigned n1, int axis, int kind) {
     free(res);
 }
 
+/* separable 2-D transform of a row-major n0 x n1 array, axis 1 then axis 0
+ * (kind 10: REDFT10, kind 1: REDFT01), as Curvature applies it */
+void oracle_dct2d(double *a, int n0, int n1, int kind) {
+    dct_axis(a, (unsigned)n0, (unsigned)n1, 1, kind);
+    dct_axis(a, (unsigned)n0, (unsigned)n1, 0, kind);
+}
+
 /* ------------------------------------------------------------------ registration */
 enum { R_DIFFUSION = 0, R_CURVATURE, R_ELASTIC, R_THIRION, R_DIFFEO, R_FLUID };
 

@@ -75,6 +75,7 @@ void oracle_motion_exp(float *u, int dimx, int dimy);
 void oracle_sor_sweep(float *x, const float *b, int dimx, int dimy, float mu, float lambda,
                       float omega);
 void oracle_get_force(const float *u, const float *dI, const float *It, int n, float *f);
+void oracle_dct2d(double *a, int n0, int n1, int kind);
 void oracle_fluid_increment(const float *u, const float *v, int dimx, int dimy, float *R);
 
 /* thread/loop-order knob for the CPU baseline: 1 = reference loop order

@@ -81,6 +81,7 @@ def lib():
             "oracle_motion_exp": (None, [_f32p, i, i]),
             "oracle_sor_sweep": (None, [_f32p, _f32p, i, i, f, f, f]),
             "oracle_get_force": (None, [_f32p, _f32p, _f32p, i, _f32p]),
+            "oracle_dct2d": (None, [_f64p, i, i, i]),
             "oracle_fluid_increment": (None, [_f32p, _f32p, i, i, _f32p]),
             "oracle_set_reference_loop_order": (None, [i]),
         }

@@ -141,3 +141,19 @@ def test_invalid_parameters(oracle):
         oracle.Registration((16, 16), [3], 0, 0, [0.1, 0.2], 1, 0)
     with pytest.raises(oracle.OracleError, match="invalid regularisation"):
         oracle.Registration((16, 16), [3], 0, 7, [0.1], 1, 0)
+
+
+@pytest.mark.parametrize("shape", [(8, 8), (5, 4), (37, 70)])
+def test_curvature_dct_matches_r2r_definitions(oracle, shape):
+    """The oracle's REDFT10/REDFT01 (Curvature's FFTW plans, OpticalFlowCurvature.cpp:52-55)
+    against scipy's unnormalised DCT-II/III, an independent implementation of the
+    same published r2r definitions.  FFTW itself is absent, so this pins the
+    definitions, not FFTW's rounding."""
+    scipy_fft = pytest.importorskip("scipy.fft")
+    n0, n1 = shape
+    a = np.random.default_rng(n0 * 100 + n1).random(shape)
+    for kind, dct_type in ((10, 2), (1, 3)):
+        b = np.ascontiguousarray(a.copy())
+        oracle.lib().oracle_dct2d(b, n0, n1, kind)
+        want = scipy_fft.dct(scipy_fft.dct(a, type=dct_type, axis=1), type=dct_type, axis=0)
+        np.testing.assert_allclose(b, want, rtol=1e-12, atol=1e-12 * np.abs(want).max())
