@@ -28,6 +28,7 @@ namespace {
 constexpr int kCx = 64;  // conv tile: 64 px wide
 constexpr int kCy = 16;  // 16 j-lines high (4 per thread row)
 constexpr int kCThreadsY = 4;
+static_assert(kCy / kCThreadsY == 4, "conv4 computes four j-lines per thread");
 
 // warp2d value of Imov at pixel (a, b) with motion u (Image.cpp:137-174)
 __device__ __forceinline__ float warped_at(const float *__restrict__ Imov,
@@ -65,44 +66,120 @@ __device__ __forceinline__ float warped_at(const float *__restrict__ Imov,
 }
 }  // namespace
 
+// Block: 64 x 4 threads, a 64 x kFy output tile (kFy/4 j-lines per thread).
+// The warped image is computed ONCE per pixel of the tile plus a one-pixel
+// halo into LDS (1.16 warps per output pixel instead of 5), then the central
+// differences, It and the force come from LDS.
+constexpr int kFy = 16;
 __global__ __launch_bounds__(256) void demons_force_kernel(
     const float *__restrict__ Iref, const float *__restrict__ Imov, const float2 *__restrict__ u,
     float2 *__restrict__ corr, int dimx, int dimy, int P, float sigma_isq, float sigma_xsq,
     unsigned *__restrict__ status) {
-    const int i = blockIdx.x * 64 + threadIdx.x;
-    const int j = blockIdx.y * 4 + threadIdx.y;
-    if (i >= dimx || j >= dimy) return;
-    const float w0 = warped_at(Imov, u, i, j, dimx, dimy, P);
-    float gx, gy;
-    if (i == 0)
-        gx = warped_at(Imov, u, i + 1, j, dimx, dimy, P) - w0;
-    else if (i == dimx - 1)
-        gx = w0 - warped_at(Imov, u, i - 1, j, dimx, dimy, P);
-    else
-        gx = (warped_at(Imov, u, i + 1, j, dimx, dimy, P) -
-              warped_at(Imov, u, i - 1, j, dimx, dimy, P)) /
-             2.0f;
-    if (j == 0)
-        gy = warped_at(Imov, u, i, j + 1, dimx, dimy, P) - w0;
-    else if (j == dimy - 1)
-        gy = w0 - warped_at(Imov, u, i, j - 1, dimx, dimy, P);
-    else
-        gy = (warped_at(Imov, u, i, j + 1, dimx, dimy, P) -
-              warped_at(Imov, u, i, j - 1, dimx, dimy, P)) /
-             2.0f;
-    const long idx = (long)j * P + i;
-    const float it = w0 - Iref[idx];
-    // Demons.cpp:57: dI * It / (dI.x^2 + dI.y^2 + It*It*sigma_isq/sigma_xsq) * -1
-    const float den = (gx * gx + gy * gy) + ((it * it) * sigma_isq) / sigma_xsq;
-    if (den == 0.0f) atomicOr(status, kStatusDivZero);
-    corr[idx] = make_float2(((gx * it) / den) * -1.0f, ((gy * it) / den) * -1.0f);
+    constexpr int TW = 64 + 2, TH = kFy + 2;
+    __shared__ float w[TH][TW];
+    const int x0 = blockIdx.x * 64, y0 = blockIdx.y * kFy;
+    const int tid = threadIdx.y * 64 + threadIdx.x;
+    // warp the tile + halo, all loads of a thread's slots issued together
+    // (the same arithmetic as warped_at / Image.cpp:137-174)
+    constexpr int NS = (TW * TH + 255) / 256;
+    float2 m[NS];
+    float own[NS];
+    long idx[NS];
+    bool in[NS];
+#pragma unroll
+    for (int q = 0; q < NS; q++) {
+        const int s = tid + 256 * q, r = s / TW, c = s - r * TW;
+        const int a = x0 - 1 + c, b = y0 - 1 + r;
+        in[q] = s < TW * TH && a >= 0 && a < dimx && b >= 0 && b < dimy;
+        idx[q] = (long)b * P + a;
+        m[q] = in[q] ? u[idx[q]] : make_float2(0.0f, 0.0f);
+        own[q] = in[q] ? Imov[idx[q]] : 0.0f;
+    }
+    float t00[NS], t10[NS], t01[NS], t11[NS], fx[NS], fy[NS];
+    bool ok[NS], ax[NS], ay[NS];
+#pragma unroll
+    for (int q = 0; q < NS; q++) {
+        const int s = tid + 256 * q, r = s / TW, c = s - r * TW;
+        const int a = x0 - 1 + c, b = y0 - 1 + r;
+        const float px = (float)a + m[q].x;
+        const int dx = (int)floorf(px);
+        fx[q] = px - (float)dx;
+        const float py = (float)b + m[q].y;
+        const int dy = (int)floorf(py);
+        fy[q] = py - (float)dy;
+        ok[q] = in[q] && !(dx < 0 || dx >= dimx || dy < 0 || dy >= dimy);
+        ax[q] = dx < dimx - 1;
+        ay[q] = dy < dimy - 1;
+        const float *g = Imov + (long)dy * P + dx;
+        t00[q] = ok[q] ? g[0] : 0.0f;
+        t10[q] = ok[q] && ax[q] ? g[1] : 0.0f;
+        t01[q] = ok[q] && ay[q] ? g[P] : 0.0f;
+        t11[q] = ok[q] && ax[q] && ay[q] ? g[P + 1] : 0.0f;
+    }
+#pragma unroll
+    for (int q = 0; q < NS; q++) {
+        if (!in[q]) continue;
+        const int s = tid + 256 * q, r = s / TW, c = s - r * TW;
+        float out = own[q];
+        if (ok[q]) {
+            const float gx = fx[q], gy = fy[q];
+            float val = (t00[q] * (1 - gx)) * (1 - gy);
+            float wt = (1 - gx) * (1 - gy);
+            if (ax[q]) {
+                val += (t10[q] * gx) * (1 - gy);
+                wt += gx * (1 - gy);
+            }
+            if (ay[q]) {
+                val += (t01[q] * (1 - gx)) * gy;
+                wt += (1 - gx) * gy;
+            }
+            if (ax[q] && ay[q]) {
+                val += (t11[q] * gx) * gy;
+                wt += gx * gy;
+            }
+            if (wt != 0) out = val / wt;
+        }
+        w[r][c] = out;
+    }
+    __syncthreads();
+    const int i = x0 + threadIdx.x;
+    if (i >= dimx) return;
+    const int c = threadIdx.x + 1;
+    bool zero = false;
+    for (int rr = threadIdx.y; rr < kFy; rr += 4) {
+        const int j = y0 + rr;
+        if (j >= dimy) break;
+        const int r = rr + 1;
+        const float w0 = w[r][c];
+        float gx, gy;
+        if (i == 0)
+            gx = w[r][c + 1] - w0;
+        else if (i == dimx - 1)
+            gx = w0 - w[r][c - 1];
+        else
+            gx = (w[r][c + 1] - w[r][c - 1]) / 2.0f;
+        if (j == 0)
+            gy = w[r + 1][c] - w0;
+        else if (j == dimy - 1)
+            gy = w0 - w[r - 1][c];
+        else
+            gy = (w[r + 1][c] - w[r - 1][c]) / 2.0f;
+        const long idx = (long)j * P + i;
+        const float it = w0 - Iref[idx];
+        // Demons.cpp:57: dI * It / (dI.x^2 + dI.y^2 + It*It*sigma_isq/sigma_xsq) * -1
+        const float den = (gx * gx + gy * gy) + ((it * it) * sigma_isq) / sigma_xsq;
+        zero |= den == 0.0f;
+        corr[idx] = make_float2(((gx * it) / den) * -1.0f, ((gy * it) / den) * -1.0f);
+    }
+    if (zero) atomicOr(status, kStatusDivZero);
 }
 
 void launch_demons_force(const float *Iref, const float *Imov, const float2 *u, float2 *corr,
                          int dimx, int dimy, int P, float sigma_isq, float sigma_xsq,
                          unsigned *status, hipStream_t st) {
-    hipLaunchKernelGGL(demons_force_kernel, dim3((dimx + 63) / 64, (dimy + 3) / 4), dim3(64, 4),
-                       0, st, Iref, Imov, u, corr, dimx, dimy, P, sigma_isq, sigma_xsq, status);
+    hipLaunchKernelGGL(demons_force_kernel, dim3((dimx + 63) / 64, (dimy + kFy - 1) / kFy),
+                       dim3(64, 4), 0, st, Iref, Imov, u, corr, dimx, dimy, P, sigma_isq,
+                       sigma_xsq, status);
     OF2D_HIP(hipGetLastError());
 }
 
@@ -118,49 +195,84 @@ struct ConvArgs {
     double wfull;  // sum of all weights in the reference's order (interior pixels)
 };
 
+template <int KW>
 __device__ __forceinline__ void conv_load_tile(float2 *tile, const float2 *__restrict__ f,
                                                int dimx, int dimy, int P, int x0, int y0,
-                                               int cx, int cy) {
+                                               int cx_rt, int cy_rt) {
+    const int cx = KW > 0 ? (KW - 1) / 2 : cx_rt, cy = KW > 0 ? (KW - 1) / 2 : cy_rt;
     const int TW = kCx + 2 * cx, TH = kCy + 2 * cy;
     const long N = (long)dimx * dimy;
     const int tid = threadIdx.y * 64 + threadIdx.x;
-    for (int s = tid; s < TW * TH; s += 256) {
+    // slot (r, c) <- f[L], L = row * dimx + col with col within cx of [0, dimx):
+    // the j-line of L is row - 1, row or row + 1 (no 64-bit division)
+    auto fetch = [&](int s) {
         const int r = s / TW, c = s - r * TW;
-        const long L = (long)(y0 - cy + r) * dimx + (x0 - cx + c);
-        float2 v = make_float2(0.0f, 0.0f);
-        if (L >= 0 && L < N) {
-            const long row = L / dimx, col = L - row * dimx;
-            v = f[row * P + col];
+        int row = y0 - cy + r, col = x0 - cx + c;
+        while (col < 0) {  // once unless cx > dimx
+            col += dimx;
+            row -= 1;
         }
-        tile[s] = v;
+        while (col >= dimx) {
+            col -= dimx;
+            row += 1;
+        }
+        const long L = (long)row * dimx + col;
+        return (L >= 0 && L < N) ? f[(long)row * P + col] : make_float2(0.0f, 0.0f);
+    };
+    if constexpr (KW > 0) {
+        // compile-time tile: every load of the thread in flight at once
+        constexpr int TWc = kCx + 2 * ((KW - 1) / 2), THc = kCy + 2 * ((KW - 1) / 2);
+        constexpr int NS = (TWc * THc + 255) / 256;
+        float2 v[NS];
+#pragma unroll
+        for (int q = 0; q < NS; q++) {
+            const int s = tid + 256 * q;
+            v[q] = s < TWc * THc ? fetch(s) : make_float2(0.0f, 0.0f);
+        }
+#pragma unroll
+        for (int q = 0; q < NS; q++) {
+            const int s = tid + 256 * q;
+            if (s < TWc * THc) tile[s] = v[q];
+        }
+    } else {
+        for (int s = tid; s < TW * TH; s += 256) tile[s] = fetch(s);
     }
 }
 
 // value of the reference's convolution at (i, j) from the LDS tile; returns
 // false when the weight sum is 0 (then the reference leaves the pixel as is)
+// KW > 0: kernel width known at compile time (taps unrolled, weights in
+// scalar registers); KW == 0: runtime width.
+template <int KW>
 __device__ __forceinline__ bool conv_px(const float2 *tile, const ConvArgs &a, int i, int j,
                                         int tx, int ty, int dimx, long N, float2 &out) {
-    const int TW = kCx + 2 * a.cx;
+    const int kw = KW > 0 ? KW : a.kw;
+    const int cx = KW > 0 ? (KW - 1) / 2 : a.cx, cy = KW > 0 ? (KW - 1) / 2 : a.cy;
+    const int TW = kCx + 2 * cx;
     const long lin = (long)j * dimx + i;
-    const bool interior = (lin - a.cx - (long)a.cy * dimx >= 0) && (lin + a.cx + (long)a.cy * dimx < N);
+    const bool interior = (lin - cx - (long)cy * dimx >= 0) && (lin + cx + (long)cy * dimx < N);
     float vx = 0.0f, vy = 0.0f;
     double weight = 0.0;
     if (interior) {
-        for (int ii = -a.cx; ii <= a.cx; ii++)
-            for (int jj = -a.cy; jj <= a.cy; jj++) {
-                const float2 t = tile[(ty + a.cy + jj) * TW + (tx + a.cx + ii)];
-                const float k = a.kf[(ii + a.cx) + (jj + a.cy) * a.kw];
+#pragma unroll
+        for (int ii = -cx; ii <= cx; ii++)
+#pragma unroll
+            for (int jj = -cy; jj <= cy; jj++) {
+                const float2 t = tile[(ty + cy + jj) * TW + (tx + cx + ii)];
+                const float k = a.kf[(ii + cx) + (jj + cy) * kw];
                 vx = vx + t.x * k;
                 vy = vy + t.y * k;
             }
         weight = a.wfull;
     } else {
-        for (int ii = -a.cx; ii <= a.cx; ii++)
-            for (int jj = -a.cy; jj <= a.cy; jj++) {
+#pragma unroll
+        for (int ii = -cx; ii <= cx; ii++)
+#pragma unroll
+            for (int jj = -cy; jj <= cy; jj++) {
                 const unsigned L = (unsigned)(i + ii) + (unsigned)(j + jj) * (unsigned)dimx;
                 if ((long)L >= N) continue;  // Field.tpp:245-247 (unsigned compare)
-                const float2 t = tile[(ty + a.cy + jj) * TW + (tx + a.cx + ii)];
-                const int ik = (ii + a.cx) + (jj + a.cy) * a.kw;
+                const float2 t = tile[(ty + cy + jj) * TW + (tx + cx + ii)];
+                const int ik = (ii + cx) + (jj + cy) * kw;
                 vx = vx + t.x * a.kf[ik];
                 vy = vy + t.y * a.kf[ik];
                 weight += a.kd[ik];
@@ -172,65 +284,148 @@ __device__ __forceinline__ bool conv_px(const float2 *tile, const ConvArgs &a, i
     return true;
 }
 
+// The convolution at four consecutive j-lines j0..j0+3 of column i.  When the
+// width is known and all four pixels are interior, the 4 + 2c tile values of
+// each tap column are read once and shared by the four outputs (each output
+// still sums ii outer / jj inner, the reference's order); otherwise per pixel.
+template <int KW>
+__device__ __forceinline__ void conv4(const float2 *tile, const ConvArgs &a, int i, int j0,
+                                      int tx, int ty0, int dimx, int dimy, long N, float2 res[4],
+                                      bool has[4]) {
+    if constexpr (KW > 0) {
+        constexpr int c = (KW - 1) / 2, TW = kCx + 2 * c;
+        const long lin0 = (long)j0 * dimx + i, lin3 = (long)(j0 + 3) * dimx + i;
+        if (j0 + 3 < dimy && lin0 - c - (long)c * dimx >= 0 && lin3 + c + (long)c * dimx < N) {
+            float vx[4] = {0.0f, 0.0f, 0.0f, 0.0f}, vy[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+            for (int ii = -c; ii <= c; ii++) {
+                float2 col[4 + 2 * c];
+#pragma unroll
+                for (int q = 0; q < 4 + 2 * c; q++) col[q] = tile[(ty0 + q) * TW + (tx + c + ii)];
+#pragma unroll
+                for (int k = 0; k < 4; k++)
+#pragma unroll
+                    for (int jj = -c; jj <= c; jj++) {
+                        const float kk = a.kf[(ii + c) + (jj + c) * KW];
+                        vx[k] = vx[k] + col[k + c + jj].x * kk;
+                        vy[k] = vy[k] + col[k + c + jj].y * kk;
+                    }
+            }
+            const float wf = (float)a.wfull;
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                has[k] = a.wfull != 0;
+                res[k] = make_float2(vx[k] / wf, vy[k] / wf);
+            }
+            return;
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        has[k] = false;
+        if (j0 + k < dimy) has[k] = conv_px<KW>(tile, a, i, j0 + k, tx, ty0 + k, dimx, N, res[k]);
+    }
+}
+
 // mode 0: Composition (Motion::accumulate), 1: Addition (Field::operator+=),
 // 2: neither (DemonsThirions.cpp:33-38 with another value), 3: store corr only
+template <int KW>
 __global__ __launch_bounds__(256) void smooth_compose_kernel(
     const float2 *__restrict__ corr, const float2 *__restrict__ u, float2 *__restrict__ out,
     int dimx, int dimy, int P, ConvArgs a, int mode) {
     extern __shared__ __attribute__((aligned(16))) float2 tile[];
     const int x0 = blockIdx.x * kCx, y0 = blockIdx.y * kCy;
-    conv_load_tile(tile, corr, dimx, dimy, P, x0, y0, a.cx, a.cy);
+    conv_load_tile<KW>(tile, corr, dimx, dimy, P, x0, y0, a.cx, a.cy);
     __syncthreads();
     const long N = (long)dimx * dimy;
     const int i = x0 + threadIdx.x;
     if (i >= dimx) return;
-    for (int r = threadIdx.y; r < kCy; r += kCThreadsY) {
-        const int j = y0 + r;
+    const int r0 = threadIdx.y * (kCy / kCThreadsY);  // four consecutive j-lines per thread
+    float2 sm[4];
+    bool has[4];
+    conv4<KW>(tile, a, i, y0 + r0, threadIdx.x, r0, dimx, dimy, N, sm, has);
+    float2 cv[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const int j = y0 + r0 + k;
+        cv[k] = make_float2(0.0f, 0.0f);
+        if (j < dimy) cv[k] = has[k] ? sm[k] : corr[(long)j * P + i];
+    }
+    if (mode == 0) {
+        // Motion::accumulate (Motion.cpp:113-178): u(x) <- c(x) + u_old(x + c(x)),
+        // bilinear with in-range taps renormalised; out of range keeps u_old(x).
+        // All gathers of the four pixels are issued before any is used.
+        float2 own[4], t00[4], t10[4], t01[4], t11[4];
+        float fx[4], fy[4];
+        bool ok[4], ax[4], ay[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const int j = y0 + r0 + k;
+            const bool in = j < dimy;
+            own[k] = in ? u[(long)j * P + i] : make_float2(0.0f, 0.0f);
+            const float px = (float)i + cv[k].x;
+            const int dx = (int)floorf(px);
+            fx[k] = px - (float)dx;
+            const float py = (float)j + cv[k].y;
+            const int dy = (int)floorf(py);
+            fy[k] = py - (float)dy;
+            ok[k] = in && !(dx < 0 || dx >= dimx || dy < 0 || dy >= dimy);
+            ax[k] = dx < dimx - 1;
+            ay[k] = dy < dimy - 1;
+            const float2 *b = u + (long)dy * P + dx;
+            const float2 z = make_float2(0.0f, 0.0f);
+            t00[k] = ok[k] ? b[0] : z;
+            t10[k] = ok[k] && ax[k] ? b[1] : z;
+            t01[k] = ok[k] && ay[k] ? b[P] : z;
+            t11[k] = ok[k] && ax[k] && ay[k] ? b[P + 1] : z;
+        }
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const int j = y0 + r0 + k;
+            if (j >= dimy) break;
+            const float2 c = cv[k];
+            float2 o = own[k];
+            if (ok[k]) {
+                o = c;
+                const float gx = fx[k], gy = fy[k];
+                float vx = (t00[k].x * (1 - gx)) * (1 - gy);
+                float vy = (t00[k].y * (1 - gx)) * (1 - gy);
+                float w = (1 - gx) * (1 - gy);
+                if (ax[k]) {
+                    vx = vx + (t10[k].x * gx) * (1 - gy);
+                    vy = vy + (t10[k].y * gx) * (1 - gy);
+                    w += gx * (1 - gy);
+                }
+                if (ay[k]) {
+                    vx = vx + (t01[k].x * (1 - gx)) * gy;
+                    vy = vy + (t01[k].y * (1 - gx)) * gy;
+                    w += (1 - gx) * gy;
+                }
+                if (ax[k] && ay[k]) {
+                    vx = vx + (t11[k].x * gx) * gy;
+                    vy = vy + (t11[k].y * gx) * gy;
+                    w += gx * gy;
+                }
+                if (w != 0) o = make_float2(c.x + vx / w, c.y + vy / w);
+            }
+            out[(long)j * P + i] = o;
+        }
+        return;
+    }
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const int j = y0 + r0 + k;
         if (j >= dimy) break;
         const long idx = (long)j * P + i;
-        float2 c = corr[idx];
-        float2 cs;
-        if (conv_px(tile, a, i, j, threadIdx.x, r, dimx, N, cs)) c = cs;
+        const float2 c = cv[k];
         float2 o;
         if (mode == 3) {
             o = c;
         } else if (mode == 1) {
             const float2 m = u[idx];
             o = make_float2(m.x + c.x, m.y + c.y);
-        } else if (mode == 2) {
-            o = u[idx];
         } else {
-            o = u[idx];  // out of range: keep u_old(x)
-            const float px = (float)i + c.x;
-            const int dx = (int)floorf(px);
-            const float fx = px - (float)dx;
-            const float py = (float)j + c.y;
-            const int dy = (int)floorf(py);
-            const float fy = py - (float)dy;
-            if (!(dx < 0 || dx >= dimx || dy < 0 || dy >= dimy)) {
-                o = c;
-                const float2 *b = u + (long)dy * P + dx;
-                float vx = (b[0].x * (1 - fx)) * (1 - fy);
-                float vy = (b[0].y * (1 - fx)) * (1 - fy);
-                float w = (1 - fx) * (1 - fy);
-                const bool ax = dx < dimx - 1, ay = dy < dimy - 1;
-                if (ax) {
-                    vx = vx + (b[1].x * fx) * (1 - fy);
-                    vy = vy + (b[1].y * fx) * (1 - fy);
-                    w += fx * (1 - fy);
-                }
-                if (ay) {
-                    vx = vx + (b[P].x * (1 - fx)) * fy;
-                    vy = vy + (b[P].y * (1 - fx)) * fy;
-                    w += (1 - fx) * fy;
-                }
-                if (ax && ay) {
-                    vx = vx + (b[P + 1].x * fx) * fy;
-                    vy = vy + (b[P + 1].y * fx) * fy;
-                    w += fx * fy;
-                }
-                if (w != 0) o = make_float2(c.x + vx / w, c.y + vy / w);
-            }
+            o = u[idx];
         }
         out[idx] = o;
     }
@@ -238,6 +433,7 @@ __global__ __launch_bounds__(256) void smooth_compose_kernel(
 
 // u_new = u_mid (*) G(sigma_diffusion); Logger partials sum ||u_new - prev||,
 // sum ||prev|| per block (fixed order)
+template <int KW>
 __global__ __launch_bounds__(256) void smooth_norm_kernel(const float2 *__restrict__ umid,
                                                           const float2 *__restrict__ prev,
                                                           float2 *__restrict__ out, int dimx,
@@ -245,19 +441,22 @@ __global__ __launch_bounds__(256) void smooth_norm_kernel(const float2 *__restri
                                                           double *__restrict__ partial) {
     extern __shared__ __attribute__((aligned(16))) float2 tile[];
     const int x0 = blockIdx.x * kCx, y0 = blockIdx.y * kCy;
-    conv_load_tile(tile, umid, dimx, dimy, P, x0, y0, a.cx, a.cy);
+    conv_load_tile<KW>(tile, umid, dimx, dimy, P, x0, y0, a.cx, a.cy);
     __syncthreads();
     const long N = (long)dimx * dimy;
     const int i = x0 + threadIdx.x;
     double sd = 0.0, sp = 0.0;
     if (i < dimx) {
-        for (int r = threadIdx.y; r < kCy; r += kCThreadsY) {
-            const int j = y0 + r;
+        const int r0 = threadIdx.y * (kCy / kCThreadsY);
+        float2 sm[4];
+        bool has[4];
+        conv4<KW>(tile, a, i, y0 + r0, threadIdx.x, r0, dimx, dimy, N, sm, has);
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const int j = y0 + r0 + k;
             if (j >= dimy) break;
             const long idx = (long)j * P + i;
-            float2 v = umid[idx];
-            float2 vs;
-            if (conv_px(tile, a, i, j, threadIdx.x, r, dimx, N, vs)) v = vs;
+            const float2 v = has[k] ? sm[k] : umid[idx];
             out[idx] = v;
             const float2 pv = prev[idx];
             const float ex = v.x - pv.x, ey = v.y - pv.y;
@@ -297,8 +496,16 @@ void launch_smooth_compose(const float2 *corr, const float2 *u, float2 *out, int
                            int mode, hipStream_t st) {
     const int c = (kw - 1) / 2;
     ConvArgs a{kf, kd, kw, c, c, wfull};
-    hipLaunchKernelGGL(smooth_compose_kernel, conv_grid(dimx, dimy), dim3(64, kCThreadsY),
-                       conv_lds_bytes(c, c), st, corr, u, out, dimx, dimy, P, a, mode);
+    auto go = [&](auto kern) {
+        hipLaunchKernelGGL(kern, conv_grid(dimx, dimy), dim3(64, kCThreadsY),
+                           conv_lds_bytes(c, c), st, corr, u, out, dimx, dimy, P, a, mode);
+    };
+    switch (kw) {
+        case 3: go(smooth_compose_kernel<3>); break;
+        case 5: go(smooth_compose_kernel<5>); break;
+        case 7: go(smooth_compose_kernel<7>); break;
+        default: go(smooth_compose_kernel<0>); break;
+    }
     OF2D_HIP(hipGetLastError());
 }
 
@@ -307,8 +514,16 @@ void launch_smooth_norm(const float2 *umid, const float2 *prev, float2 *out, int
                         double *partial, hipStream_t st) {
     const int c = (kw - 1) / 2;
     ConvArgs a{kf, kd, kw, c, c, wfull};
-    hipLaunchKernelGGL(smooth_norm_kernel, conv_grid(dimx, dimy), dim3(64, kCThreadsY),
-                       conv_lds_bytes(c, c), st, umid, prev, out, dimx, dimy, P, a, partial);
+    auto go = [&](auto kern) {
+        hipLaunchKernelGGL(kern, conv_grid(dimx, dimy), dim3(64, kCThreadsY),
+                           conv_lds_bytes(c, c), st, umid, prev, out, dimx, dimy, P, a, partial);
+    };
+    switch (kw) {
+        case 3: go(smooth_norm_kernel<3>); break;
+        case 5: go(smooth_norm_kernel<5>); break;
+        case 7: go(smooth_norm_kernel<7>); break;
+        default: go(smooth_norm_kernel<0>); break;
+    }
     OF2D_HIP(hipGetLastError());
 }
 
