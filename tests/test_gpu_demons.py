@@ -78,3 +78,14 @@ def test_demons_config3_scale_512(gpu, oracle):
     g, w = both(oracle, (512, 512), [40], 0, 3, [1.0, 0.25, 2.0, 2.0, 5, 0], 1, ref, mov)
     assert g["iters"] == w["iters"]
     assert np.array_equal(g["motion"], w["motion"])
+
+
+def test_demons_config3_full_size_4096(gpu, oracle):
+    """BASELINE config 3 at its full size (4096^2, its parameters), two fixed
+    iterations bit for bit."""
+    ref, mov = S.procedural_pair(4096, 0, 4096)
+    g, w = both(oracle, (4096, 4096), [2], 0, 3, [1.0, 0.25, 2.0, 2.0, 5, 0], 1, ref, mov,
+                fixed_iters=1)
+    assert g["iters"] == w["iters"] == [2]
+    assert np.array_equal(g["motion"], w["motion"])
+    assert np.array_equal(g["warped"], w["warped"])

@@ -96,3 +96,15 @@ def test_elastic_wide_sweep(gpu, oracle):
     g, w, _, _ = run_both(gpu, oracle, (1100, 300), [3], 0, 2, [0.3, 0.1], 1, ref, mov,
                           fixed_iters=1)
     assert np.array_equal(g["motion"], w["motion"])
+
+
+def test_fluid_config4_full_size_8192(gpu, oracle):
+    """BASELINE config 4 at its full size: 8192^2, 3-level pyramid, one fixed
+    iteration per level (130 wavefront strips at the finest level), bit for bit
+    with identical printed Dumax lines."""
+    ref, mov = S.shifted_disk(8192)
+    g, w, gt, ot = run_both(gpu, oracle, (8192, 8192), [1, 1, 1], 2, 5, [0.25, 0.0], 1, ref, mov,
+                            fixed_iters=1)
+    assert g["iters"] == w["iters"]
+    assert np.array_equal(g["motion"], w["motion"])
+    assert body(gt) == body(ot)

@@ -196,3 +196,25 @@ def test_slab_full_size_4096_bitwise(gpu, oracle):
     L.oracle_accumulate(motion, u, n, n)
     got = np.stack([m[:, :, 0].reshape(-1, order="F"), m[:, :, 1].reshape(-1, order="F")], 1)
     assert np.array_equal(got.astype(np.float32).reshape(-1), motion)
+
+
+def test_hs_16384_interior_matches_cropped_oracle(gpu, oracle):
+    """BASELINE config 5 grid (16384^2) on one GPU.  The oracle cannot run that
+    grid in test time, but a Jacobi iteration (and the gradients before it) only
+    reaches one pixel further per step, so after k fixed iterations every pixel
+    more than k + 2 px from a crop's cut edges equals the oracle run on the crop
+    alone (edges shared with the image keep the same border rule)."""
+    n, iters, c = 16384, 3, 160
+    ref, mov = S.procedural_pair(n, 0, n)
+    s = SlabSolver(n, n, 0.1)
+    s.set_images(ref, mov)
+    assert s.run(iters, fixed_iters=True) == iters
+    m = s.motion()
+    s.close()
+    margin = iters + 2
+    for x0, y0 in [(0, 0), (n // 2 - 77, 7001), (n - c, n - c), (0, n - c)]:
+        w = oracle_run(oracle, (c, c), [iters], 0, 0, [0.1], 1, ref[x0:x0 + c, y0:y0 + c],
+                       mov[x0:x0 + c, y0:y0 + c], fixed=True)["motion"]
+        xl, xh = (0 if x0 == 0 else margin), (c if x0 + c == n else c - margin)
+        yl, yh = (0 if y0 == 0 else margin), (c if y0 + c == n else c - margin)
+        assert np.array_equal(m[x0 + xl:x0 + xh, y0 + yl:y0 + yh], w[xl:xh, yl:yh]), (x0, y0)

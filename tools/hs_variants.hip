@@ -85,7 +85,7 @@ int main(int argc, char **argv) {
     const int iters = argc > 2 ? atoi(argv[2]) : 200;
     Bufs b;
     b.dimx = b.dimy = n;
-    b.P = (n + 255) / 256 * 256;
+    b.P = (n + 255) / 256 * 256 + (argc > 4 ? atoi(argv[4]) : 0);  // optional pitch padding
     const size_t rows = (size_t)n + 2;
     float2 *base0, *base1, *based;
     float *baset;
