@@ -28,6 +28,22 @@ namespace of2d {
 using HsKernel = decltype(&hs::jacobi_kernel<kHsRows, kHsPxl, kHsWaves, true, true, false>);
 static const HsKernel kHsJacobi = &hs::jacobi_kernel<kHsRows, kHsPxl, kHsWaves, true, true, false>;
 
+// Two iterations per launch (tools/hs_variants.hip "two": 32 j-lines, 4 waves
+// fastest; 51 us per iteration against 79 us for the single step at 4096^2).
+static const auto kHsJacobi2 = &hs::jacobi2_kernel<kHs2Rows, kHs2Waves>;
+
+void launch_hs_jacobi2(const float2 *u_old, float2 *u_new, const float2 *dI, const float *It,
+                       int P, int dimx, int nrows, int row0, int dimy, float alphasq, int glo,
+                       int ghi, double *partial, double *partial2, unsigned *status,
+                       hipStream_t st) {
+    if (P % kHsStrip != 0 || nrows <= 0 || dimx > P || dimx < 2 || glo > -1 || ghi < nrows + 1)
+        throw std::invalid_argument("launch_hs_jacobi2: bad geometry");
+    hipLaunchKernelGGL(kHsJacobi2, hs2_grid(dimx, nrows), dim3(64 * kHs2Waves), 0, st, u_old,
+                       u_new, dI, It, P, dimx, nrows, row0, dimy, alphasq, glo, ghi, partial,
+                       partial2, status);
+    OF2D_HIP(hipGetLastError());
+}
+
 void launch_hs_jacobi(const float2 *u_old, float2 *u_new, const float2 *dI, const float *It,
                       int P, int dimx, int nrows, int row0, int dimy, float alphasq,
                       double *partial, unsigned *status, hipStream_t st) {

@@ -62,6 +62,27 @@ inline int hs_nblocks(int P, int nrows) {
 void launch_hs_jacobi(const float2 *u_old, float2 *u_new, const float2 *dI, const float *It,
                       int P, int dimx, int nrows, int row0, int dimy, float alphasq,
                       double *partial, unsigned *status, hipStream_t st);
+// Two Jacobi iterations per launch (temporal blocking, hs::jacobi2_kernel):
+// u_new = step(step(u_old)), bit-identical to two launch_hs_jacobi calls.
+// Rows [glo, ghi) (relative to the first owned row; ghost j-lines included)
+// are readable: u and dI/It outside the owned rows feed the first step's halo
+// row on each side.  Logger partials of the first iteration go to partial,
+// of the second to partial2 (hs2_nblocks blocks each).
+constexpr int kHs2Out = 124;  // output columns per wave (hs_jacobi_impl.h)
+constexpr int kHs2Rows = 32;
+constexpr int kHs2Waves = 4;
+inline dim3 hs2_grid(int dimx, int nrows) {
+    return dim3((dimx + kHs2Out - 1) / kHs2Out,
+                (nrows + kHs2Rows * kHs2Waves - 1) / (kHs2Rows * kHs2Waves));
+}
+inline int hs2_nblocks(int dimx, int nrows) {
+    dim3 g = hs2_grid(dimx, nrows);
+    return int(g.x * g.y);
+}
+void launch_hs_jacobi2(const float2 *u_old, float2 *u_new, const float2 *dI, const float *It,
+                       int P, int dimx, int nrows, int row0, int dimy, float alphasq, int glo,
+                       int ghi, double *partial, double *partial2, unsigned *status,
+                       hipStream_t st);
 // Sum C iterations' per-block partials in a fixed order: sums[2t+{0,1}] =
 // {sum ||diff||, sum ||prev||} for t < C.
 void launch_reduce_partials(const double *partial, int nblocks, int C, double *sums,

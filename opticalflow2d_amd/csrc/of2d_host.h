@@ -143,9 +143,14 @@ class Registration {
     int dimy() const { return dimy_; }
 
     using StepFn = std::function<void(const float2 *src, float2 *dst, double *partial)>;
+    // two iterations in one pass: partial / partial2 receive the Logger partials
+    // of the first / second (nb blocks each, as the single step's)
+    using StepFn2 = std::function<void(const float2 *src, float2 *dst, double *partial,
+                                       double *partial2)>;
 
    private:
-    int run_chunked(Level &L, int niter, int nb, const StepFn &step, int &final_buf);
+    int run_chunked(Level &L, int niter, int nb, const StepFn &step, int &final_buf,
+                    const StepFn2 &step2 = nullptr);
     void ensure_device();
     void estimate_level(int s);
     int loop_hs(Level &L, int niter, float alpha, int &final_buf);

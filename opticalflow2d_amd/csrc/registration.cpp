@@ -269,8 +269,14 @@ void Registration::estimate_level(int s) {
 // Speculative chunked iteration loop shared by every solver whose iteration
 // reads motion_est from one buffer and writes the next iterate to another
 // (HS, Demons, Elastic, Curvature).  step(src, dst, partial) enqueues one
-// get_update plus the fused Logger partials (nb blocks x {diff, prev}).
-int Registration::run_chunked(Level &L, int niter, int nb, const StepFn &step, int &final_buf) {
+// get_update plus the fused Logger partials (nb blocks x {diff, prev}).  With
+// step2 (HS), iterations run in pairs fused into one pass, alternating between
+// the two buffers other than the chunk's start buffer a, and a single step
+// fills an odd tail.  a is never written inside a chunk, so a break at
+// iteration t is replayed from it with single steps (iteration t reads
+// src_of(a, t) and writes dst_of(a, t)).
+int Registration::run_chunked(Level &L, int niter, int nb, const StepFn &step, int &final_buf,
+                              const StepFn2 &step2) {
     const double npx = (double)L.dx * L.dy;
     last_err_.clear();
     int a = 0, k0 = 0;
@@ -278,8 +284,27 @@ int Registration::run_chunked(Level &L, int niter, int nb, const StepFn &step, i
     auto dst_of = [](int a_, int t) { return t % 2 == 0 ? (a_ + 1) % 3 : (a_ + 2) % 3; };
     while (k0 < niter) {
         const int C = std::min(chunk_, niter - k0);
-        for (int t = 0; t < C; t++)
-            step(L.est[src_of(a, t)].p, L.est[dst_of(a, t)].p, d_partial_ + (size_t)t * nb * 2);
+        auto part = [&](int t) { return d_partial_ + (size_t)t * nb * 2; };
+        int end = -1;  // pairs: the buffer holding the chunk's last iterate
+        if (step2) {
+            // pairs alternate between the two buffers other than a
+            auto other = [&](int b) { return b == (a + 1) % 3 ? (a + 2) % 3 : (a + 1) % 3; };
+            int cur = a, t = 0;
+            for (; t + 1 < C; t += 2) {
+                const int nxt = other(cur);
+                step2(L.est[cur].p, L.est[nxt].p, part(t), part(t + 1));
+                cur = nxt;
+            }
+            if (t < C) {
+                const int nxt = other(cur);
+                OF2D_HIP(hipMemsetAsync(part(t), 0, sizeof(double) * 2 * nb, st_));
+                step(L.est[cur].p, L.est[nxt].p, part(t));
+                cur = nxt;
+            }
+            end = cur;
+        } else {
+            for (int t = 0; t < C; t++) step(L.est[src_of(a, t)].p, L.est[dst_of(a, t)].p, part(t));
+        }
         launch_reduce_partials(d_partial_, nb, C, d_sums_, st_);
         OF2D_HIP(hipMemcpyAsync(hs_.sums, d_sums_, sizeof(double) * 2 * C, hipMemcpyDeviceToHost,
                                 st_));
@@ -290,14 +315,16 @@ int Registration::run_chunked(Level &L, int niter, int nb, const StepFn &step, i
             last_err_.push_back(err);
             if (verbose_) print("Iteration: %d\tError:%.4f\n", k, (double)err);
             if (!fixed_ && err < 0.001f && k > 1) {  // ImageRegistrationOpticalFlow.cpp:131-134
-                if (t + 2 <= C - 1)  // dst(t) was overwritten by iteration t+2: replay from a
+                // dst(t) was overwritten by iteration t+2, or (pairs) never
+                // written: replay single steps from the chunk's start buffer a
+                if (step2 || t + 2 <= C - 1)
                     for (int r = 0; r <= t; r++)
                         step(L.est[src_of(a, r)].p, L.est[dst_of(a, r)].p, d_partial_);
                 final_buf = dst_of(a, t);
                 return k + 1;
             }
         }
-        a = dst_of(a, C - 1);
+        a = step2 ? end : dst_of(a, C - 1);
         k0 += C;
     }
     final_buf = a;
@@ -307,14 +334,23 @@ int Registration::run_chunked(Level &L, int niter, int nb, const StepFn &step, i
 // HS iteration loop (ImageRegistrationOpticalFlow.cpp:117-135) with fused Logger
 int Registration::loop_hs(Level &L, int niter, float alpha, int &final_buf) {
     const float alphasq = alpha * alpha;  // OpticalFlowDiffusion.cpp:70
-    const int nb = hs_nblocks(L.P, L.dy);
+    // the pair kernel's block count (>= the single step's: a single step's
+    // partial row is zero-padded to it)
+    const int nb = hs2_nblocks(L.dx, L.dy);
+    const bool pairs = L.dx >= 2;
     return run_chunked(
         L, niter, nb,
         [&](const float2 *src, float2 *dst, double *partial) {
             launch_hs_jacobi(src, dst, L.dI.p, L.It.p, L.P, L.dx, L.dy, 0, L.dy, alphasq, partial,
                              d_status_, st_);
         },
-        final_buf);
+        final_buf,
+        pairs ? StepFn2([&](const float2 *src, float2 *dst, double *p1, double *p2) {
+            // one ghost j-line above and below the level's fields
+            launch_hs_jacobi2(src, dst, L.dI.p, L.It.p, L.P, L.dx, L.dy, 0, L.dy, alphasq, -1,
+                              L.dy + 1, p1, p2, d_status_, st_);
+        })
+              : StepFn2());
 }
 
 // WrapperOpticalFlow2d.cpp:105-117 -> Motion::copy_motion_to_input

@@ -1,15 +1,19 @@
 // slab.cpp — row-slab Horn-Schunck over RCCL (the multi-GPU north-star path).
 //
 // The global dimx x dimy grid is cut into contiguous slabs of j-lines (the
-// memory-slow axis), one per process/GPU.  A Jacobi step of
-// OpticalFlowDiffusion::get_update (OpticalFlowDiffusion.cpp:43-55) at j-line
-// j reads u at j-1 and j+1, so each slab keeps one ghost j-line above and one
-// below and, before every step, sends its first owned j-line to the rank above
-// and its last to the rank below (ncclSend/ncclRecv of 8*dimx bytes each, one
-// group).  The Logger's norms (Logger.cpp:32-51) are fused into the stencil
-// kernel per block, reduced per rank, and all-reduced once per chunk of
-// iterations (two doubles per iteration) — the host then applies the
-// reference's break test (ImageRegistrationOpticalFlow.cpp:131-134).
+// memory-slow axis), one per process/GPU.  Iterations run in PAIRS fused into
+// one pass (hs::jacobi2_kernel): the pass computes the first iteration on the
+// owned rows plus one halo row on each side, then the second on the owned
+// rows, so each slab keeps two ghost j-lines of u above and below and, before
+// every pair, sends its first two owned j-lines to the rank above and its last
+// two to the rank below (ncclSend/ncclRecv of 2 x 8*dimx bytes each, one
+// group) — the same bytes per iteration as a one-line exchange per step, half
+// the messages.  The gradients of the halo rows are computed locally from two
+// image halo rows (set_images).  An odd tail iteration runs the single step
+// after a one-line exchange.  The Logger's norms (Logger.cpp:32-51) are fused
+// into the stencil kernel per block, reduced per rank, and all-reduced once
+// per chunk of iterations (two doubles per iteration) — the host then applies
+// the reference's break test (ImageRegistrationOpticalFlow.cpp:131-134).
 // The border rule of gradients::qlaplacian uses the GLOBAL j (gradients.h:73),
 // so the slab result equals the single-grid result bit for bit.
 //
@@ -74,18 +78,21 @@ int sguard(of2d_slab *s, F &&f) {
     }
 }
 
-void halo_exchange(of2d_slab *s, float2 *u) {
+// `lines` (1 or 2) boundary j-lines to each neighbour; a slab thinner than
+// that sends what it has (its own ghost lines above hold the rest)
+void halo_exchange(of2d_slab *s, float2 *u, int lines) {
     if (s->nranks == 1) return;
-    const size_t cnt = 2 * (size_t)s->dimx;  // one j-line of float2
     const long P = s->P;
+    // lines are contiguous at pitch P: 2 floats per px, the padding travels too
+    const size_t cnt = 2 * ((size_t)(lines - 1) * P + (size_t)s->dimx);
     OF2D_NCCL(ncclGroupStart());
     if (s->rank > 0) {
         OF2D_NCCL(ncclSend(u, cnt, ncclFloat, s->rank - 1, s->comm, s->st));
-        OF2D_NCCL(ncclRecv(u - P, cnt, ncclFloat, s->rank - 1, s->comm, s->st));
+        OF2D_NCCL(ncclRecv(u - lines * P, cnt, ncclFloat, s->rank - 1, s->comm, s->st));
     }
     if (s->rank < s->nranks - 1) {
-        OF2D_NCCL(ncclSend(u + (long)(s->nrows - 1) * P, cnt, ncclFloat, s->rank + 1, s->comm,
-                           s->st));
+        OF2D_NCCL(ncclSend(u + (long)(s->nrows - lines) * P, cnt, ncclFloat, s->rank + 1,
+                           s->comm, s->st));
         OF2D_NCCL(ncclRecv(u + (long)s->nrows * P, cnt, ncclFloat, s->rank + 1, s->comm, s->st));
     }
     OF2D_NCCL(ncclGroupEnd());
@@ -123,7 +130,7 @@ int of2d_slab_create(of2d_slab **out, int dimx, int dimy, float alpha, int rank,
         if (of2d_slab_bounds(dimy, rank, nranks, &s->rb, &s->re) != OF2D_OK)
             throw std::invalid_argument("slab: bad rank/nranks");
         s->nrows = s->re - s->rb;
-        if (s->nrows < 1) throw std::invalid_argument("slab: more ranks than j-lines");
+        if (s->nrows < 2) throw std::invalid_argument("slab: fewer than 2 j-lines per rank");
         s->dimx = dimx;
         s->dimy = dimy;
         s->rank = rank;
@@ -135,18 +142,18 @@ int of2d_slab_create(of2d_slab **out, int dimx, int dimy, float alpha, int rank,
         OF2D_HIP(hipStreamCreateWithFlags(&s->st, hipStreamNonBlocking));
         OF2D_HIP(hipEventCreate(&s->ev0));
         OF2D_HIP(hipEventCreate(&s->ev1));
-        for (auto &f : s->u) f.alloc(dimx, s->nrows);
+        for (auto &f : s->u) f.alloc(dimx, s->nrows, 2);  // two ghost j-lines each side
         s->dI.alloc(dimx, s->nrows);
         s->It.alloc(dimx, s->nrows);
-        s->Iref.alloc(dimx, s->nrows);
-        s->Imov.alloc(dimx, s->nrows);
-        const int nb = of2d::hs_nblocks(s->P, s->nrows);
+        s->Iref.alloc(dimx, s->nrows, 2);
+        s->Imov.alloc(dimx, s->nrows, 2);
+        const int nb = std::max(of2d::hs_nblocks(s->P, s->nrows), of2d::hs2_nblocks(dimx, s->nrows));
         OF2D_HIP(hipMalloc(&s->d_partial, sizeof(double) * 2 * (size_t)nb * s->chunk));
         OF2D_HIP(hipMalloc(&s->d_sums, sizeof(double) * 2 * s->chunk));
         OF2D_HIP(hipMalloc(&s->d_status, 64 * sizeof(unsigned)));
         OF2D_HIP(hipMemset(s->d_status, 0, 64 * sizeof(unsigned)));
         OF2D_HIP(hipDeviceSynchronize());  // null-stream memset vs the non-blocking stream
-        OF2D_HIP(hipMalloc(&s->d_stage, sizeof(double) * 2 * (size_t)dimx * (s->nrows + 2)));
+        OF2D_HIP(hipMalloc(&s->d_stage, sizeof(double) * 2 * (size_t)dimx * (s->nrows + 4)));
         s->hs.ensure(s->chunk);
         if (nranks > 1) {
             if (!uid || id_len < (int)sizeof(ncclUniqueId))
@@ -168,20 +175,24 @@ int of2d_slab_create(of2d_slab **out, int dimx, int dimy, float alpha, int rank,
 int of2d_slab_set_images(of2d_slab *s, const double *Iref_rows, const double *Imov_rows) {
     if (!s || !Iref_rows || !Imov_rows) return OF2D_ERR_INVALID_ARGUMENT;
     return sguard(s, [&] {
-        // rows [rb-1, re+1) clipped to [0, dimy) -> local rows [-has_up, nrows+has_dn)
-        const int has_up = s->rb > 0 ? 1 : 0, has_dn = s->re < s->dimy ? 1 : 0;
-        const int rows = s->nrows + has_up + has_dn;
+        // rows [rb-2, re+2) clipped to [0, dimy) -> local rows [-up2, nrows+dn2)
+        const int up2 = std::min(2, s->rb), dn2 = std::min(2, s->dimy - s->re);
+        const int rows = s->nrows + up2 + dn2;
         for (int which = 0; which < 2; which++) {
             const double *src = which ? Imov_rows : Iref_rows;
             of2d::Field<float> &dst = which ? s->Imov : s->Iref;
             OF2D_HIP(hipMemcpyAsync(s->d_stage, src, sizeof(double) * s->dimx * rows,
                                     hipMemcpyHostToDevice, s->st));
-            of2d::launch_d2f(s->d_stage, s->dimx, rows, dst.p - (long)has_up * s->P, s->P, 0,
+            of2d::launch_d2f(s->d_stage, s->dimx, rows, dst.p - (long)up2 * s->P, s->P, 0,
                              s->st);
         }
         // IterativeSolver::set_derivatives(Iref, Iaux = Imov) on the owned rows
-        of2d::launch_gradients_rows(s->Iref.p, s->Imov.p, s->dI.p, s->It.p, s->dimx, s->nrows,
-                                    s->P, s->rb, s->dimy, s->st);
+        // plus the halo row on each side that the pair kernel's first step needs
+        const int up1 = std::min(1, s->rb), dn1 = std::min(1, s->dimy - s->re);
+        const long o = -(long)up1 * s->P;
+        of2d::launch_gradients_rows(s->Iref.p + o, s->Imov.p + o, s->dI.p + o, s->It.p + o,
+                                    s->dimx, s->nrows + up1 + dn1, s->P, s->rb - up1, s->dimy,
+                                    s->st);
         for (auto &f : s->u) f.zero(s->st);
         s->fin = 0;
         OF2D_HIP(hipStreamSynchronize(s->st));
@@ -192,15 +203,29 @@ int of2d_slab_run(of2d_slab *s, int niter, int fixed_iters, int *iters_done) {
     if (!s) return OF2D_ERR_INVALID_ARGUMENT;
     return sguard(s, [&] {
         const float alphasq = s->alpha * s->alpha;
-        const int nb = of2d::hs_nblocks(s->P, s->nrows);
+        // partial rows sized for the pair kernel; a single step's are zero-padded
+        const int nb = std::max(of2d::hs_nblocks(s->P, s->nrows), of2d::hs2_nblocks(s->dimx, s->nrows));
         const double npx = (double)s->dimx * s->dimy;
         auto src_of = [](int a, int t) { return t == 0 ? a : (t % 2 == 1 ? (a + 1) % 3 : (a + 2) % 3); };
         auto dst_of = [](int a, int t) { return t % 2 == 0 ? (a + 1) % 3 : (a + 2) % 3; };
+        // two iterations in one pass from buffer `in` to buffer `out`
+        auto pair = [&](int in, int out, double *p1, double *p2) {
+            float2 *uin = s->u[in].p;
+            halo_exchange(s, uin, 2);
+            of2d::launch_hs_jacobi2(uin, s->u[out].p, s->dI.p, s->It.p, s->P, s->dimx, s->nrows,
+                                    s->rb, s->dimy, alphasq, -2, s->nrows + 2, p1, p2,
+                                    s->d_status, s->st);
+        };
+        // a single step from buffer `in` to `out`
+        auto single = [&](int in, int out, double *partial) {
+            float2 *uin = s->u[in].p;
+            halo_exchange(s, uin, 1);
+            OF2D_HIP(hipMemsetAsync(partial, 0, sizeof(double) * 2 * nb, s->st));
+            of2d::launch_hs_jacobi(uin, s->u[out].p, s->dI.p, s->It.p, s->P, s->dimx, s->nrows,
+                                   s->rb, s->dimy, alphasq, partial, s->d_status, s->st);
+        };
         auto step = [&](int a, int t, double *partial) {
-            float2 *uin = s->u[src_of(a, t)].p;
-            halo_exchange(s, uin);
-            of2d::launch_hs_jacobi(uin, s->u[dst_of(a, t)].p, s->dI.p, s->It.p, s->P, s->dimx,
-                                   s->nrows, s->rb, s->dimy, alphasq, partial, s->d_status, s->st);
+            single(src_of(a, t), dst_of(a, t), partial);
         };
         for (auto &f : s->u) f.zero(s->st);  // motion_est starts at zero
         OF2D_HIP(hipMemsetAsync(s->d_status, 0, sizeof(unsigned), s->st));
@@ -209,7 +234,16 @@ int of2d_slab_run(of2d_slab *s, int niter, int fixed_iters, int *iters_done) {
         int a = 0, k0 = 0, done = -1;
         while (k0 < niter && done < 0) {
             const int C = std::min(s->chunk, niter - k0);
-            for (int t = 0; t < C; t++) step(a, t, s->d_partial + (size_t)t * nb * 2);
+            auto part = [&](int t) { return s->d_partial + (size_t)t * nb * 2; };
+            // pairs (and an odd tail step) alternate between the two buffers other
+            // than the chunk's start buffer a, which stays intact for a replay
+            auto other = [&](int b) { return b == (a + 1) % 3 ? (a + 2) % 3 : (a + 1) % 3; };
+            int cur = a, tp = 0;
+            for (; tp + 1 < C; tp += 2, cur = other(cur)) pair(cur, other(cur), part(tp), part(tp + 1));
+            if (tp < C) {
+                single(cur, other(cur), part(tp));
+                cur = other(cur);
+            }
             of2d::launch_reduce_partials(s->d_partial, nb, C, s->d_sums, s->st);
             if (s->nranks > 1)
                 OF2D_NCCL(ncclAllReduce(s->d_sums, s->d_sums, 2 * (size_t)C, ncclDouble, ncclSum,
@@ -226,15 +260,17 @@ int of2d_slab_run(of2d_slab *s, int niter, int fixed_iters, int *iters_done) {
                 const float e = of2d::logger_error(s->hs.sums[2 * t], s->hs.sums[2 * t + 1], npx);
                 s->errs.push_back(e);
                 if (!fixed_iters && e < 0.001f && k > 1) {
-                    if (t + 2 <= C - 1)  // replay up to the break (all ranks agree: sums are global)
-                        for (int r = 0; r <= t; r++) step(a, r, s->d_partial);
+                    // replay single steps from the chunk's start buffer up to the
+                    // break (pairs never wrote iteration t's own buffer; all ranks
+                    // agree: the sums are global)
+                    for (int r = 0; r <= t; r++) step(a, r, s->d_partial);
                     s->fin = dst_of(a, t);
                     done = k + 1;
                     break;
                 }
             }
             if (done < 0) {
-                a = dst_of(a, C - 1);
+                a = cur;
                 k0 += C;
             }
         }
@@ -270,14 +306,18 @@ int of2d_slab_time_kernel(of2d_slab *s, int nlaunch, double *avg_us) {
     if (!s || nlaunch <= 0 || !avg_us) return OF2D_ERR_INVALID_ARGUMENT;
     return sguard(s, [&] {
         const float alphasq = s->alpha * s->alpha;
-        // warm-up launch, then nlaunch back-to-back launches between two events
-        of2d::launch_hs_jacobi(s->u[1].p, s->u[2].p, s->dI.p, s->It.p, s->P, s->dimx, s->nrows,
-                               s->rb, s->dimy, alphasq, s->d_partial, s->d_status, s->st);
+        // the pair kernel (two iterations per launch): warm-up launch, then
+        // nlaunch back-to-back launches between two events
+        const int nb = std::max(of2d::hs_nblocks(s->P, s->nrows), of2d::hs2_nblocks(s->dimx, s->nrows));
+        double *p2 = s->d_partial + (size_t)nb * 2;
+        auto go = [&](int k) {
+            of2d::launch_hs_jacobi2(s->u[1 + (k & 1)].p, s->u[2 - (k & 1)].p, s->dI.p, s->It.p,
+                                    s->P, s->dimx, s->nrows, s->rb, s->dimy, alphasq, -2,
+                                    s->nrows + 2, s->d_partial, p2, s->d_status, s->st);
+        };
+        go(0);
         OF2D_HIP(hipEventRecord(s->ev0, s->st));
-        for (int k = 0; k < nlaunch; k++)
-            of2d::launch_hs_jacobi(s->u[1 + (k & 1)].p, s->u[2 - (k & 1)].p, s->dI.p, s->It.p,
-                                   s->P, s->dimx, s->nrows, s->rb, s->dimy, alphasq, s->d_partial,
-                                   s->d_status, s->st);
+        for (int k = 0; k < nlaunch; k++) go(k);
         OF2D_HIP(hipEventRecord(s->ev1, s->st));
         OF2D_HIP(hipEventSynchronize(s->ev1));
         float ms = 0.0f;

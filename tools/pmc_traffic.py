@@ -28,13 +28,18 @@ def per_kernel(path, counter):
 
 
 def main():
-    fetch_csv, write_csv = sys.argv[1], sys.argv[2]
-    n = int(sys.argv[3]) if len(sys.argv) > 3 else 4096
+    args = sys.argv[1:]
+    out_path = None
+    if args and args[0] == "--out":
+        out_path, args = args[1], args[2:]
+    fetch_csv, write_csv = args[0], args[1]
+    n = int(args[2]) if len(args) > 2 else 4096
     P = (n + 255) // 256 * 256
     fetch = per_kernel(fetch_csv, "FETCH_SIZE")  # KB
     write = per_kernel(write_csv, "WRITE_SIZE")  # KB
     probe = [k for k in fetch if "probe_kernel" in k][0]
-    jac = [k for k in fetch if "jacobi_kernel" in k][0]
+    jac = ([k for k in fetch if "jacobi2_kernel" in k] or [k for k in fetch if "jacobi_kernel" in k])[0]
+    pair = "jacobi2_kernel" in jac
     px = P * n  # the probe sweeps the pitched rows
     probe_read_true = 20.0 * px
     probe_write_true = 8.0 * px
@@ -54,12 +59,15 @@ def main():
         "write_bytes_per_launch": wr,
         "bytes_per_launch": rd + wr,
         "algorithmic_bytes_per_launch": alg,
+        "iterations_per_launch": 2 if pair else 1,
         "traffic_over_algorithmic": (rd + wr) / alg,
         "source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes) on tools/hs_variants, "
                   "calibrated on the probe kernel's known bytes",
     }
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    with open(os.path.join(root, "profiles", "hs_traffic.json"), "w") as f:
+    if out_path is None:  # on the GPU box write under gpurun_out/ (merged back), copy by hand
+        out_path = os.path.join(root, "profiles", "hs_traffic.json")
+    with open(out_path, "w") as f:
         json.dump(out, f, indent=1)
     print(json.dumps(out, indent=1))
 
