@@ -216,59 +216,74 @@ __global__ __launch_bounds__(64 * WAVES) void jacobi_kernel(
 // ---------------------------------------------------------------------------
 // Two Jacobi iterations per pass over HBM (temporal blocking).  Same per-pixel
 // arithmetic as jacobi_kernel, applied twice: u1 = step(u), u2 = step(u1).
-// A wave loads a 128-px strip starting 2 px left of its 124 output columns
-// (lanes 1..62 own 2 px each; lanes 0 and 63 are the halo that u1 needs), so
-// no edge lane loads anything extra and every load stays 16-B aligned.  Down
-// the strip it keeps u at rows j..j+2 and u1 at rows j-1..j+1 in registers: one
-// u row, one dI row and one It row in, one u2 row out per step, 28 B per pixel
-// for TWO iterations (+ the 4 / 2 halo rows of a ROWS band).  Rows outside
-// [0, dimy) are read from the clamped ghost lines and never feed a pixel of
-// the image (the border rule zeroes q there).  Logger partials of both
-// iterations over the owned pixels: partial[2*blk..] for the first,
-// partial2[2*blk..] for the second.
-template <int ROWS, int WAVES>
+// A wave loads a strip of 64*PXL px starting PXL px left of its 62*PXL output
+// columns (lanes 1..62 own PXL px each; lanes 0 and 63 are the halo that u1
+// needs), so no edge lane loads anything extra and every load stays 16-B
+// aligned.  Down the strip it keeps u at rows j..j+2 and u1 at rows j-1..j+1
+// in registers: one u row, one dI row and one It row in, one u2 row out per
+// step, 28 B per pixel for TWO iterations (+ the 4 / 2 halo rows of a ROWS
+// band and the 2 halo lanes).  Rows outside [0, dimy) are read from the
+// clamped ghost lines and never feed a pixel of the image (the border rule
+// zeroes q there).  Logger partials of both iterations over the owned pixels:
+// partial[2*blk..] for the first, partial2[2*blk..] for the second.
+template <int PXL>
+constexpr int hs2_out() {
+    return 62 * PXL;
+}
+
+template <int ROWS, int WAVES, int PXL = 2>
 __global__ __launch_bounds__(64 * WAVES) void jacobi2_kernel(
     const float2 *__restrict__ uo, float2 *__restrict__ un, const float2 *__restrict__ dI,
     const float *__restrict__ It, int P, int dimx, int nrows, int row0, int dimy, float alphasq,
     int glo, int ghi, double *__restrict__ partial, double *__restrict__ partial2,
     unsigned *__restrict__ status) {
+    static_assert(PXL == 2 || PXL == 4, "PXL");
     // glo / ghi: first / one-past-last local row whose u, dI and It may be
     // read (ghost j-lines included); rows outside are clamped into it
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
-    const int x = blockIdx.x * kHs2Out - 2 + 2 * lane;  // this lane's two pixels x, x+1
+    const int x = blockIdx.x * hs2_out<PXL>() - PXL + PXL * lane;  // this lane's px x..x+PXL-1
     const bool own = lane >= 1 && lane <= 62 && x < dimx;
-    const bool xin = x >= 0 && x < P;  // the pair lies inside the pitched row
+    const bool xin = x >= 0 && x + PXL <= P;  // the lane's px lie inside the pitched row
     const int jbeg = (blockIdx.y * WAVES + wave) * ROWS;
     const int jend = min(jbeg + ROWS, nrows);
     double sd1 = 0.0, sp1 = 0.0, sd2 = 0.0, sp2 = 0.0;
     unsigned bad = 0;
     auto cl = [&](int j) { return min(max(j, glo), ghi - 1); };
-    // lanes whose pair lies outside the pitched row read a clamped in-row
-    // pair instead (their values only reach the halo lanes 0 / 63)
-    const int xl = xin ? x : (x < 0 ? 0 : P - 2);
-    auto ldu = [&](int j) { return load_row<2, true>(uo + (long)cl(j) * P, xl); };
-    auto ldg = [&](int j, Row<2> &g, float t[2]) {
-        g = load_row<2, false>(dI + (long)cl(j) * P, xl);
-        const float2 tt = *reinterpret_cast<const float2 *>(It + (long)cl(j) * P + xl);
-        t[0] = tt.x;
-        t[1] = tt.y;
+    // lanes whose px lie outside the pitched row read a clamped in-row group
+    // instead (their values only reach the halo lanes 0 / 63)
+    const int xl = xin ? x : (x < 0 ? 0 : P - PXL);
+    auto ldu = [&](int j) { return load_row<PXL, true>(uo + (long)cl(j) * P, xl); };
+    auto ldg = [&](int j, Row<PXL> &g, float t[PXL]) {
+        g = load_row<PXL, false>(dI + (long)cl(j) * P, xl);
+        const float *tp = It + (long)cl(j) * P + xl;
+        if constexpr (PXL == 2) {
+            const float2 tt = *reinterpret_cast<const float2 *>(tp);
+            t[0] = tt.x;
+            t[1] = tt.y;
+        } else {
+            const float4 tt = *reinterpret_cast<const float4 *>(tp);
+            t[0] = tt.x;
+            t[1] = tt.y;
+            t[2] = tt.z;
+            t[3] = tt.w;
+        }
     };
     // one Jacobi step at row j from rows (m, c, p) of its input
-    auto stepr = [&](int j, const Row<2> &m, const Row<2> &c, const Row<2> &p, const Row<2> &g,
-                     const float t[2], unsigned &b) {
+    auto stepr = [&](int j, const Row<PXL> &m, const Row<PXL> &c, const Row<PXL> &p,
+                     const Row<PXL> &g, const float t[PXL], unsigned &b) {
         float2 left, right;
-        left.x = dpp_from_left(c.v[1].x);
-        left.y = dpp_from_left(c.v[1].y);
+        left.x = dpp_from_left(c.v[PXL - 1].x);
+        left.y = dpp_from_left(c.v[PXL - 1].y);
         right.x = dpp_from_right(c.v[0].x);
         right.y = dpp_from_right(c.v[0].y);
         const int jg = row0 + j;
         const bool yb = (jg == 0) || (jg == dimy - 1);
-        Row<2> o;
+        Row<PXL> o;
 #pragma unroll
-        for (int k = 0; k < 2; k++) {
-            const float2 l = (k == 0) ? left : c.v[0];
-            const float2 r = (k == 1) ? right : c.v[1];
+        for (int k = 0; k < PXL; k++) {
+            const float2 l = (k == 0) ? left : c.v[k - 1];
+            const float2 r = (k == PXL - 1) ? right : c.v[k + 1];
             float2 q;
             q.x = (((l.x + r.x) + m.v[k].x) + p.v[k].x) / 4.0f;
             q.y = (((l.y + r.y) + m.v[k].y) + p.v[k].y) / 4.0f;
@@ -278,42 +293,46 @@ __global__ __launch_bounds__(64 * WAVES) void jacobi2_kernel(
         }
         return o;
     };
-    const bool in1 = x + 1 < dimx;  // second pixel of the pair in the image (a select,
-                                    // not a product: padding may hold 0/0 when alpha = 0)
-    auto norms = [&](const Row<2> &nw, const Row<2> &od, double &sd, double &sp) {
-        sd += norm_d(nw.v[0].x - od.v[0].x, nw.v[0].y - od.v[0].y);
-        sp += norm_d(od.v[0].x, od.v[0].y);
-        const double d1 = norm_d(nw.v[1].x - od.v[1].x, nw.v[1].y - od.v[1].y);
-        const double p1 = norm_d(od.v[1].x, od.v[1].y);
-        sd += in1 ? d1 : 0.0;
-        sp += in1 ? p1 : 0.0;
+    // px k of the lane inside the image: a select, not a product (padding may
+    // hold 0/0 when alpha = 0)
+    auto norms = [&](const Row<PXL> &nw, const Row<PXL> &od, double &sd, double &sp) {
+#pragma unroll
+        for (int k = 0; k < PXL; k++) {
+            const double d = norm_d(nw.v[k].x - od.v[k].x, nw.v[k].y - od.v[k].y);
+            const double q = norm_d(od.v[k].x, od.v[k].y);
+            const bool in = x + k < dimx;
+            sd += in ? d : 0.0;
+            sp += in ? q : 0.0;
+        }
     };
     if (jbeg < nrows) {
         // u rows jbeg-2 .. jbeg+1; u1 rows jbeg-1, jbeg
-        Row<2> a0 = ldu(jbeg - 2), a1 = ldu(jbeg - 1), a2 = ldu(jbeg), a3 = ldu(jbeg + 1);
-        Row<2> gm, gc;
-        float tm[2], tc[2];
+        Row<PXL> a0 = ldu(jbeg - 2), a1 = ldu(jbeg - 1), a2 = ldu(jbeg), a3 = ldu(jbeg + 1);
+        Row<PXL> gm, gc;
+        float tm[PXL], tc[PXL];
         ldg(jbeg - 1, gm, tm);
         ldg(jbeg, gc, tc);
         unsigned bx = 0;  // halo rows: flagged by the waves that own them
-        Row<2> v0 = stepr(jbeg - 1, a0, a1, a2, gm, tm, bx);  // u1 row j-1
-        Row<2> v1 = stepr(jbeg, a1, a2, a3, gc, tc, bx);      // u1 row j
-        // a1 = u row j-1 (unused now), a2 = u row j, a3 = u row j+1; the loads
-        // of step j+1 are issued during step j (one row of software prefetch)
-        Row<2> nu = ldu(jbeg + 2), ng;
-        float nt[2];
+        Row<PXL> v0 = stepr(jbeg - 1, a0, a1, a2, gm, tm, bx);  // u1 row j-1
+        Row<PXL> v1 = stepr(jbeg, a1, a2, a3, gc, tc, bx);      // u1 row j
+        // a2 = u row j, a3 = u row j+1; the loads of step j+1 are issued during
+        // step j (one row of software prefetch)
+        Row<PXL> nu = ldu(jbeg + 2), ng;
+        float nt[PXL];
         ldg(jbeg + 1, ng, nt);
         for (int j = jbeg; j < jend; ++j) {
-            const Row<2> a4 = nu;
-            Row<2> gp = ng;
-            float tp[2] = {nt[0], nt[1]};
+            const Row<PXL> a4 = nu;
+            const Row<PXL> gp = ng;
+            float tp[PXL];
+#pragma unroll
+            for (int k = 0; k < PXL; k++) tp[k] = nt[k];
             if (j + 1 < jend) {
                 nu = ldu(j + 3);
                 ldg(j + 2, ng, nt);
             }
             unsigned b1 = 0, b2 = 0;
-            const Row<2> v2 = stepr(j + 1, a2, a3, a4, gp, tp, b1);  // u1 row j+1
-            const Row<2> w = stepr(j, v0, v1, v2, gc, tc, b2);       // u2 row j
+            const Row<PXL> v2 = stepr(j + 1, a2, a3, a4, gp, tp, b1);  // u1 row j+1
+            const Row<PXL> w = stepr(j, v0, v1, v2, gc, tc, b2);       // u2 row j
             if (own) {
                 norms(v1, a2, sd1, sp1);  // first iteration at row j: u1 against u
                 norms(w, v1, sd2, sp2);   // second: u2 against u1
@@ -321,19 +340,25 @@ __global__ __launch_bounds__(64 * WAVES) void jacobi2_kernel(
                 // zero test at (x, j) is also the first one's
                 bad |= b2;
                 float2 *dst = un + (long)j * P + x;
-                if (x + 2 <= dimx)
-                    st4<true>(reinterpret_cast<float4 *>(dst),
-                              make_float4(w.v[0].x, w.v[0].y, w.v[1].x, w.v[1].y));
-                else
-                    dst[0] = w.v[0];
+                if (x + PXL <= dimx) {
+#pragma unroll
+                    for (int k = 0; k < PXL / 2; k++)
+                        st4<true>(reinterpret_cast<float4 *>(dst) + k,
+                                  make_float4(w.v[2 * k].x, w.v[2 * k].y, w.v[2 * k + 1].x,
+                                              w.v[2 * k + 1].y));
+                } else {
+#pragma unroll
+                    for (int k = 0; k < PXL; k++)
+                        if (x + k < dimx) dst[k] = w.v[k];
+                }
             }
             v0 = v1;
             v1 = v2;
             a2 = a3;
             a3 = a4;
             gc = gp;
-            tc[0] = tp[0];
-            tc[1] = tp[1];
+#pragma unroll
+            for (int k = 0; k < PXL; k++) tc[k] = tp[k];
         }
     }
     // fixed-order block reductions -> (diff, prev) per iteration per block
@@ -370,9 +395,10 @@ __global__ __launch_bounds__(64 * WAVES) void jacobi2_kernel(
     }
 }
 
-template <int ROWS, int WAVES>
+template <int ROWS, int WAVES, int PXL = 2>
 inline dim3 grid2_for(int dimx, int nrows) {
-    return dim3((dimx + kHs2Out - 1) / kHs2Out, (nrows + ROWS * WAVES - 1) / (ROWS * WAVES));
+    return dim3((dimx + hs2_out<PXL>() - 1) / hs2_out<PXL>(),
+                (nrows + ROWS * WAVES - 1) / (ROWS * WAVES));
 }
 
 template <int ROWS, int PXL, int WAVES>

@@ -30,7 +30,8 @@ static const HsKernel kHsJacobi = &hs::jacobi_kernel<kHsRows, kHsPxl, kHsWaves, 
 
 // Two iterations per launch (tools/hs_variants.hip "two": 32 j-lines, 4 waves
 // fastest; 51 us per iteration against 79 us for the single step at 4096^2).
-static const auto kHsJacobi2 = &hs::jacobi2_kernel<kHs2Rows, kHs2Waves>;
+static const auto kHsJacobi2 = &hs::jacobi2_kernel<kHs2Rows, kHs2Waves, 2>;
+static_assert(kHs2Out == hs::hs2_out<2>(), "hs2_grid and the kernel disagree on the strip");
 
 void launch_hs_jacobi2(const float2 *u_old, float2 *u_new, const float2 *dI, const float *It,
                        int P, int dimx, int nrows, int row0, int dimy, float alphasq, int glo,

@@ -82,10 +82,10 @@ float run(const Bufs &b, int iters, float2 *out_host, const char *name, double b
 
 // two iterations per launch (hs::jacobi2_kernel): timed per ITERATION, and
 // checked bit for bit against 6 single steps of the product kernel
-template <int ROWS, int WAVES>
+template <int ROWS, int WAVES, int PXL = 2>
 int run2(const Bufs &b, int iters, const char *name, double bytes) {
-    const dim3 g = hs::grid2_for<ROWS, WAVES>(b.dimx, b.dimy);
-    auto k = hs::jacobi2_kernel<ROWS, WAVES>;
+    const dim3 g = hs::grid2_for<ROWS, WAVES, PXL>(b.dimx, b.dimy);
+    auto k = hs::jacobi2_kernel<ROWS, WAVES, PXL>;
     auto k1 = hs::jacobi_kernel<32, 2, 4, true, true, false>;
     const dim3 g1 = hs::grid_for<32, 2, 4>(b.P, b.dimy);
     double *p2 = b.partial + 2 * 65536 / 2;
@@ -215,10 +215,11 @@ int main(int argc, char **argv) {
         int b2 = 0;
         V3(32, 2, 4, true, true, false);
         b2 |= run2<32, 4>(b, iters, "two-step 32r 4w", bytes);
-        b2 |= run2<16, 4>(b, iters, "two-step 16r 4w", bytes);
-        b2 |= run2<24, 4>(b, iters, "two-step 24r 4w", bytes);
+        b2 |= run2<32, 4, 4>(b, iters, "two-step 32r 4w 4px", bytes);
+        b2 |= run2<32, 2, 4>(b, iters, "two-step 32r 2w 4px", bytes);
+        b2 |= run2<16, 4, 4>(b, iters, "two-step 16r 4w 4px", bytes);
+        b2 |= run2<64, 2, 4>(b, iters, "two-step 64r 2w 4px", bytes);
         b2 |= run2<32, 2>(b, iters, "two-step 32r 2w", bytes);
-        b2 |= run2<48, 4>(b, iters, "two-step 48r 4w", bytes);
         return b2;
     }
     V3(32, 2, 4, true, true, false);  // the product configuration (hs_kernels.hip)
