@@ -236,8 +236,11 @@ __global__ __launch_bounds__(64 * WAVES) void jacobi2_kernel(
     const float2 *__restrict__ uo, float2 *__restrict__ un, const float2 *__restrict__ dI,
     const float *__restrict__ It, int P, int dimx, int nrows, int row0, int dimy, float alphasq,
     int glo, int ghi, double *__restrict__ partial, double *__restrict__ partial2,
-    unsigned *__restrict__ status) {
+    unsigned *__restrict__ status, int band0) {
     static_assert(PXL == 2 || PXL == 4, "PXL");
+    // band0: this launch covers row bands band0 .. band0 + gridDim.y - 1 (a
+    // band = WAVES * ROWS j-lines), so a slab can run its interior bands while
+    // the halo exchange that only the outer bands read is in flight
     // glo / ghi: first / one-past-last local row whose u, dI and It may be
     // read (ghost j-lines included); rows outside are clamped into it
     const int lane = threadIdx.x & 63;
@@ -245,7 +248,8 @@ __global__ __launch_bounds__(64 * WAVES) void jacobi2_kernel(
     const int x = blockIdx.x * hs2_out<PXL>() - PXL + PXL * lane;  // this lane's px x..x+PXL-1
     const bool own = lane >= 1 && lane <= 62 && x < dimx;
     const bool xin = x >= 0 && x + PXL <= P;  // the lane's px lie inside the pitched row
-    const int jbeg = (blockIdx.y * WAVES + wave) * ROWS;
+    const int band = band0 + (int)blockIdx.y;
+    const int jbeg = (band * WAVES + wave) * ROWS;
     const int jend = min(jbeg + ROWS, nrows);
     double sd1 = 0.0, sp1 = 0.0, sd2 = 0.0, sp2 = 0.0;
     unsigned bad = 0;
@@ -387,7 +391,7 @@ __global__ __launch_bounds__(64 * WAVES) void jacobi2_kernel(
             c += red[2][w];
             d += red[3][w];
         }
-        const long blk = (long)blockIdx.y * gridDim.x + blockIdx.x;
+        const long blk = (long)band * gridDim.x + blockIdx.x;
         partial[2 * blk] = a;
         partial[2 * blk + 1] = b;
         partial2[2 * blk] = c;

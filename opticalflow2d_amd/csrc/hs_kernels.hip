@@ -36,12 +36,18 @@ static_assert(kHs2Out == hs::hs2_out<2>(), "hs2_grid and the kernel disagree on 
 void launch_hs_jacobi2(const float2 *u_old, float2 *u_new, const float2 *dI, const float *It,
                        int P, int dimx, int nrows, int row0, int dimy, float alphasq, int glo,
                        int ghi, double *partial, double *partial2, unsigned *status,
-                       hipStream_t st) {
+                       hipStream_t st, int band_lo, int band_hi) {
     if (P % kHsStrip != 0 || nrows <= 0 || dimx > P || dimx < 2 || glo > -1 || ghi < nrows + 1)
         throw std::invalid_argument("launch_hs_jacobi2: bad geometry");
-    hipLaunchKernelGGL(kHsJacobi2, hs2_grid(dimx, nrows), dim3(64 * kHs2Waves), 0, st, u_old,
-                       u_new, dI, It, P, dimx, nrows, row0, dimy, alphasq, glo, ghi, partial,
-                       partial2, status);
+    const int nb = hs2_nbands(nrows);
+    if (band_lo < 0) band_lo = 0;
+    if (band_hi < 0) band_hi = nb;
+    if (band_lo > band_hi || band_hi > nb) throw std::invalid_argument("launch_hs_jacobi2: bands");
+    if (band_lo == band_hi) return;
+    dim3 g = hs2_grid(dimx, nrows);
+    g.y = band_hi - band_lo;
+    hipLaunchKernelGGL(kHsJacobi2, g, dim3(64 * kHs2Waves), 0, st, u_old, u_new, dI, It, P, dimx,
+                       nrows, row0, dimy, alphasq, glo, ghi, partial, partial2, status, band_lo);
     OF2D_HIP(hipGetLastError());
 }
 

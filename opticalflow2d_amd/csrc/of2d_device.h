@@ -79,10 +79,15 @@ inline int hs2_nblocks(int dimx, int nrows) {
     dim3 g = hs2_grid(dimx, nrows);
     return int(g.x * g.y);
 }
+// band_lo / band_hi: the row bands (kHs2Rows * kHs2Waves j-lines each) this
+// launch covers; -1 / -1 = all of them.
+inline int hs2_nbands(int nrows) {
+    return (nrows + kHs2Rows * kHs2Waves - 1) / (kHs2Rows * kHs2Waves);
+}
 void launch_hs_jacobi2(const float2 *u_old, float2 *u_new, const float2 *dI, const float *It,
                        int P, int dimx, int nrows, int row0, int dimy, float alphasq, int glo,
                        int ghi, double *partial, double *partial2, unsigned *status,
-                       hipStream_t st);
+                       hipStream_t st, int band_lo = -1, int band_hi = -1);
 // Sum C iterations' per-block partials in a fixed order: sums[2t+{0,1}] =
 // {sum ||diff||, sum ||prev||} for t < C.
 void launch_reduce_partials(const double *partial, int nblocks, int C, double *sums,

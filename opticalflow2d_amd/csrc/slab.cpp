@@ -42,6 +42,8 @@ struct of2d_slab {
     int device = 0;
     float alpha = 0.0f;
     hipStream_t st = nullptr;
+    hipStream_t comm_st = nullptr;  // the halo exchange, overlapped with interior bands
+    hipEvent_t ev_src = nullptr, ev_halo = nullptr;
     ncclComm_t comm = nullptr;
     of2d::Field<float2> u[3];
     of2d::Field<float2> dI;
@@ -78,22 +80,21 @@ int sguard(of2d_slab *s, F &&f) {
     }
 }
 
-// `lines` (1 or 2) boundary j-lines to each neighbour; a slab thinner than
-// that sends what it has (its own ghost lines above hold the rest)
-void halo_exchange(of2d_slab *s, float2 *u, int lines) {
+// `lines` (1 or 2) boundary j-lines to each neighbour, on stream `st`
+void halo_exchange(of2d_slab *s, float2 *u, int lines, hipStream_t st) {
     if (s->nranks == 1) return;
     const long P = s->P;
     // lines are contiguous at pitch P: 2 floats per px, the padding travels too
     const size_t cnt = 2 * ((size_t)(lines - 1) * P + (size_t)s->dimx);
     OF2D_NCCL(ncclGroupStart());
     if (s->rank > 0) {
-        OF2D_NCCL(ncclSend(u, cnt, ncclFloat, s->rank - 1, s->comm, s->st));
-        OF2D_NCCL(ncclRecv(u - lines * P, cnt, ncclFloat, s->rank - 1, s->comm, s->st));
+        OF2D_NCCL(ncclSend(u, cnt, ncclFloat, s->rank - 1, s->comm, st));
+        OF2D_NCCL(ncclRecv(u - lines * P, cnt, ncclFloat, s->rank - 1, s->comm, st));
     }
     if (s->rank < s->nranks - 1) {
         OF2D_NCCL(ncclSend(u + (long)(s->nrows - lines) * P, cnt, ncclFloat, s->rank + 1,
-                           s->comm, s->st));
-        OF2D_NCCL(ncclRecv(u + (long)s->nrows * P, cnt, ncclFloat, s->rank + 1, s->comm, s->st));
+                           s->comm, st));
+        OF2D_NCCL(ncclRecv(u + (long)s->nrows * P, cnt, ncclFloat, s->rank + 1, s->comm, st));
     }
     OF2D_NCCL(ncclGroupEnd());
 }
@@ -142,6 +143,9 @@ int of2d_slab_create(of2d_slab **out, int dimx, int dimy, float alpha, int rank,
         OF2D_HIP(hipStreamCreateWithFlags(&s->st, hipStreamNonBlocking));
         OF2D_HIP(hipEventCreate(&s->ev0));
         OF2D_HIP(hipEventCreate(&s->ev1));
+        OF2D_HIP(hipStreamCreateWithFlags(&s->comm_st, hipStreamNonBlocking));
+        OF2D_HIP(hipEventCreateWithFlags(&s->ev_src, hipEventDisableTiming));
+        OF2D_HIP(hipEventCreateWithFlags(&s->ev_halo, hipEventDisableTiming));
         for (auto &f : s->u) f.alloc(dimx, s->nrows, 2);  // two ghost j-lines each side
         s->dI.alloc(dimx, s->nrows);
         s->It.alloc(dimx, s->nrows);
@@ -208,18 +212,39 @@ int of2d_slab_run(of2d_slab *s, int niter, int fixed_iters, int *iters_done) {
         const double npx = (double)s->dimx * s->dimy;
         auto src_of = [](int a, int t) { return t == 0 ? a : (t % 2 == 1 ? (a + 1) % 3 : (a + 2) % 3); };
         auto dst_of = [](int a, int t) { return t % 2 == 0 ? (a + 1) % 3 : (a + 2) % 3; };
-        // two iterations in one pass from buffer `in` to buffer `out`
+        // two iterations in one pass from buffer `in` to buffer `out`.  Only the
+        // first and last row band read the ghost lines, so with neighbours the
+        // exchange runs on comm_st while the interior bands run on st: the
+        // exchange reads owned lines of `in` (no kernel writes `in`) and
+        // writes its ghost lines (read by the outer bands only, after ev_halo).
+        const int nbands = of2d::hs2_nbands(s->nrows);
         auto pair = [&](int in, int out, double *p1, double *p2) {
             float2 *uin = s->u[in].p;
-            halo_exchange(s, uin, 2);
-            of2d::launch_hs_jacobi2(uin, s->u[out].p, s->dI.p, s->It.p, s->P, s->dimx, s->nrows,
-                                    s->rb, s->dimy, alphasq, -2, s->nrows + 2, p1, p2,
-                                    s->d_status, s->st);
+            auto bands = [&](int lo, int hi) {
+                of2d::launch_hs_jacobi2(uin, s->u[out].p, s->dI.p, s->It.p, s->P, s->dimx,
+                                        s->nrows, s->rb, s->dimy, alphasq, -2, s->nrows + 2, p1,
+                                        p2, s->d_status, s->st, lo, hi);
+            };
+            if (s->nranks == 1) {
+                bands(0, nbands);
+            } else if (nbands < 3) {
+                halo_exchange(s, uin, 2, s->st);
+                bands(0, nbands);
+            } else {
+                OF2D_HIP(hipEventRecord(s->ev_src, s->st));  // `in` complete
+                OF2D_HIP(hipStreamWaitEvent(s->comm_st, s->ev_src, 0));
+                halo_exchange(s, uin, 2, s->comm_st);
+                OF2D_HIP(hipEventRecord(s->ev_halo, s->comm_st));
+                bands(1, nbands - 1);
+                OF2D_HIP(hipStreamWaitEvent(s->st, s->ev_halo, 0));
+                bands(0, 1);
+                bands(nbands - 1, nbands);
+            }
         };
         // a single step from buffer `in` to `out`
         auto single = [&](int in, int out, double *partial) {
             float2 *uin = s->u[in].p;
-            halo_exchange(s, uin, 1);
+            halo_exchange(s, uin, 1, s->st);
             OF2D_HIP(hipMemsetAsync(partial, 0, sizeof(double) * 2 * nb, s->st));
             of2d::launch_hs_jacobi(uin, s->u[out].p, s->dI.p, s->It.p, s->P, s->dimx, s->nrows,
                                    s->rb, s->dimy, alphasq, partial, s->d_status, s->st);
@@ -334,6 +359,8 @@ int of2d_slab_last_run_ms(const of2d_slab *s, double *ms) {
 
 int of2d_slab_destroy(of2d_slab *s) {
     if (!s) return OF2D_ERR_INVALID_ARGUMENT;
+    if (s->st) (void)hipStreamSynchronize(s->st);
+    if (s->comm_st) (void)hipStreamSynchronize(s->comm_st);
     if (s->comm) ncclCommDestroy(s->comm);
     if (s->d_partial) (void)hipFree(s->d_partial);
     if (s->d_sums) (void)hipFree(s->d_sums);
@@ -341,11 +368,14 @@ int of2d_slab_destroy(of2d_slab *s) {
     if (s->d_stage) (void)hipFree(s->d_stage);
     if (s->ev0) (void)hipEventDestroy(s->ev0);
     if (s->ev1) (void)hipEventDestroy(s->ev1);
+    if (s->ev_src) (void)hipEventDestroy(s->ev_src);
+    if (s->ev_halo) (void)hipEventDestroy(s->ev_halo);
     for (auto &f : s->u) f.release();
     s->dI.release();
     s->It.release();
     s->Iref.release();
     s->Imov.release();
+    if (s->comm_st) (void)hipStreamDestroy(s->comm_st);
     if (s->st) (void)hipStreamDestroy(s->st);
     delete s;
     return OF2D_OK;

@@ -91,7 +91,7 @@ int run2(const Bufs &b, int iters, const char *name, double bytes) {
     double *p2 = b.partial + 2 * 65536 / 2;
     auto launch2 = [&](const float2 *in, float2 *out) {
         hipLaunchKernelGGL(k, g, dim3(64 * WAVES), 0, 0, in, out, b.dI, b.It, b.P, b.dimx, b.dimy,
-                           0, b.dimy, 0.01f, -1, b.dimy + 1, b.partial, p2, b.status);
+                           0, b.dimy, 0.01f, -1, b.dimy + 1, b.partial, p2, b.status, 0);
     };
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
@@ -117,6 +117,35 @@ int run2(const Bufs &b, int iters, const char *name, double bytes) {
     CK(hipMemset(b.u1 - b.P, 0, sizeof(float2) * (size_t)b.P * (b.dimy + 2)));
     for (int it = 0; it < 3; it++) launch2((it & 1) ? b.u1 : b.u0, (it & 1) ? b.u0 : b.u1);
     CK(hipMemcpy(B.data(), b.u1, sizeof(float2) * cnt, hipMemcpyDeviceToHost));
+    // the slab's overlapped form: interior bands first, then the two outer ones
+    {
+        const int nb = (int)g.y;
+        auto split = [&](const float2 *in, float2 *out) {
+            auto bands = [&](int lo, int hi) {
+                dim3 gg = g;
+                gg.y = hi - lo;
+                hipLaunchKernelGGL(k, gg, dim3(64 * WAVES), 0, 0, in, out, b.dI, b.It, b.P, b.dimx,
+                                   b.dimy, 0, b.dimy, 0.01f, -1, b.dimy + 1, b.partial, p2,
+                                   b.status, lo);
+            };
+            if (nb >= 3) {
+                bands(1, nb - 1);
+                bands(0, 1);
+                bands(nb - 1, nb);
+            } else {
+                bands(0, nb);
+            }
+        };
+        std::vector<float2> Cb(cnt);
+        CK(hipMemset(b.u0 - b.P, 0, sizeof(float2) * (size_t)b.P * (b.dimy + 2)));
+        CK(hipMemset(b.u1 - b.P, 0, sizeof(float2) * (size_t)b.P * (b.dimy + 2)));
+        for (int it = 0; it < 3; it++) split((it & 1) ? b.u1 : b.u0, (it & 1) ? b.u0 : b.u1);
+        CK(hipMemcpy(Cb.data(), b.u1, sizeof(float2) * cnt, hipMemcpyDeviceToHost));
+        if (memcmp(Cb.data(), B.data(), sizeof(float2) * cnt) != 0) {
+            printf("   band-split launches differ from the full launch\n");
+            return 1;
+        }
+    }
     long bad = 0;
     for (int j = 0; j < b.dimy; j++)
         for (int i = 0; i < b.dimx; i++) {
