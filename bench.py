@@ -187,7 +187,7 @@ def main():
             },
             "roofline": {
                 "bound": "hbm",
-                "kernel": "of2d::hs::jacobi2_kernel<32,4>",
+                "kernel": "of2d::hs::jacobi2_kernel<32,4,2,true>",
                 "iterations_per_launch": ITERS_PER_LAUNCH,
                 "achieved": round(achieved, 1),
                 "peak": HBM_PEAK_GBS,

@@ -231,12 +231,33 @@ constexpr int hs2_out() {
     return 62 * PXL;
 }
 
-template <int ROWS, int WAVES, int PXL = 2>
+// XCD-aware block order: the hardware deals workgroup w to XCD w % 8, so
+// logical block L = (w % 8) * ceil(n / 8) + w / 8 puts runs of consecutive
+// strips (which share the 128-B lines at their unaligned borders and, a band
+// row further, their halo rows) on one XCD and its L2.  Returns false for the
+// padding workgroups of the last XCD.
+__device__ __forceinline__ bool xcd_block(int gx, int gy, int &bx, int &by) {
+    const int n = gx * gy, per = (n + 7) / 8;
+    const int w = (int)blockIdx.x;
+    const int L = (w % 8) * per + w / 8;
+    if (L >= n) return false;
+    bx = L % gx;
+    by = L / gx;
+    return true;
+}
+
+template <int ROWS, int WAVES, int PXL = 2, bool XCD = false>
 __global__ __launch_bounds__(64 * WAVES) void jacobi2_kernel(
     const float2 *__restrict__ uo, float2 *__restrict__ un, const float2 *__restrict__ dI,
     const float *__restrict__ It, int P, int dimx, int nrows, int row0, int dimy, float alphasq,
     int glo, int ghi, double *__restrict__ partial, double *__restrict__ partial2,
-    unsigned *__restrict__ status, int band0) {
+    unsigned *__restrict__ status, int band0, int gx, int gy) {
+    // XCD: a 1-D grid of 8 * ceil(gx * gy / 8) workgroups remapped by
+    // xcd_block; otherwise a gx x gy grid
+    int bx = (int)blockIdx.x, by = (int)blockIdx.y;
+    if constexpr (XCD) {
+        if (!xcd_block(gx, gy, bx, by)) return;
+    }
     static_assert(PXL == 2 || PXL == 4, "PXL");
     // band0: this launch covers row bands band0 .. band0 + gridDim.y - 1 (a
     // band = WAVES * ROWS j-lines), so a slab can run its interior bands while
@@ -245,10 +266,10 @@ __global__ __launch_bounds__(64 * WAVES) void jacobi2_kernel(
     // read (ghost j-lines included); rows outside are clamped into it
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
-    const int x = blockIdx.x * hs2_out<PXL>() - PXL + PXL * lane;  // this lane's px x..x+PXL-1
+    const int x = bx * hs2_out<PXL>() - PXL + PXL * lane;  // this lane's px x..x+PXL-1
     const bool own = lane >= 1 && lane <= 62 && x < dimx;
     const bool xin = x >= 0 && x + PXL <= P;  // the lane's px lie inside the pitched row
-    const int band = band0 + (int)blockIdx.y;
+    const int band = band0 + by;
     const int jbeg = (band * WAVES + wave) * ROWS;
     const int jend = min(jbeg + ROWS, nrows);
     double sd1 = 0.0, sp1 = 0.0, sd2 = 0.0, sp2 = 0.0;
@@ -391,12 +412,194 @@ __global__ __launch_bounds__(64 * WAVES) void jacobi2_kernel(
             c += red[2][w];
             d += red[3][w];
         }
-        const long blk = (long)band * gridDim.x + blockIdx.x;
+        const long blk = (long)band * gx + bx;
         partial[2 * blk] = a;
         partial[2 * blk + 1] = b;
         partial2[2 * blk] = c;
         partial2[2 * blk + 1] = d;
     }
+}
+
+// ---------------------------------------------------------------------------
+// Three Jacobi iterations per pass (u1 = step(u), u2 = step(u1), u3 = step(u2)):
+// the pair kernel's scheme one level deeper.  A wave loads 128 px starting
+// 4 px left of its 120 output columns (lanes 2..61 own 2 px each; lanes 0-1
+// and 62-63 are the halo the first two steps need), keeps u at rows j..j+3,
+// u1 at j..j+2 and u2 at j-1..j+1 in registers, and per step reads one u row,
+// one dI and one It row and writes one u3 row: 28 B per pixel for THREE
+// iterations (+ the 6 / 4 halo rows of a band).  Bit-identical to three
+// single steps.  Logger partials of the three iterations: partial, partial2,
+// partial3.  Measured in tools/hs_variants.hip ("two"): ~10 % less time per
+// iteration than the pair kernel at 4096^2 (47.6 vs 52.7 us) — the kernels are
+// now issue/latency-bound more than HBM-bound.  Not wired into the drivers
+// yet (it needs three ghost j-lines and a three-line halo in the slab path).
+constexpr int kHs3Out = 120;
+
+template <int ROWS, int WAVES, bool XCD = true>
+__global__ __launch_bounds__(64 * WAVES) void jacobi3_kernel(
+    const float2 *__restrict__ uo, float2 *__restrict__ un, const float2 *__restrict__ dI,
+    const float *__restrict__ It, int P, int dimx, int nrows, int row0, int dimy, float alphasq,
+    int glo, int ghi, double *__restrict__ partial, double *__restrict__ partial2,
+    double *__restrict__ partial3, unsigned *__restrict__ status, int band0, int gx, int gy) {
+    int bx = (int)blockIdx.x, by = (int)blockIdx.y;
+    if constexpr (XCD) {
+        if (!xcd_block(gx, gy, bx, by)) return;
+    }
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int x = bx * kHs3Out - 4 + 2 * lane;  // this lane's px x, x+1
+    const bool own = lane >= 2 && lane <= 61 && x < dimx;
+    const bool xin = x >= 0 && x + 2 <= P;
+    const int band = band0 + by;
+    const int jbeg = (band * WAVES + wave) * ROWS;
+    const int jend = min(jbeg + ROWS, nrows);
+    double s1d = 0.0, s1p = 0.0, s2d = 0.0, s2p = 0.0, s3d = 0.0, s3p = 0.0;
+    unsigned bad = 0;
+    auto cl = [&](int j) { return min(max(j, glo), ghi - 1); };
+    const int xl = xin ? x : (x < 0 ? 0 : P - 2);
+    auto ldu = [&](int j) { return load_row<2, true>(uo + (long)cl(j) * P, xl); };
+    // one row of gradients with the denominator (alpha^2 + gx^2) + gy^2
+    // (OpticalFlowDiffusion.cpp:78), which the three steps share
+    struct G {
+        Row<2> g;
+        float t[2], den[2];
+    };
+    auto ldg = [&](int j) {
+        G r;
+        r.g = load_row<2, false>(dI + (long)cl(j) * P, xl);
+        const float2 tt = *reinterpret_cast<const float2 *>(It + (long)cl(j) * P + xl);
+        r.t[0] = tt.x;
+        r.t[1] = tt.y;
+#pragma unroll
+        for (int k = 0; k < 2; k++)
+            r.den[k] = (alphasq + r.g.v[k].x * r.g.v[k].x) + r.g.v[k].y * r.g.v[k].y;
+        return r;
+    };
+    auto stepr = [&](int j, const Row<2> &m, const Row<2> &c, const Row<2> &p, const G &g,
+                     unsigned &b) {
+        float2 left, right;
+        left.x = dpp_from_left(c.v[1].x);
+        left.y = dpp_from_left(c.v[1].y);
+        right.x = dpp_from_right(c.v[0].x);
+        right.y = dpp_from_right(c.v[0].y);
+        const int jg = row0 + j;
+        const bool yb = (jg == 0) || (jg == dimy - 1);
+        Row<2> o;
+#pragma unroll
+        for (int k = 0; k < 2; k++) {
+            const float2 l = (k == 0) ? left : c.v[0];
+            const float2 r = (k == 1) ? right : c.v[1];
+            float2 q;
+            q.x = (((l.x + r.x) + m.v[k].x) + p.v[k].x) / 4.0f;
+            q.y = (((l.y + r.y) + m.v[k].y) + p.v[k].y) / 4.0f;
+            const int xi = x + k;
+            q = zero_if(yb || xi == 0 || xi == dimx - 1, q);
+            // update_px with the row's denominator
+            const float gx = g.g.v[k].x, gy = g.g.v[k].y;
+            const float sc = (g.t[k] + q.x * gx) + q.y * gy;
+            const float fx = gx * sc, fy = gy * sc;
+            b |= (g.den[k] == 0.0f) ? 1u : 0u;
+            o.v[k] = make_float2(q.x - fx / g.den[k], q.y - fy / g.den[k]);
+        }
+        return o;
+    };
+    const bool in1 = x + 1 < dimx;
+    auto norms = [&](const Row<2> &nw, const Row<2> &od, double &sd, double &sp) {
+        sd += norm_d(nw.v[0].x - od.v[0].x, nw.v[0].y - od.v[0].y);
+        sp += norm_d(od.v[0].x, od.v[0].y);
+        const double d1 = norm_d(nw.v[1].x - od.v[1].x, nw.v[1].y - od.v[1].y);
+        const double p1 = norm_d(od.v[1].x, od.v[1].y);
+        sd += in1 ? d1 : 0.0;
+        sp += in1 ? p1 : 0.0;
+    };
+    if (jbeg < nrows) {
+        unsigned bx_ = 0;  // halo rows: flagged by the waves that own them
+        const Row<2> a0 = ldu(jbeg - 3), a1 = ldu(jbeg - 2), a2 = ldu(jbeg - 1);
+        Row<2> uj = ldu(jbeg), uj1 = ldu(jbeg + 1), uj2 = ldu(jbeg + 2);
+        const G gm2 = ldg(jbeg - 2), gm1 = ldg(jbeg - 1);
+        G gj = ldg(jbeg), gj1 = ldg(jbeg + 1);
+        // u1 rows jbeg-2 .. jbeg+1, u2 rows jbeg-1, jbeg
+        const Row<2> p0 = stepr(jbeg - 2, a0, a1, a2, gm2, bx_);
+        const Row<2> p1 = stepr(jbeg - 1, a1, a2, uj, gm1, bx_);
+        Row<2> vj = stepr(jbeg, a2, uj, uj1, gj, bx_);
+        Row<2> vj1 = stepr(jbeg + 1, uj, uj1, uj2, gj1, bx_);
+        Row<2> wm1 = stepr(jbeg - 1, p0, p1, vj, gm1, bx_);
+        Row<2> wj = stepr(jbeg, p1, vj, vj1, gj, bx_);
+        Row<2> nu = ldu(jbeg + 3);
+        G ng = ldg(jbeg + 2);
+        for (int j = jbeg; j < jend; ++j) {
+            const Row<2> a3 = nu;  // u row j+3
+            const G gj2 = ng;      // gradients row j+2
+            if (j + 1 < jend) {
+                nu = ldu(j + 4);
+                ng = ldg(j + 3);
+            }
+            unsigned b1 = 0, b3 = 0;
+            const Row<2> vj2 = stepr(j + 2, uj1, uj2, a3, gj2, b1);  // u1 row j+2
+            const Row<2> wj1 = stepr(j + 1, vj, vj1, vj2, gj1, b1);  // u2 row j+1
+            const Row<2> z = stepr(j, wm1, wj, wj1, gj, b3);         // u3 row j
+            if (own) {
+                norms(vj, uj, s1d, s1p);
+                norms(wj, vj, s2d, s2p);
+                norms(z, wj, s3d, s3p);
+                bad |= b3;  // the denominator depends on dI only: one test per pixel
+                float2 *dst = un + (long)j * P + x;
+                if (x + 2 <= dimx)
+                    st4<true>(reinterpret_cast<float4 *>(dst),
+                              make_float4(z.v[0].x, z.v[0].y, z.v[1].x, z.v[1].y));
+                else
+                    dst[0] = z.v[0];
+            }
+            uj = uj1;
+            uj1 = uj2;
+            uj2 = a3;
+            vj = vj1;
+            vj1 = vj2;
+            wm1 = wj;
+            wj = wj1;
+            gj = gj1;
+            gj1 = gj2;
+        }
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        s1d += __shfl_down(s1d, off);
+        s1p += __shfl_down(s1p, off);
+        s2d += __shfl_down(s2d, off);
+        s2p += __shfl_down(s2p, off);
+        s3d += __shfl_down(s3d, off);
+        s3p += __shfl_down(s3p, off);
+    }
+    __shared__ double red[6][WAVES];
+    if (lane == 0) {
+        red[0][wave] = s1d;
+        red[1][wave] = s1p;
+        red[2][wave] = s2d;
+        red[3][wave] = s2p;
+        red[4][wave] = s3d;
+        red[5][wave] = s3p;
+    }
+    if (__any(bad) && lane == 0) atomicOr(status, kStatusDivZero);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double r[6] = {0, 0, 0, 0, 0, 0};
+#pragma unroll
+        for (int w = 0; w < WAVES; ++w)
+#pragma unroll
+            for (int q = 0; q < 6; q++) r[q] += red[q][w];
+        const long blk = (long)band * gx + bx;
+        partial[2 * blk] = r[0];
+        partial[2 * blk + 1] = r[1];
+        partial2[2 * blk] = r[2];
+        partial2[2 * blk + 1] = r[3];
+        partial3[2 * blk] = r[4];
+        partial3[2 * blk + 1] = r[5];
+    }
+}
+
+template <int ROWS, int WAVES>
+inline dim3 grid3_for(int dimx, int nrows) {
+    return dim3((dimx + kHs3Out - 1) / kHs3Out, (nrows + ROWS * WAVES - 1) / (ROWS * WAVES));
 }
 
 template <int ROWS, int WAVES, int PXL = 2>

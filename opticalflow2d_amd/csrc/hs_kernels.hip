@@ -30,7 +30,8 @@ static const HsKernel kHsJacobi = &hs::jacobi_kernel<kHsRows, kHsPxl, kHsWaves, 
 
 // Two iterations per launch (tools/hs_variants.hip "two": 32 j-lines, 4 waves
 // fastest; 51 us per iteration against 79 us for the single step at 4096^2).
-static const auto kHsJacobi2 = &hs::jacobi2_kernel<kHs2Rows, kHs2Waves, 2>;
+// XCD-aware block order (1-D launch grid remapped in the kernel): ~2 % faster
+static const auto kHsJacobi2 = &hs::jacobi2_kernel<kHs2Rows, kHs2Waves, 2, true>;
 static_assert(kHs2Out == hs::hs2_out<2>(), "hs2_grid and the kernel disagree on the strip");
 
 void launch_hs_jacobi2(const float2 *u_old, float2 *u_new, const float2 *dI, const float *It,
@@ -46,8 +47,10 @@ void launch_hs_jacobi2(const float2 *u_old, float2 *u_new, const float2 *dI, con
     if (band_lo == band_hi) return;
     dim3 g = hs2_grid(dimx, nrows);
     g.y = band_hi - band_lo;
-    hipLaunchKernelGGL(kHsJacobi2, g, dim3(64 * kHs2Waves), 0, st, u_old, u_new, dI, It, P, dimx,
-                       nrows, row0, dimy, alphasq, glo, ghi, partial, partial2, status, band_lo);
+    const dim3 gl(8 * ((g.x * g.y + 7) / 8));
+    hipLaunchKernelGGL(kHsJacobi2, gl, dim3(64 * kHs2Waves), 0, st, u_old, u_new, dI, It, P,
+                       dimx, nrows, row0, dimy, alphasq, glo, ghi, partial, partial2, status,
+                       band_lo, (int)g.x, (int)g.y);
     OF2D_HIP(hipGetLastError());
 }
 

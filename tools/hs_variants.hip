@@ -82,16 +82,18 @@ float run(const Bufs &b, int iters, float2 *out_host, const char *name, double b
 
 // two iterations per launch (hs::jacobi2_kernel): timed per ITERATION, and
 // checked bit for bit against 6 single steps of the product kernel
-template <int ROWS, int WAVES, int PXL = 2>
+template <int ROWS, int WAVES, int PXL = 2, bool XCD = false>
 int run2(const Bufs &b, int iters, const char *name, double bytes) {
     const dim3 g = hs::grid2_for<ROWS, WAVES, PXL>(b.dimx, b.dimy);
-    auto k = hs::jacobi2_kernel<ROWS, WAVES, PXL>;
+    auto k = hs::jacobi2_kernel<ROWS, WAVES, PXL, XCD>;
+    const dim3 gl = XCD ? dim3(8 * ((g.x * g.y + 7) / 8)) : g;  // launch grid
     auto k1 = hs::jacobi_kernel<32, 2, 4, true, true, false>;
     const dim3 g1 = hs::grid_for<32, 2, 4>(b.P, b.dimy);
     double *p2 = b.partial + 2 * 65536 / 2;
     auto launch2 = [&](const float2 *in, float2 *out) {
-        hipLaunchKernelGGL(k, g, dim3(64 * WAVES), 0, 0, in, out, b.dI, b.It, b.P, b.dimx, b.dimy,
-                           0, b.dimy, 0.01f, -1, b.dimy + 1, b.partial, p2, b.status, 0);
+        hipLaunchKernelGGL(k, gl, dim3(64 * WAVES), 0, 0, in, out, b.dI, b.It, b.P, b.dimx, b.dimy,
+                           0, b.dimy, 0.01f, -1, b.dimy + 1, b.partial, p2, b.status, 0, (int)g.x,
+                           (int)g.y);
     };
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
@@ -124,9 +126,10 @@ int run2(const Bufs &b, int iters, const char *name, double bytes) {
             auto bands = [&](int lo, int hi) {
                 dim3 gg = g;
                 gg.y = hi - lo;
-                hipLaunchKernelGGL(k, gg, dim3(64 * WAVES), 0, 0, in, out, b.dI, b.It, b.P, b.dimx,
-                                   b.dimy, 0, b.dimy, 0.01f, -1, b.dimy + 1, b.partial, p2,
-                                   b.status, lo);
+                const dim3 ggl = XCD ? dim3(8 * ((gg.x * gg.y + 7) / 8)) : gg;
+                hipLaunchKernelGGL(k, ggl, dim3(64 * WAVES), 0, 0, in, out, b.dI, b.It, b.P,
+                                   b.dimx, b.dimy, 0, b.dimy, 0.01f, -1, b.dimy + 1, b.partial,
+                                   p2, b.status, lo, (int)gg.x, (int)gg.y);
             };
             if (nb >= 3) {
                 bands(1, nb - 1);
@@ -146,6 +149,57 @@ int run2(const Bufs &b, int iters, const char *name, double bytes) {
             return 1;
         }
     }
+    long bad = 0;
+    for (int j = 0; j < b.dimy; j++)
+        for (int i = 0; i < b.dimx; i++) {
+            const float2 x = A[(size_t)j * b.P + i], y = B[(size_t)j * b.P + i];
+            if (memcmp(&x, &y, sizeof x) != 0 && bad++ < 3)
+                printf("   mismatch at (%d,%d): %.9g %.9g vs %.9g %.9g\n", i, j, x.x, x.y, y.x, y.y);
+        }
+    printf("%-28s grid=%5ux%-4u  %8.2f us/iter  %7.1f GB/s-equiv  %s\n", name, g.x, g.y, us,
+           bytes / us / 1e3, bad ? "MISMATCH" : "bit-identical to 6 single steps");
+    return bad ? 1 : 0;
+}
+
+// three iterations per launch: timed per ITERATION, checked against 6 single steps
+template <int ROWS, int WAVES>
+int run3(const Bufs &b, int iters, const char *name, double bytes) {
+    const dim3 g = hs::grid3_for<ROWS, WAVES>(b.dimx, b.dimy);
+    const dim3 gl(8 * ((g.x * g.y + 7) / 8));
+    auto k = hs::jacobi3_kernel<ROWS, WAVES, true>;
+    auto k1 = hs::jacobi_kernel<32, 2, 4, true, true, false>;
+    const dim3 g1 = hs::grid_for<32, 2, 4>(b.P, b.dimy);
+    double *p2 = b.partial + 2 * 16384, *p3 = b.partial + 4 * 16384;
+    auto launch3 = [&](const float2 *in, float2 *out) {
+        hipLaunchKernelGGL(k, gl, dim3(64 * WAVES), 0, 0, in, out, b.dI, b.It, b.P, b.dimx, b.dimy,
+                           0, b.dimy, 0.01f, -1, b.dimy + 1, b.partial, p2, p3, b.status, 0,
+                           (int)g.x, (int)g.y);
+    };
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    CK(hipMemset(b.u0 - b.P, 0, sizeof(float2) * (size_t)b.P * (b.dimy + 2)));
+    for (int it = 0; it < 3; it++) launch3((it & 1) ? b.u1 : b.u0, (it & 1) ? b.u0 : b.u1);
+    CK(hipEventRecord(e0, 0));
+    const int nl = iters / 3;
+    for (int it = 0; it < nl; it++) launch3((it & 1) ? b.u1 : b.u0, (it & 1) ? b.u0 : b.u1);
+    CK(hipEventRecord(e1, 0));
+    CK(hipEventSynchronize(e1));
+    float ms;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    const double us = 1000.0 * ms / (3 * nl);
+    const size_t cnt = (size_t)b.P * b.dimy;
+    std::vector<float2> A(cnt), B(cnt);
+    CK(hipMemset(b.u0 - b.P, 0, sizeof(float2) * (size_t)b.P * (b.dimy + 2)));
+    CK(hipMemset(b.u1 - b.P, 0, sizeof(float2) * (size_t)b.P * (b.dimy + 2)));
+    for (int it = 0; it < 6; it++)
+        hipLaunchKernelGGL(k1, g1, dim3(256), 0, 0, (it & 1) ? b.u1 : b.u0, (it & 1) ? b.u0 : b.u1,
+                           b.dI, b.It, b.P, b.dimx, b.dimy, 0, b.dimy, 0.01f, b.partial, b.status);
+    CK(hipMemcpy(A.data(), b.u0, sizeof(float2) * cnt, hipMemcpyDeviceToHost));
+    CK(hipMemset(b.u0 - b.P, 0, sizeof(float2) * (size_t)b.P * (b.dimy + 2)));
+    CK(hipMemset(b.u1 - b.P, 0, sizeof(float2) * (size_t)b.P * (b.dimy + 2)));
+    for (int it = 0; it < 2; it++) launch3((it & 1) ? b.u1 : b.u0, (it & 1) ? b.u0 : b.u1);
+    CK(hipMemcpy(B.data(), b.u0, sizeof(float2) * cnt, hipMemcpyDeviceToHost));
     long bad = 0;
     for (int j = 0; j < b.dimy; j++)
         for (int i = 0; i < b.dimx; i++) {
@@ -239,16 +293,18 @@ int main(int argc, char **argv) {
     } while (0)
     const bool product_only = argc > 3 && strcmp(argv[3], "product") == 0;
     if (argc > 3 && strcmp(argv[3], "pair") == 0)  // the product pair kernel (PMC runs)
-        return run2<32, 4>(b, iters, "two-step 32r 4w (product)", bytes);
+        return run2<32, 4, 2, true>(b, iters, "two-step 32r 4w xcd (product)", bytes);
     if (argc > 3 && strcmp(argv[3], "two") == 0) {
         int b2 = 0;
         V3(32, 2, 4, true, true, false);
         b2 |= run2<32, 4>(b, iters, "two-step 32r 4w", bytes);
-        b2 |= run2<32, 4, 4>(b, iters, "two-step 32r 4w 4px", bytes);
-        b2 |= run2<32, 2, 4>(b, iters, "two-step 32r 2w 4px", bytes);
-        b2 |= run2<16, 4, 4>(b, iters, "two-step 16r 4w 4px", bytes);
-        b2 |= run2<64, 2, 4>(b, iters, "two-step 64r 2w 4px", bytes);
-        b2 |= run2<32, 2>(b, iters, "two-step 32r 2w", bytes);
+        b2 |= run3<32, 4>(b, iters, "three-step 32r 4w xcd", bytes);
+        b2 |= run3<32, 2>(b, iters, "three-step 32r 2w xcd", bytes);
+        b2 |= run3<64, 2>(b, iters, "three-step 64r 2w xcd", bytes);
+        b2 |= run2<32, 4, 2, true>(b, iters, "two-step 32r 4w xcd", bytes);
+        b2 |= run2<32, 2, 2, true>(b, iters, "two-step 32r 2w xcd", bytes);
+        b2 |= run2<16, 4, 2, true>(b, iters, "two-step 16r 4w xcd", bytes);
+        b2 |= run2<32, 4>(b, iters, "two-step 32r 4w (again)", bytes);
         return b2;
     }
     V3(32, 2, 4, true, true, false);  // the product configuration (hs_kernels.hip)
