@@ -173,6 +173,7 @@ class Registration {
     double *d_stage_ = nullptr;  // double staging for boundary copies
     size_t stage_count_ = 0;
     double *d_partial_ = nullptr;
+    DevArray<double> d_all_;  // fixed_iters: every iteration's Logger sums of a level
     size_t partial_count_ = 0;
     double *d_sums_ = nullptr;
     unsigned *d_status_ = nullptr;

@@ -279,6 +279,10 @@ int Registration::run_chunked(Level &L, int niter, int nb, const StepFn &step, i
                               const StepFn2 &step2) {
     const double npx = (double)L.dx * L.dy;
     last_err_.clear();
+    if (fixed_ && d_all_.n < 2 * (size_t)niter) {
+        d_all_.alloc(2 * (size_t)niter);
+        hs_.ensure((niter + 1) / 2);  // 4 doubles per unit of capacity
+    }
     int a = 0, k0 = 0;
     auto src_of = [](int a_, int t) { return t == 0 ? a_ : (t % 2 == 1 ? (a_ + 1) % 3 : (a_ + 2) % 3); };
     auto dst_of = [](int a_, int t) { return t % 2 == 0 ? (a_ + 1) % 3 : (a_ + 2) % 3; };
@@ -305,6 +309,14 @@ int Registration::run_chunked(Level &L, int niter, int nb, const StepFn &step, i
         } else {
             for (int t = 0; t < C; t++) step(L.est[src_of(a, t)].p, L.est[dst_of(a, t)].p, part(t));
         }
+        if (fixed_) {
+            // no break to decide: every chunk's sums stay on the device and are
+            // read back once after the loop (no host round trip per chunk)
+            launch_reduce_partials(d_partial_, nb, C, d_all_.p + 2 * (size_t)k0, st_);
+            a = step2 ? end : dst_of(a, C - 1);
+            k0 += C;
+            continue;
+        }
         launch_reduce_partials(d_partial_, nb, C, d_sums_, st_);
         OF2D_HIP(hipMemcpyAsync(hs_.sums, d_sums_, sizeof(double) * 2 * C, hipMemcpyDeviceToHost,
                                 st_));
@@ -326,6 +338,16 @@ int Registration::run_chunked(Level &L, int niter, int nb, const StepFn &step, i
         }
         a = step2 ? end : dst_of(a, C - 1);
         k0 += C;
+    }
+    if (fixed_ && niter > 0) {
+        OF2D_HIP(hipMemcpyAsync(hs_.sums, d_all_.p, sizeof(double) * 2 * niter,
+                                hipMemcpyDeviceToHost, st_));
+        check_status();
+        for (int k = 0; k < niter; k++) {
+            const float err = logger_error(hs_.sums[2 * k], hs_.sums[2 * k + 1], npx);
+            last_err_.push_back(err);
+            if (verbose_) print("Iteration: %d\tError:%.4f\n", k, (double)err);
+        }
     }
     final_buf = a;
     return niter;

@@ -49,6 +49,8 @@ struct of2d_slab {
     of2d::Field<float2> dI;
     of2d::Field<float> It, Iref, Imov;
     double *d_partial = nullptr, *d_sums = nullptr, *d_stage = nullptr;
+    double *d_all = nullptr;  // fixed_iters: the sums of every iteration of a run
+    size_t all_cap = 0;
     unsigned *d_status = nullptr;
     of2d::HostScratch hs;
     int chunk = 32;
@@ -252,6 +254,12 @@ int of2d_slab_run(of2d_slab *s, int niter, int fixed_iters, int *iters_done) {
         auto step = [&](int a, int t, double *partial) {
             single(src_of(a, t), dst_of(a, t), partial);
         };
+        if (fixed_iters && s->all_cap < 2 * (size_t)niter) {
+            if (s->d_all) OF2D_HIP(hipFree(s->d_all));
+            s->all_cap = 2 * (size_t)niter;
+            OF2D_HIP(hipMalloc(&s->d_all, sizeof(double) * s->all_cap));
+            s->hs.ensure((niter + 1) / 2);  // 4 doubles per unit of capacity
+        }
         for (auto &f : s->u) f.zero(s->st);  // motion_est starts at zero
         OF2D_HIP(hipMemsetAsync(s->d_status, 0, sizeof(unsigned), s->st));
         s->errs.clear();
@@ -268,6 +276,18 @@ int of2d_slab_run(of2d_slab *s, int niter, int fixed_iters, int *iters_done) {
             if (tp < C) {
                 single(cur, other(cur), part(tp));
                 cur = other(cur);
+            }
+            if (fixed_iters) {
+                // no break to decide: keep every chunk's sums on the device and
+                // read them back once after the run (no host sync per chunk)
+                double *sums = s->d_all + 2 * (size_t)k0;
+                of2d::launch_reduce_partials(s->d_partial, nb, C, sums, s->st);
+                if (s->nranks > 1)
+                    OF2D_NCCL(ncclAllReduce(sums, sums, 2 * (size_t)C, ncclDouble, ncclSum,
+                                            s->comm, s->st));
+                a = cur;
+                k0 += C;
+                continue;
             }
             of2d::launch_reduce_partials(s->d_partial, nb, C, s->d_sums, s->st);
             if (s->nranks > 1)
@@ -302,6 +322,18 @@ int of2d_slab_run(of2d_slab *s, int niter, int fixed_iters, int *iters_done) {
         if (done < 0) {
             s->fin = a;
             done = niter;
+        }
+        if (fixed_iters && niter > 0) {
+            OF2D_HIP(hipMemcpyAsync(s->hs.sums, s->d_all, sizeof(double) * 2 * niter,
+                                    hipMemcpyDeviceToHost, s->st));
+            OF2D_HIP(hipMemcpyAsync(s->hs.status, s->d_status, sizeof(unsigned),
+                                    hipMemcpyDeviceToHost, s->st));
+            OF2D_HIP(hipStreamSynchronize(s->st));
+            if (s->hs.status[0] & of2d::kStatusDivZero)
+                throw std::runtime_error("Divide by zero exception");
+            for (int t = 0; t < niter; t++)
+                s->errs.push_back(
+                    of2d::logger_error(s->hs.sums[2 * t], s->hs.sums[2 * t + 1], npx));
         }
         OF2D_HIP(hipEventRecord(s->ev1, s->st));
         OF2D_HIP(hipEventSynchronize(s->ev1));
@@ -364,6 +396,7 @@ int of2d_slab_destroy(of2d_slab *s) {
     if (s->comm) ncclCommDestroy(s->comm);
     if (s->d_partial) (void)hipFree(s->d_partial);
     if (s->d_sums) (void)hipFree(s->d_sums);
+    if (s->d_all) (void)hipFree(s->d_all);
     if (s->d_status) (void)hipFree(s->d_status);
     if (s->d_stage) (void)hipFree(s->d_stage);
     if (s->ev0) (void)hipEventDestroy(s->ev0);
