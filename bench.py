@@ -7,10 +7,11 @@ One step = one Horn-Schunck iteration of the reference loop
 (ImageRegistrationOpticalFlow.cpp:123-135): OpticalFlowDiffusion::get_update +
 the Logger norms over the whole grid, the per-chunk norm reduction /
 convergence read-back, and — for N > 1 — the RCCL halo exchange.  Iterations
-run in pairs fused into one pass over HBM (hs::jacobi2_kernel: 28 B/px per
-launch, two iterations per launch, bit-identical to two single steps), with a
-two-j-line halo exchange per pair.  Early exit is disabled (fixed_iters) so
-that exactly K iterations run.
+run in threes fused into one pass over HBM (hs::jacobi3_kernel: 28 B/px per
+launch, three iterations per launch, bit-identical to three single steps; a
+pair kernel fills a chunk's tail), with a three-j-line halo exchange per
+launch overlapped with the interior bands.  Early exit is disabled
+(fixed_iters) so that exactly K iterations run.
 
 Workload: N = 1 is BASELINE config 2 (Horn-Schunck 4096^2 fp32).  For N > 1
 every rank owns a 4096-row slab of a 4096 x (4096 N) grid (weak scaling, the
@@ -35,9 +36,9 @@ sys.path.insert(0, ROOT)
 
 METRIC = "Mpixel-iterations/sec + achieved HBM GB/s, Horn-Schunck 4096^2 @ 1/2/4/8 GPU"
 BYTES_PER_PX_IT = 28  # read u 8 + dI 8 + It 4, write u 8
-# the pair kernel moves those 28 B/px once per launch and advances TWO iterations
+# the fused kernel moves those 28 B/px once per launch and advances THREE iterations
 BYTES_PER_PX_LAUNCH = 28
-ITERS_PER_LAUNCH = 2
+ITERS_PER_LAUNCH = 3
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s peak (spec)
 ALPHA = 0.1
 
@@ -178,7 +179,7 @@ def main():
                 "fixed_iters": True,
                 "parallelism": f"row-slab x{world}",
                 "gpu_ms_rank0": round(gpu_ms, 3),
-                # the path's own algorithmic traffic (28 B/px per pair) per GPU
+                # the path's own algorithmic traffic (28 B/px per fused launch) per GPU
                 "hbm_GBps_from_step_time": round(BYTES_PER_PX_LAUNCH * total_px * args.steps
                                                  / ITERS_PER_LAUNCH / elapsed / 1e9 / world, 1),
                 # the reference algorithm's 28 B per pixel-iteration at this rate
@@ -187,7 +188,7 @@ def main():
             },
             "roofline": {
                 "bound": "hbm",
-                "kernel": "of2d::hs::jacobi2_kernel<32,4,2,true>",
+                "kernel": "of2d::hs::jacobi3_kernel<32,4,true>",
                 "iterations_per_launch": ITERS_PER_LAUNCH,
                 "achieved": round(achieved, 1),
                 "peak": HBM_PEAK_GBS,
@@ -196,6 +197,10 @@ def main():
                 "avg_launch_us": round(avg_us, 3),
                 "bytes_per_launch": BYTES_PER_PX_LAUNCH * px_rank,
                 "traffic": (traffic or {}).get("bytes_per_launch"),
+                # the unfused reference algorithm's 28 B per pixel-iteration at the
+                # kernel's per-iteration rate, as a fraction of the HBM peak
+                "ref_equiv_frac": round(BYTES_PER_PX_IT * px_rank * ITERS_PER_LAUNCH
+                                        / (avg_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
                 "traffic_source": (traffic or {}).get("source"),
             },
             "cpu_baseline": None,

@@ -111,8 +111,9 @@ const char *of2d_gateway_last_error(void);
 /* ---- row-slab Horn-Schunck solver (multi-GPU north-star path) ----
  * One process per GPU.  Global grid dimx x dimy is split into contiguous slabs
  * of j-lines; rank r owns rows [row_begin, row_end) (of2d_slab_bounds).  The
- * halo (two j-lines to each neighbour before every pair of iterations, one
- * before an odd tail iteration) travels over RCCL.  A slab needs >= 2 j-lines.
+ * halo (K j-lines to each neighbour before every fused launch of K = 3, 2 or 1
+ * iterations) travels over RCCL, overlapped with the interior row bands.  A
+ * slab needs >= 3 j-lines.
  * nranks == 1 needs no unique id (pass NULL). */
 int of2d_slab_bounds(int dimy, int rank, int nranks, int *row_begin, int *row_end);
 int of2d_rccl_unique_id_size(void);
@@ -120,9 +121,9 @@ int of2d_rccl_get_unique_id(void *out, int len);
 typedef struct of2d_slab of2d_slab;
 int of2d_slab_create(of2d_slab **out, int dimx, int dimy, float alpha, int rank, int nranks,
                      int device, const void *rccl_unique_id, int id_len);
-/* images: rows [row_begin-2, row_end+2) clipped to [0, dimy), double, x fast
- * (two halo rows: iterations run in pairs, whose first step also covers one
- * halo j-line on each side) */
+/* images: rows [row_begin-3, row_end+3) clipped to [0, dimy), double, x fast
+ * (three halo rows: iterations run fused in threes, whose first step also
+ * covers two halo j-lines on each side) */
 int of2d_slab_set_images(of2d_slab *s, const double *Iref_rows, const double *Imov_rows);
 /* runs niter Jacobi iterations (HS, Logger, convergence unless fixed_iters);
  * *iters_done receives the iterations executed */
@@ -130,7 +131,7 @@ int of2d_slab_run(of2d_slab *s, int niter, int fixed_iters, int *iters_done);
 /* owned rows of the motion, planar double [dimx*nrows*2] */
 int of2d_slab_get_motion(of2d_slab *s, double *out);
 /* average duration (microseconds) of one launch of the Jacobi kernel (the
- * pair kernel: TWO iterations per launch) over nlaunch launches, timed with
+ * fused kernel: THREE iterations per launch) over nlaunch launches, timed with
  * HIP events on the stream it is launched on */
 int of2d_slab_time_kernel(of2d_slab *s, int nlaunch, double *avg_us);
 /* wall time (ms, HIP events) of the last of2d_slab_run on this rank */

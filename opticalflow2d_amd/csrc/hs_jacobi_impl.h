@@ -431,10 +431,7 @@ __global__ __launch_bounds__(64 * WAVES) void jacobi2_kernel(
 // single steps.  Logger partials of the three iterations: partial, partial2,
 // partial3.  Measured in tools/hs_variants.hip ("two"): ~10 % less time per
 // iteration than the pair kernel at 4096^2 (47.6 vs 52.7 us) — the kernels are
-// now issue/latency-bound more than HBM-bound.  Not wired into the drivers
-// yet (it needs three ghost j-lines and a three-line halo in the slab path).
-constexpr int kHs3Out = 120;
-
+// now issue/latency-bound more than HBM-bound.  band0 as in jacobi2_kernel.
 template <int ROWS, int WAVES, bool XCD = true>
 __global__ __launch_bounds__(64 * WAVES) void jacobi3_kernel(
     const float2 *__restrict__ uo, float2 *__restrict__ un, const float2 *__restrict__ dI,

@@ -88,6 +88,33 @@ void launch_hs_jacobi2(const float2 *u_old, float2 *u_new, const float2 *dI, con
                        int P, int dimx, int nrows, int row0, int dimy, float alphasq, int glo,
                        int ghi, double *partial, double *partial2, unsigned *status,
                        hipStream_t st, int band_lo = -1, int band_hi = -1);
+// Three Jacobi iterations per launch (hs::jacobi3_kernel): bit-identical to
+// three launch_hs_jacobi calls; rows [glo, ghi) readable as for the pair
+// kernel (the first two steps also cover two / one halo rows each side).
+constexpr int kHs3Out = 120;  // output columns per wave (hs_jacobi_impl.h)
+constexpr int kHs3Rows = 32;
+constexpr int kHs3Waves = 4;
+inline dim3 hs3_grid(int dimx, int nrows) {
+    return dim3((dimx + kHs3Out - 1) / kHs3Out,
+                (nrows + kHs3Rows * kHs3Waves - 1) / (kHs3Rows * kHs3Waves));
+}
+inline int hs3_nblocks(int dimx, int nrows) {
+    dim3 g = hs3_grid(dimx, nrows);
+    return int(g.x * g.y);
+}
+inline int hs3_nbands(int nrows) {
+    return (nrows + kHs3Rows * kHs3Waves - 1) / (kHs3Rows * kHs3Waves);
+}
+void launch_hs_jacobi3(const float2 *u_old, float2 *u_new, const float2 *dI, const float *It,
+                       int P, int dimx, int nrows, int row0, int dimy, float alphasq, int glo,
+                       int ghi, double *partial, double *partial2, double *partial3,
+                       unsigned *status, hipStream_t st, int band_lo = -1, int band_hi = -1);
+// partial-row length that fits every HS kernel (single, pair, triple)
+inline int hs_partial_blocks(int P, int dimx, int nrows) {
+    int nb = hs_nblocks(P, nrows);
+    nb = nb > hs2_nblocks(dimx, nrows) ? nb : hs2_nblocks(dimx, nrows);
+    return nb > hs3_nblocks(dimx, nrows) ? nb : hs3_nblocks(dimx, nrows);
+}
 // Sum C iterations' per-block partials in a fixed order: sums[2t+{0,1}] =
 // {sum ||diff||, sum ||prev||} for t < C.
 void launch_reduce_partials(const double *partial, int nblocks, int C, double *sums,

@@ -147,10 +147,12 @@ class Registration {
     // of the first / second (nb blocks each, as the single step's)
     using StepFn2 = std::function<void(const float2 *src, float2 *dst, double *partial,
                                        double *partial2)>;
+    using StepFn3 = std::function<void(const float2 *src, float2 *dst, double *partial,
+                                       double *partial2, double *partial3)>;
 
    private:
     int run_chunked(Level &L, int niter, int nb, const StepFn &step, int &final_buf,
-                    const StepFn2 &step2 = nullptr);
+                    const StepFn2 &step2 = nullptr, const StepFn3 &step3 = nullptr);
     void ensure_device();
     void estimate_level(int s);
     int loop_hs(Level &L, int niter, float alpha, int &final_buf);

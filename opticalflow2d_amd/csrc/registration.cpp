@@ -276,7 +276,7 @@ void Registration::estimate_level(int s) {
 // iteration t is replayed from it with single steps (iteration t reads
 // src_of(a, t) and writes dst_of(a, t)).
 int Registration::run_chunked(Level &L, int niter, int nb, const StepFn &step, int &final_buf,
-                              const StepFn2 &step2) {
+                              const StepFn2 &step2, const StepFn3 &step3) {
     const double npx = (double)L.dx * L.dy;
     last_err_.clear();
     if (fixed_ && d_all_.n < 2 * (size_t)niter) {
@@ -291,18 +291,24 @@ int Registration::run_chunked(Level &L, int niter, int nb, const StepFn &step, i
         auto part = [&](int t) { return d_partial_ + (size_t)t * nb * 2; };
         int end = -1;  // pairs: the buffer holding the chunk's last iterate
         if (step2) {
-            // pairs alternate between the two buffers other than a
+            // fused launches (triples, then a pair / single tail) alternate
+            // between the two buffers other than a; kernels with fewer blocks
+            // than nb leave zeros in the rest of their partial rows
+            OF2D_HIP(hipMemsetAsync(part(0), 0, sizeof(double) * 2 * nb * C, st_));
             auto other = [&](int b) { return b == (a + 1) % 3 ? (a + 2) % 3 : (a + 1) % 3; };
             int cur = a, t = 0;
-            for (; t + 1 < C; t += 2) {
+            while (t < C) {
                 const int nxt = other(cur);
-                step2(L.est[cur].p, L.est[nxt].p, part(t), part(t + 1));
-                cur = nxt;
-            }
-            if (t < C) {
-                const int nxt = other(cur);
-                OF2D_HIP(hipMemsetAsync(part(t), 0, sizeof(double) * 2 * nb, st_));
-                step(L.est[cur].p, L.est[nxt].p, part(t));
+                if (step3 && C - t >= 3) {
+                    step3(L.est[cur].p, L.est[nxt].p, part(t), part(t + 1), part(t + 2));
+                    t += 3;
+                } else if (C - t >= 2) {
+                    step2(L.est[cur].p, L.est[nxt].p, part(t), part(t + 1));
+                    t += 2;
+                } else {
+                    step(L.est[cur].p, L.est[nxt].p, part(t));
+                    t += 1;
+                }
                 cur = nxt;
             }
             end = cur;
@@ -356,9 +362,8 @@ int Registration::run_chunked(Level &L, int niter, int nb, const StepFn &step, i
 // HS iteration loop (ImageRegistrationOpticalFlow.cpp:117-135) with fused Logger
 int Registration::loop_hs(Level &L, int niter, float alpha, int &final_buf) {
     const float alphasq = alpha * alpha;  // OpticalFlowDiffusion.cpp:70
-    // the pair kernel's block count (>= the single step's: a single step's
-    // partial row is zero-padded to it)
-    const int nb = hs2_nblocks(L.dx, L.dy);
+    // partial rows long enough for every HS kernel (zero-padded per chunk)
+    const int nb = hs_partial_blocks(L.P, L.dx, L.dy);
     const bool pairs = L.dx >= 2;
     return run_chunked(
         L, niter, nb,
@@ -368,11 +373,17 @@ int Registration::loop_hs(Level &L, int niter, float alpha, int &final_buf) {
         },
         final_buf,
         pairs ? StepFn2([&](const float2 *src, float2 *dst, double *p1, double *p2) {
-            // one ghost j-line above and below the level's fields
+            // one ghost j-line above and below the level's fields (rows beyond
+            // are clamped onto it; they only feed pixels outside the image)
             launch_hs_jacobi2(src, dst, L.dI.p, L.It.p, L.P, L.dx, L.dy, 0, L.dy, alphasq, -1,
                               L.dy + 1, p1, p2, d_status_, st_);
         })
-              : StepFn2());
+              : StepFn2(),
+        pairs ? StepFn3([&](const float2 *src, float2 *dst, double *p1, double *p2, double *p3) {
+            launch_hs_jacobi3(src, dst, L.dI.p, L.It.p, L.P, L.dx, L.dy, 0, L.dy, alphasq, -1,
+                              L.dy + 1, p1, p2, p3, d_status_, st_);
+        })
+              : StepFn3());
 }
 
 // WrapperOpticalFlow2d.cpp:105-117 -> Motion::copy_motion_to_input

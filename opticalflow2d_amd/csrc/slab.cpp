@@ -1,21 +1,23 @@
 // slab.cpp — row-slab Horn-Schunck over RCCL (the multi-GPU north-star path).
 //
 // The global dimx x dimy grid is cut into contiguous slabs of j-lines (the
-// memory-slow axis), one per process/GPU.  Iterations run in PAIRS fused into
-// one pass (hs::jacobi2_kernel): the pass computes the first iteration on the
-// owned rows plus one halo row on each side, then the second on the owned
-// rows, so each slab keeps two ghost j-lines of u above and below and, before
-// every pair, sends its first two owned j-lines to the rank above and its last
-// two to the rank below (ncclSend/ncclRecv of 2 x 8*dimx bytes each, one
-// group) — the same bytes per iteration as a one-line exchange per step, half
-// the messages.  The gradients of the halo rows are computed locally from two
-// image halo rows (set_images).  An odd tail iteration runs the single step
-// after a one-line exchange.  The Logger's norms (Logger.cpp:32-51) are fused
-// into the stencil kernel per block, reduced per rank, and all-reduced once
-// per chunk of iterations (two doubles per iteration) — the host then applies
-// the reference's break test (ImageRegistrationOpticalFlow.cpp:131-134).
-// The border rule of gradients::qlaplacian uses the GLOBAL j (gradients.h:73),
-// so the slab result equals the single-grid result bit for bit.
+// memory-slow axis), one per process/GPU.  Iterations run in TRIPLES fused into
+// one pass (hs::jacobi3_kernel; a pair or single step fills a chunk's tail):
+// the pass computes the first iteration on the owned rows plus two halo rows
+// on each side, the second with one, the third on the owned rows, so each slab
+// keeps three ghost j-lines of u above and below and, before every fused
+// launch of K iterations, sends its first K owned j-lines to the rank above
+// and its last K to the rank below (ncclSend/ncclRecv, one group) — the same
+// bytes per iteration as a one-line exchange per step, a third of the
+// messages.  The exchange runs on its own stream while the interior row bands
+// compute; only the outer bands wait for it.  The gradients of the halo rows
+// are computed locally from three image halo rows (set_images).  The Logger's
+// norms (Logger.cpp:32-51) are fused into the stencil kernels per block,
+// reduced per rank, and all-reduced once per chunk of iterations (two doubles
+// per iteration) — the host then applies the reference's break test
+// (ImageRegistrationOpticalFlow.cpp:131-134).  The border rule of
+// gradients::qlaplacian uses the GLOBAL j (gradients.h:73), so the slab result
+// equals the single-grid result bit for bit.
 //
 // The slab path registers with zero initial motion, one level, one refine:
 // warp2d by a zero field is the identity (src/Image.cpp:144-173 with fx=fy=0),
@@ -82,7 +84,7 @@ int sguard(of2d_slab *s, F &&f) {
     }
 }
 
-// `lines` (1 or 2) boundary j-lines to each neighbour, on stream `st`
+// `lines` (1..3) boundary j-lines to each neighbour, on stream `st`
 void halo_exchange(of2d_slab *s, float2 *u, int lines, hipStream_t st) {
     if (s->nranks == 1) return;
     const long P = s->P;
@@ -133,7 +135,7 @@ int of2d_slab_create(of2d_slab **out, int dimx, int dimy, float alpha, int rank,
         if (of2d_slab_bounds(dimy, rank, nranks, &s->rb, &s->re) != OF2D_OK)
             throw std::invalid_argument("slab: bad rank/nranks");
         s->nrows = s->re - s->rb;
-        if (s->nrows < 2) throw std::invalid_argument("slab: fewer than 2 j-lines per rank");
+        if (s->nrows < 3) throw std::invalid_argument("slab: fewer than 3 j-lines per rank");
         s->dimx = dimx;
         s->dimy = dimy;
         s->rank = rank;
@@ -148,18 +150,18 @@ int of2d_slab_create(of2d_slab **out, int dimx, int dimy, float alpha, int rank,
         OF2D_HIP(hipStreamCreateWithFlags(&s->comm_st, hipStreamNonBlocking));
         OF2D_HIP(hipEventCreateWithFlags(&s->ev_src, hipEventDisableTiming));
         OF2D_HIP(hipEventCreateWithFlags(&s->ev_halo, hipEventDisableTiming));
-        for (auto &f : s->u) f.alloc(dimx, s->nrows, 2);  // two ghost j-lines each side
-        s->dI.alloc(dimx, s->nrows);
-        s->It.alloc(dimx, s->nrows);
-        s->Iref.alloc(dimx, s->nrows, 2);
-        s->Imov.alloc(dimx, s->nrows, 2);
-        const int nb = std::max(of2d::hs_nblocks(s->P, s->nrows), of2d::hs2_nblocks(dimx, s->nrows));
+        for (auto &f : s->u) f.alloc(dimx, s->nrows, 3);  // three ghost j-lines each side
+        s->dI.alloc(dimx, s->nrows, 2);
+        s->It.alloc(dimx, s->nrows, 2);
+        s->Iref.alloc(dimx, s->nrows, 3);
+        s->Imov.alloc(dimx, s->nrows, 3);
+        const int nb = of2d::hs_partial_blocks(s->P, dimx, s->nrows);
         OF2D_HIP(hipMalloc(&s->d_partial, sizeof(double) * 2 * (size_t)nb * s->chunk));
         OF2D_HIP(hipMalloc(&s->d_sums, sizeof(double) * 2 * s->chunk));
         OF2D_HIP(hipMalloc(&s->d_status, 64 * sizeof(unsigned)));
         OF2D_HIP(hipMemset(s->d_status, 0, 64 * sizeof(unsigned)));
         OF2D_HIP(hipDeviceSynchronize());  // null-stream memset vs the non-blocking stream
-        OF2D_HIP(hipMalloc(&s->d_stage, sizeof(double) * 2 * (size_t)dimx * (s->nrows + 4)));
+        OF2D_HIP(hipMalloc(&s->d_stage, sizeof(double) * 2 * (size_t)dimx * (s->nrows + 6)));
         s->hs.ensure(s->chunk);
         if (nranks > 1) {
             if (!uid || id_len < (int)sizeof(ncclUniqueId))
@@ -181,23 +183,24 @@ int of2d_slab_create(of2d_slab **out, int dimx, int dimy, float alpha, int rank,
 int of2d_slab_set_images(of2d_slab *s, const double *Iref_rows, const double *Imov_rows) {
     if (!s || !Iref_rows || !Imov_rows) return OF2D_ERR_INVALID_ARGUMENT;
     return sguard(s, [&] {
-        // rows [rb-2, re+2) clipped to [0, dimy) -> local rows [-up2, nrows+dn2)
-        const int up2 = std::min(2, s->rb), dn2 = std::min(2, s->dimy - s->re);
-        const int rows = s->nrows + up2 + dn2;
+        // rows [rb-3, re+3) clipped to [0, dimy) -> local rows [-up3, nrows+dn3)
+        const int up3 = std::min(3, s->rb), dn3 = std::min(3, s->dimy - s->re);
+        const int rows = s->nrows + up3 + dn3;
         for (int which = 0; which < 2; which++) {
             const double *src = which ? Imov_rows : Iref_rows;
             of2d::Field<float> &dst = which ? s->Imov : s->Iref;
             OF2D_HIP(hipMemcpyAsync(s->d_stage, src, sizeof(double) * s->dimx * rows,
                                     hipMemcpyHostToDevice, s->st));
-            of2d::launch_d2f(s->d_stage, s->dimx, rows, dst.p - (long)up2 * s->P, s->P, 0,
+            of2d::launch_d2f(s->d_stage, s->dimx, rows, dst.p - (long)up3 * s->P, s->P, 0,
                              s->st);
         }
         // IterativeSolver::set_derivatives(Iref, Iaux = Imov) on the owned rows
-        // plus the halo row on each side that the pair kernel's first step needs
-        const int up1 = std::min(1, s->rb), dn1 = std::min(1, s->dimy - s->re);
-        const long o = -(long)up1 * s->P;
+        // plus the two halo rows on each side that the fused kernels' first
+        // steps need
+        const int up2 = std::min(2, s->rb), dn2 = std::min(2, s->dimy - s->re);
+        const long o = -(long)up2 * s->P;
         of2d::launch_gradients_rows(s->Iref.p + o, s->Imov.p + o, s->dI.p + o, s->It.p + o,
-                                    s->dimx, s->nrows + up1 + dn1, s->P, s->rb - up1, s->dimy,
+                                    s->dimx, s->nrows + up2 + dn2, s->P, s->rb - up2, s->dimy,
                                     s->st);
         for (auto &f : s->u) f.zero(s->st);
         s->fin = 0;
@@ -209,33 +212,39 @@ int of2d_slab_run(of2d_slab *s, int niter, int fixed_iters, int *iters_done) {
     if (!s) return OF2D_ERR_INVALID_ARGUMENT;
     return sguard(s, [&] {
         const float alphasq = s->alpha * s->alpha;
-        // partial rows sized for the pair kernel; a single step's are zero-padded
-        const int nb = std::max(of2d::hs_nblocks(s->P, s->nrows), of2d::hs2_nblocks(s->dimx, s->nrows));
+        // partial rows long enough for every kernel; zeroed per chunk
+        const int nb = of2d::hs_partial_blocks(s->P, s->dimx, s->nrows);
         const double npx = (double)s->dimx * s->dimy;
         auto src_of = [](int a, int t) { return t == 0 ? a : (t % 2 == 1 ? (a + 1) % 3 : (a + 2) % 3); };
         auto dst_of = [](int a, int t) { return t % 2 == 0 ? (a + 1) % 3 : (a + 2) % 3; };
-        // two iterations in one pass from buffer `in` to buffer `out`.  Only the
-        // first and last row band read the ghost lines, so with neighbours the
-        // exchange runs on comm_st while the interior bands run on st: the
-        // exchange reads owned lines of `in` (no kernel writes `in`) and
-        // writes its ghost lines (read by the outer bands only, after ev_halo).
-        const int nbands = of2d::hs2_nbands(s->nrows);
-        auto pair = [&](int in, int out, double *p1, double *p2) {
+        // K (2 or 3) iterations in one pass from buffer `in` to buffer `out`.
+        // Only the first and last row band read the ghost lines, so with
+        // neighbours the exchange runs on comm_st while the interior bands run
+        // on st: the exchange reads owned lines of `in` (no kernel writes `in`)
+        // and writes its ghost lines (read by the outer bands only, after
+        // ev_halo).
+        auto fused = [&](int K, int in, int out, double *p1, double *p2, double *p3) {
             float2 *uin = s->u[in].p;
+            const int nbands = K == 3 ? of2d::hs3_nbands(s->nrows) : of2d::hs2_nbands(s->nrows);
             auto bands = [&](int lo, int hi) {
-                of2d::launch_hs_jacobi2(uin, s->u[out].p, s->dI.p, s->It.p, s->P, s->dimx,
-                                        s->nrows, s->rb, s->dimy, alphasq, -2, s->nrows + 2, p1,
-                                        p2, s->d_status, s->st, lo, hi);
+                if (K == 3)
+                    of2d::launch_hs_jacobi3(uin, s->u[out].p, s->dI.p, s->It.p, s->P, s->dimx,
+                                            s->nrows, s->rb, s->dimy, alphasq, -3, s->nrows + 3,
+                                            p1, p2, p3, s->d_status, s->st, lo, hi);
+                else
+                    of2d::launch_hs_jacobi2(uin, s->u[out].p, s->dI.p, s->It.p, s->P, s->dimx,
+                                            s->nrows, s->rb, s->dimy, alphasq, -3, s->nrows + 3,
+                                            p1, p2, s->d_status, s->st, lo, hi);
             };
             if (s->nranks == 1) {
                 bands(0, nbands);
             } else if (nbands < 3) {
-                halo_exchange(s, uin, 2, s->st);
+                halo_exchange(s, uin, K, s->st);
                 bands(0, nbands);
             } else {
                 OF2D_HIP(hipEventRecord(s->ev_src, s->st));  // `in` complete
                 OF2D_HIP(hipStreamWaitEvent(s->comm_st, s->ev_src, 0));
-                halo_exchange(s, uin, 2, s->comm_st);
+                halo_exchange(s, uin, K, s->comm_st);
                 OF2D_HIP(hipEventRecord(s->ev_halo, s->comm_st));
                 bands(1, nbands - 1);
                 OF2D_HIP(hipStreamWaitEvent(s->st, s->ev_halo, 0));
@@ -268,14 +277,25 @@ int of2d_slab_run(of2d_slab *s, int niter, int fixed_iters, int *iters_done) {
         while (k0 < niter && done < 0) {
             const int C = std::min(s->chunk, niter - k0);
             auto part = [&](int t) { return s->d_partial + (size_t)t * nb * 2; };
-            // pairs (and an odd tail step) alternate between the two buffers other
-            // than the chunk's start buffer a, which stays intact for a replay
+            // triples (then a pair / single tail) alternate between the two
+            // buffers other than the chunk's start buffer a, which stays intact
+            // for a replay; kernels with fewer blocks than nb leave zeros
+            OF2D_HIP(hipMemsetAsync(part(0), 0, sizeof(double) * 2 * nb * C, s->st));
             auto other = [&](int b) { return b == (a + 1) % 3 ? (a + 2) % 3 : (a + 1) % 3; };
             int cur = a, tp = 0;
-            for (; tp + 1 < C; tp += 2, cur = other(cur)) pair(cur, other(cur), part(tp), part(tp + 1));
-            if (tp < C) {
-                single(cur, other(cur), part(tp));
-                cur = other(cur);
+            while (tp < C) {
+                const int nxt = other(cur);
+                if (C - tp >= 3) {
+                    fused(3, cur, nxt, part(tp), part(tp + 1), part(tp + 2));
+                    tp += 3;
+                } else if (C - tp == 2) {
+                    fused(2, cur, nxt, part(tp), part(tp + 1), nullptr);
+                    tp += 2;
+                } else {
+                    single(cur, nxt, part(tp));
+                    tp += 1;
+                }
+                cur = nxt;
             }
             if (fixed_iters) {
                 // no break to decide: keep every chunk's sums on the device and
@@ -363,14 +383,14 @@ int of2d_slab_time_kernel(of2d_slab *s, int nlaunch, double *avg_us) {
     if (!s || nlaunch <= 0 || !avg_us) return OF2D_ERR_INVALID_ARGUMENT;
     return sguard(s, [&] {
         const float alphasq = s->alpha * s->alpha;
-        // the pair kernel (two iterations per launch): warm-up launch, then
+        // the triple kernel (three iterations per launch): warm-up launch, then
         // nlaunch back-to-back launches between two events
-        const int nb = std::max(of2d::hs_nblocks(s->P, s->nrows), of2d::hs2_nblocks(s->dimx, s->nrows));
-        double *p2 = s->d_partial + (size_t)nb * 2;
+        const int nb = of2d::hs_partial_blocks(s->P, s->dimx, s->nrows);
+        double *p2 = s->d_partial + (size_t)nb * 2, *p3 = s->d_partial + (size_t)nb * 4;
         auto go = [&](int k) {
-            of2d::launch_hs_jacobi2(s->u[1 + (k & 1)].p, s->u[2 - (k & 1)].p, s->dI.p, s->It.p,
-                                    s->P, s->dimx, s->nrows, s->rb, s->dimy, alphasq, -2,
-                                    s->nrows + 2, s->d_partial, p2, s->d_status, s->st);
+            of2d::launch_hs_jacobi3(s->u[1 + (k & 1)].p, s->u[2 - (k & 1)].p, s->dI.p, s->It.p,
+                                    s->P, s->dimx, s->nrows, s->rb, s->dimy, alphasq, -3,
+                                    s->nrows + 3, s->d_partial, p2, p3, s->d_status, s->st);
         };
         go(0);
         OF2D_HIP(hipEventRecord(s->ev0, s->st));

@@ -46,7 +46,7 @@ int max_partial_blocks(const Level &L, int reg) {
     if (reg == 3 || reg == 4) return conv_nblocks(L.dx, L.dy);
     if (reg == 2 || reg == 5) return increment_nblocks(L.dx, L.dy);
     if (reg == 1) return curv_nblocks(L.dx, L.dy);
-    return std::max(hs_nblocks(L.P, L.dy), hs2_nblocks(L.dx, L.dy));
+    return hs_partial_blocks(L.P, L.dx, L.dy);
 }
 
 }  // namespace solvers

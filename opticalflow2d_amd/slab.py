@@ -27,11 +27,11 @@ def slab_bounds(dimy: int, rank: int, nranks: int) -> Tuple[int, int]:
 
 
 def halo_rows(dimy: int, rank: int, nranks: int) -> Tuple[int, int]:
-    """Image rows a rank must supply: [row_begin-2, row_end+2) clipped (the
-    pair kernel's first step covers one halo j-line, whose gradients need one
+    """Image rows a rank must supply: [row_begin-3, row_end+3) clipped (the
+    fused kernels' first step covers two halo j-lines, whose gradients need one
     more)."""
     b, e = slab_bounds(dimy, rank, nranks)
-    return max(b - 2, 0), min(e + 2, dimy)
+    return max(b - 3, 0), min(e + 3, dimy)
 
 
 def rccl_unique_id() -> bytes:
@@ -66,7 +66,7 @@ class SlabSolver:
         check(st, _lib.lib().of2d_slab_last_error(self._h).decode())
 
     def set_images(self, Iref_rows: np.ndarray, Imov_rows: np.ndarray) -> None:
-        """Rows [row_begin-2, row_end+2) (clipped, see halo_rows) of the global
+        """Rows [row_begin-3, row_end+3) (clipped, see halo_rows) of the global
         images as arrays of shape [dimx, rows] (column-major, x fastest)."""
         lo, hi = halo_rows(self.dimy, self.rank, self.nranks)
         n = self.dimx * (hi - lo)

@@ -2,12 +2,12 @@
 
 Each rank takes its slab from the library's own partition function
 (of2d_slab_bounds) and runs the protocol opticalflow2d_amd/csrc/slab.cpp runs
-over RCCL: iterations in pairs, two ghost j-lines above and below exchanged
-before every pair (the first two / last two owned lines), the pair's first step
-computed on the owned rows plus one halo row each side (whose gradients come
-from two image halo rows), the second on the owned rows; an odd tail iteration
-after a one-line exchange; the global-j border rule; the Logger sums of the
-owned rows all-reduced per iteration.  The step itself is a
+over RCCL: chunks of 32 iterations run as fused launches of K = 3 (then a
+pair / single tail); before each launch K ghost j-lines above and below are
+exchanged (the first K / last K owned lines); step k of a launch is computed
+on the owned rows plus K-k halo rows on each side (their gradients come from
+image halo rows); the global-j border rule; the Logger sums of the owned rows
+all-reduced per iteration.  The step itself is a
 numpy float32 restatement (elementwise IEEE ops in the reference's order).
 The gathered motion must equal the single-grid oracle bit for bit, and the
 iteration count with convergence on must match the oracle's.
@@ -74,36 +74,37 @@ def _worker(rank, world, port, dimx, dimy, niter, fixed, outdir):
     It = np.zeros(dimx * dimy, np.float32)
     O.lib().oracle_spatial_derivative(I, dimx, dimy, dI)
     O.lib().oracle_temporal_derivative(Ir, I, dimx * dimy, It)
-    # owned rows plus one halo row each side (zero outside the image)
+    # owned rows plus two halo rows each side (zero outside the image)
     dIf = dI.reshape(dimy, dimx, 2)
     Itf = It.reshape(dimy, dimx)
     rows = e - b
-    dIh = np.zeros((rows + 2, dimx, 2), np.float32)
-    Ith = np.zeros((rows + 2, dimx), np.float32)
-    lo, hi = max(b - 1, 0), min(e + 1, dimy)
-    dIh[lo - (b - 1):hi - (b - 1)] = dIf[lo:hi]
-    Ith[lo - (b - 1):hi - (b - 1)] = Itf[lo:hi]
-    u = np.zeros((rows + 4, dimx, 2), np.float32)  # owned rows at u[2:rows+2]
+    H = 3  # ghost j-lines of u
+    dIh = np.zeros((rows + 4, dimx, 2), np.float32)
+    Ith = np.zeros((rows + 4, dimx), np.float32)
+    lo, hi = max(b - 2, 0), min(e + 2, dimy)
+    dIh[lo - (b - 2):hi - (b - 2)] = dIf[lo:hi]
+    Ith[lo - (b - 2):hi - (b - 2)] = Itf[lo:hi]
+    u = np.zeros((rows + 2 * H, dimx, 2), np.float32)  # owned rows at u[H:H+rows]
     alpha = F(0.2)
     alphasq = alpha * alpha
 
     def exchange(lines):
         reqs = []
         if rank > 0:
-            reqs.append(dist.isend(torch.from_numpy(u[2:2 + lines].copy()), rank - 1))
+            reqs.append(dist.isend(torch.from_numpy(u[H:H + lines].copy()), rank - 1))
             up = torch.empty((lines, dimx, 2), dtype=torch.float32)
             reqs.append(dist.irecv(up, rank - 1))
         if rank < world - 1:
-            reqs.append(dist.isend(torch.from_numpy(u[rows + 2 - lines:rows + 2].copy()),
+            reqs.append(dist.isend(torch.from_numpy(u[H + rows - lines:H + rows].copy()),
                                    rank + 1))
             dn = torch.empty((lines, dimx, 2), dtype=torch.float32)
             reqs.append(dist.irecv(dn, rank + 1))
         for r in reqs:
             r.wait()
         if rank > 0:
-            u[2 - lines:2] = up.numpy()
+            u[H - lines:H] = up.numpy()
         if rank < world - 1:
-            u[rows + 2:rows + 2 + lines] = dn.numpy()
+            u[H + rows:H + rows + lines] = dn.numpy()
 
     def sums(new, old):
         d = (new - old).astype(np.float64)
@@ -114,35 +115,41 @@ def _worker(rank, world, port, dimx, dimy, niter, fixed, outdir):
         dist.all_reduce(t)
         return logger_error(float(t[0]), float(t[1]), dimx * dimy)
 
+    def fused(K):
+        """K iterations of one fused launch: states of the owned rows after each."""
+        exchange(K)
+        w = u[H - K:H + rows + K]  # owned rows + K neighbour lines each side
+        states = []
+        for k in range(1, K + 1):
+            h = K - k  # halo rows computed by step k
+            w, _, _ = hs_step(w, dIh[2 - h:2 + rows + h], Ith[2 - h:2 + rows + h], alphasq,
+                              b - h, dimy)
+            states.append(w[h:h + rows].copy())
+        return states
+
     done = niter
-    k = 0
-    while k < niter:
-        if k + 1 < niter:  # a pair
-            exchange(2)
-            u1, _, _ = hs_step(u, dIh, Ith, alphasq, b - 1, dimy)  # rows -1 .. rows
-            u2, _, _ = hs_step(u1, dIh[1:-1], Ith[1:-1], alphasq, b, dimy)  # owned rows
-            errs = [sums(u1[1:-1], u[2:rows + 2]), sums(u2, u1[1:-1])]
-            states = [u1[1:-1], u2]
-            steps = 2
-        else:  # odd tail: a single step after a one-line exchange
-            exchange(1)
-            w = u[1:rows + 3]
-            u1, _, _ = hs_step(w, dIh[1:-1], Ith[1:-1], alphasq, b, dimy)
-            errs = [sums(u1, u[2:rows + 2])]
-            states = [u1]
-            steps = 1
-        stop = False
-        for i in range(steps):
-            if not fixed and errs[i] < F(0.001) and k + i > 1:
-                u[2:rows + 2] = states[i]
-                done = k + i + 1
-                stop = True
-                break
-        if stop:
-            break
-        u[2:rows + 2] = states[-1]
-        k += steps
-    np.save(os.path.join(outdir, f"slab{rank}.npy"), u[2:rows + 2])
+    k0 = 0
+    stop = False
+    while k0 < niter and not stop:
+        C = min(32, niter - k0)
+        t = 0
+        while t < C and not stop:
+            K = 3 if C - t >= 3 else C - t
+            prev = u[H:H + rows].copy()
+            states = fused(K)
+            olds = [prev] + states[:-1]
+            for i in range(K):
+                err = sums(states[i], olds[i])
+                if not fixed and err < F(0.001) and k0 + t + i > 1:
+                    u[H:H + rows] = states[i]
+                    done = k0 + t + i + 1
+                    stop = True
+                    break
+            if not stop:
+                u[H:H + rows] = states[-1]
+            t += K
+        k0 += C
+    np.save(os.path.join(outdir, f"slab{rank}.npy"), u[H:H + rows])
     np.save(os.path.join(outdir, f"iters{rank}.npy"), np.array([done]))
     dist.barrier()
     dist.destroy_process_group()
@@ -159,7 +166,8 @@ def _free_port():
 @pytest.mark.parametrize("world,dimx,dimy,niter,fixed", [(2, 48, 40, 12, True),
                                                          (2, 40, 33, 600, False),
                                                          (3, 32, 29, 11, True),
-                                                         (4, 24, 9, 7, True)])
+                                                         (4, 24, 12, 37, True),
+                                                         (3, 20, 10, 400, False)])
 def test_row_slab_halo_protocol_matches_single_grid(oracle, world, dimx, dimy, niter, fixed):
     import torch.multiprocessing as mp
     with tempfile.TemporaryDirectory() as d:

@@ -294,6 +294,8 @@ int main(int argc, char **argv) {
     const bool product_only = argc > 3 && strcmp(argv[3], "product") == 0;
     if (argc > 3 && strcmp(argv[3], "pair") == 0)  // the product pair kernel (PMC runs)
         return run2<32, 4, 2, true>(b, iters, "two-step 32r 4w xcd (product)", bytes);
+    if (argc > 3 && strcmp(argv[3], "triple") == 0)  // the product triple kernel (PMC runs)
+        return run3<32, 4>(b, iters, "three-step 32r 4w xcd (product)", bytes);
     if (argc > 3 && strcmp(argv[3], "two") == 0) {
         int b2 = 0;
         V3(32, 2, 4, true, true, false);

@@ -38,8 +38,9 @@ def main():
     fetch = per_kernel(fetch_csv, "FETCH_SIZE")  # KB
     write = per_kernel(write_csv, "WRITE_SIZE")  # KB
     probe = [k for k in fetch if "probe_kernel" in k][0]
-    jac = ([k for k in fetch if "jacobi2_kernel" in k] or [k for k in fetch if "jacobi_kernel" in k])[0]
-    pair = "jacobi2_kernel" in jac
+    jac = ([k for k in fetch if "jacobi3_kernel" in k] or [k for k in fetch if "jacobi2_kernel" in k]
+           or [k for k in fetch if "jacobi_kernel" in k])[0]
+    per_launch = 3 if "jacobi3_kernel" in jac else (2 if "jacobi2_kernel" in jac else 1)
     px = P * n  # the probe sweeps the pitched rows
     probe_read_true = 20.0 * px
     probe_write_true = 8.0 * px
@@ -59,7 +60,7 @@ def main():
         "write_bytes_per_launch": wr,
         "bytes_per_launch": rd + wr,
         "algorithmic_bytes_per_launch": alg,
-        "iterations_per_launch": 2 if pair else 1,
+        "iterations_per_launch": per_launch,
         "traffic_over_algorithmic": (rd + wr) / alg,
         "source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes) on tools/hs_variants, "
                   "calibrated on the probe kernel's known bytes",
