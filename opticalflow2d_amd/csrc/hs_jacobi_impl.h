@@ -432,12 +432,15 @@ __global__ __launch_bounds__(64 * WAVES) void jacobi2_kernel(
 // partial3.  Measured in tools/hs_variants.hip ("two"): ~10 % less time per
 // iteration than the pair kernel at 4096^2 (47.6 vs 52.7 us) — the kernels are
 // now issue/latency-bound more than HBM-bound.  band0 as in jacobi2_kernel.
+// ROWS > 0: j-lines per wave fixed at compile time; ROWS == 0: `rows` (chosen
+// by the launcher so that the grid fills whole rounds of resident blocks)
 template <int ROWS, int WAVES, bool XCD = true>
 __global__ __launch_bounds__(64 * WAVES) void jacobi3_kernel(
     const float2 *__restrict__ uo, float2 *__restrict__ un, const float2 *__restrict__ dI,
     const float *__restrict__ It, int P, int dimx, int nrows, int row0, int dimy, float alphasq,
     int glo, int ghi, double *__restrict__ partial, double *__restrict__ partial2,
-    double *__restrict__ partial3, unsigned *__restrict__ status, int band0, int gx, int gy) {
+    double *__restrict__ partial3, unsigned *__restrict__ status, int band0, int gx, int gy,
+    int rows = ROWS) {
     int bx = (int)blockIdx.x, by = (int)blockIdx.y;
     if constexpr (XCD) {
         if (!xcd_block(gx, gy, bx, by)) return;
@@ -448,8 +451,8 @@ __global__ __launch_bounds__(64 * WAVES) void jacobi3_kernel(
     const bool own = lane >= 2 && lane <= 61 && x < dimx;
     const bool xin = x >= 0 && x + 2 <= P;
     const int band = band0 + by;
-    const int jbeg = (band * WAVES + wave) * ROWS;
-    const int jend = min(jbeg + ROWS, nrows);
+    const int jbeg = (band * WAVES + wave) * rows;
+    const int jend = min(jbeg + rows, nrows);
     double s1d = 0.0, s1p = 0.0, s2d = 0.0, s2p = 0.0, s3d = 0.0, s3p = 0.0;
     unsigned bad = 0;
     auto cl = [&](int j) { return min(max(j, glo), ghi - 1); };

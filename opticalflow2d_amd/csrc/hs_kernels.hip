@@ -54,7 +54,7 @@ void launch_hs_jacobi2(const float2 *u_old, float2 *u_new, const float2 *dI, con
     OF2D_HIP(hipGetLastError());
 }
 
-static const auto kHsJacobi3 = &hs::jacobi3_kernel<kHs3Rows, kHs3Waves, true>;
+static const auto kHsJacobi3 = &hs::jacobi3_kernel<0, kHs3Waves, true>;
 
 void launch_hs_jacobi3(const float2 *u_old, float2 *u_new, const float2 *dI, const float *It,
                        int P, int dimx, int nrows, int row0, int dimy, float alphasq, int glo,
@@ -62,7 +62,7 @@ void launch_hs_jacobi3(const float2 *u_old, float2 *u_new, const float2 *dI, con
                        unsigned *status, hipStream_t st, int band_lo, int band_hi) {
     if (P % kHsStrip != 0 || nrows <= 0 || dimx > P || dimx < 2 || glo > -1 || ghi < nrows + 1)
         throw std::invalid_argument("launch_hs_jacobi3: bad geometry");
-    const int nb = hs3_nbands(nrows);
+    const int nb = hs3_nbands(dimx, nrows);
     if (band_lo < 0) band_lo = 0;
     if (band_hi < 0) band_hi = nb;
     if (band_lo > band_hi || band_hi > nb) throw std::invalid_argument("launch_hs_jacobi3: bands");
@@ -72,7 +72,7 @@ void launch_hs_jacobi3(const float2 *u_old, float2 *u_new, const float2 *dI, con
     const dim3 gl(8 * ((g.x * g.y + 7) / 8));
     hipLaunchKernelGGL(kHsJacobi3, gl, dim3(64 * kHs3Waves), 0, st, u_old, u_new, dI, It, P,
                        dimx, nrows, row0, dimy, alphasq, glo, ghi, partial, partial2, partial3,
-                       status, band_lo, (int)g.x, (int)g.y);
+                       status, band_lo, (int)g.x, (int)g.y, hs3_rows(dimx, nrows));
     OF2D_HIP(hipGetLastError());
 }
 

@@ -92,18 +92,33 @@ void launch_hs_jacobi2(const float2 *u_old, float2 *u_new, const float2 *dI, con
 // three launch_hs_jacobi calls; rows [glo, ghi) readable as for the pair
 // kernel (the first two steps also cover two / one halo rows each side).
 constexpr int kHs3Out = 120;  // output columns per wave (hs_jacobi_impl.h)
-constexpr int kHs3Rows = 32;
 constexpr int kHs3Waves = 4;
+// j-lines per wave: the 4-wave blocks (4 resident per CU at the kernel's
+// register count, 256 CUs) should fill whole rounds of 1024 blocks — a grid of
+// 1120 blocks at 4096^2 with 32 j-lines ran a 9 % second round; 36 j-lines
+// (1015 blocks) is 3 % faster.  Rows per wave stay within [16, 64].
+inline int hs3_rows(int dimx, int nrows) {
+    const int gx = (dimx + kHs3Out - 1) / kHs3Out;
+    const int per_round = gx <= 1024 ? 1024 / gx : 1;  // bands per round of blocks
+    int rounds = 1;
+    for (;;) {
+        const int bands = per_round * rounds;
+        const int rows = (nrows + kHs3Waves * bands - 1) / (kHs3Waves * bands);
+        // below 16 j-lines per wave the 6 + 4 halo rows would dominate
+        if (rows <= 64 || bands >= nrows) return rows < 16 ? 16 : rows;
+        rounds++;
+    }
+}
+inline int hs3_nbands(int dimx, int nrows) {
+    const int r = kHs3Waves * hs3_rows(dimx, nrows);
+    return (nrows + r - 1) / r;
+}
 inline dim3 hs3_grid(int dimx, int nrows) {
-    return dim3((dimx + kHs3Out - 1) / kHs3Out,
-                (nrows + kHs3Rows * kHs3Waves - 1) / (kHs3Rows * kHs3Waves));
+    return dim3((dimx + kHs3Out - 1) / kHs3Out, hs3_nbands(dimx, nrows));
 }
 inline int hs3_nblocks(int dimx, int nrows) {
     dim3 g = hs3_grid(dimx, nrows);
     return int(g.x * g.y);
-}
-inline int hs3_nbands(int nrows) {
-    return (nrows + kHs3Rows * kHs3Waves - 1) / (kHs3Rows * kHs3Waves);
 }
 void launch_hs_jacobi3(const float2 *u_old, float2 *u_new, const float2 *dI, const float *It,
                        int P, int dimx, int nrows, int row0, int dimy, float alphasq, int glo,

@@ -225,7 +225,8 @@ int of2d_slab_run(of2d_slab *s, int niter, int fixed_iters, int *iters_done) {
         // ev_halo).
         auto fused = [&](int K, int in, int out, double *p1, double *p2, double *p3) {
             float2 *uin = s->u[in].p;
-            const int nbands = K == 3 ? of2d::hs3_nbands(s->nrows) : of2d::hs2_nbands(s->nrows);
+            const int nbands =
+                K == 3 ? of2d::hs3_nbands(s->dimx, s->nrows) : of2d::hs2_nbands(s->nrows);
             auto bands = [&](int lo, int hi) {
                 if (K == 3)
                     of2d::launch_hs_jacobi3(uin, s->u[out].p, s->dI.p, s->It.p, s->P, s->dimx,

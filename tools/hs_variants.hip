@@ -173,7 +173,7 @@ int run3(const Bufs &b, int iters, const char *name, double bytes) {
     auto launch3 = [&](const float2 *in, float2 *out) {
         hipLaunchKernelGGL(k, gl, dim3(64 * WAVES), 0, 0, in, out, b.dI, b.It, b.P, b.dimx, b.dimy,
                            0, b.dimy, 0.01f, -1, b.dimy + 1, b.partial, p2, p3, b.status, 0,
-                           (int)g.x, (int)g.y);
+                           (int)g.x, (int)g.y, ROWS);
     };
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
@@ -295,14 +295,16 @@ int main(int argc, char **argv) {
     if (argc > 3 && strcmp(argv[3], "pair") == 0)  // the product pair kernel (PMC runs)
         return run2<32, 4, 2, true>(b, iters, "two-step 32r 4w xcd (product)", bytes);
     if (argc > 3 && strcmp(argv[3], "triple") == 0)  // the product triple kernel (PMC runs)
-        return run3<32, 4>(b, iters, "three-step 32r 4w xcd (product)", bytes);
+        return run3<36, 4>(b, iters, "three-step 36r 4w xcd (product at 4096^2)", bytes);
     if (argc > 3 && strcmp(argv[3], "two") == 0) {
         int b2 = 0;
         V3(32, 2, 4, true, true, false);
         b2 |= run2<32, 4>(b, iters, "two-step 32r 4w", bytes);
         b2 |= run3<32, 4>(b, iters, "three-step 32r 4w xcd", bytes);
-        b2 |= run3<32, 2>(b, iters, "three-step 32r 2w xcd", bytes);
-        b2 |= run3<64, 2>(b, iters, "three-step 64r 2w xcd", bytes);
+        b2 |= run3<36, 4>(b, iters, "three-step 36r 4w xcd", bytes);
+        b2 |= run3<37, 4>(b, iters, "three-step 37r 4w xcd", bytes);
+        b2 |= run3<40, 4>(b, iters, "three-step 40r 4w xcd", bytes);
+        b2 |= run3<72, 2>(b, iters, "three-step 72r 2w xcd", bytes);
         b2 |= run2<32, 4, 2, true>(b, iters, "two-step 32r 4w xcd", bytes);
         b2 |= run2<32, 2, 2, true>(b, iters, "two-step 32r 2w xcd", bytes);
         b2 |= run2<16, 4, 2, true>(b, iters, "two-step 16r 4w xcd", bytes);
