@@ -434,8 +434,8 @@ __global__ __launch_bounds__(64 * WAVES) void jacobi2_kernel(
 // now issue/latency-bound more than HBM-bound.  band0 as in jacobi2_kernel.
 // ROWS > 0: j-lines per wave fixed at compile time; ROWS == 0: `rows` (chosen
 // by the launcher so that the grid fills whole rounds of resident blocks)
-template <int ROWS, int WAVES, bool XCD = true>
-__global__ __launch_bounds__(64 * WAVES) void jacobi3_kernel(
+template <int ROWS, int WAVES, bool XCD = true, int MINB = 1>
+__global__ __launch_bounds__(64 * WAVES, MINB) void jacobi3_kernel(
     const float2 *__restrict__ uo, float2 *__restrict__ un, const float2 *__restrict__ dI,
     const float *__restrict__ It, int P, int dimx, int nrows, int row0, int dimy, float alphasq,
     int glo, int ghi, double *__restrict__ partial, double *__restrict__ partial2,

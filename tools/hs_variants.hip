@@ -162,11 +162,11 @@ int run2(const Bufs &b, int iters, const char *name, double bytes) {
 }
 
 // three iterations per launch: timed per ITERATION, checked against 6 single steps
-template <int ROWS, int WAVES>
+template <int ROWS, int WAVES, int MINB = 1>
 int run3(const Bufs &b, int iters, const char *name, double bytes) {
     const dim3 g = hs::grid3_for<ROWS, WAVES>(b.dimx, b.dimy);
     const dim3 gl(8 * ((g.x * g.y + 7) / 8));
-    auto k = hs::jacobi3_kernel<ROWS, WAVES, true>;
+    auto k = hs::jacobi3_kernel<ROWS, WAVES, true, MINB>;
     auto k1 = hs::jacobi_kernel<32, 2, 4, true, true, false>;
     const dim3 g1 = hs::grid_for<32, 2, 4>(b.P, b.dimy);
     double *p2 = b.partial + 2 * 16384, *p3 = b.partial + 4 * 16384;
@@ -300,11 +300,10 @@ int main(int argc, char **argv) {
         int b2 = 0;
         V3(32, 2, 4, true, true, false);
         b2 |= run2<32, 4>(b, iters, "two-step 32r 4w", bytes);
-        b2 |= run3<32, 4>(b, iters, "three-step 32r 4w xcd", bytes);
         b2 |= run3<36, 4>(b, iters, "three-step 36r 4w xcd", bytes);
-        b2 |= run3<37, 4>(b, iters, "three-step 37r 4w xcd", bytes);
-        b2 |= run3<40, 4>(b, iters, "three-step 40r 4w xcd", bytes);
-        b2 |= run3<72, 2>(b, iters, "three-step 72r 2w xcd", bytes);
+        b2 |= run3<36, 4, 5>(b, iters, "three-step 36r 4w xcd 5blk", bytes);
+        b2 |= run3<29, 4, 5>(b, iters, "three-step 29r 4w xcd 5blk", bytes);
+        b2 |= run3<29, 4>(b, iters, "three-step 29r 4w xcd", bytes);
         b2 |= run2<32, 4, 2, true>(b, iters, "two-step 32r 4w xcd", bytes);
         b2 |= run2<32, 2, 2, true>(b, iters, "two-step 32r 2w xcd", bytes);
         b2 |= run2<16, 4, 2, true>(b, iters, "two-step 16r 4w xcd", bytes);
