@@ -188,7 +188,7 @@ def main():
             },
             "roofline": {
                 "bound": "hbm",
-                "kernel": "of2d::hs::jacobi3_kernel<0,4,true>",
+                "kernel": "of2d::hs::jacobi3_kernel<0,4,true,4,4,true>",
                 "iterations_per_launch": ITERS_PER_LAUNCH,
                 "achieved": round(achieved, 1),
                 "peak": HBM_PEAK_GBS,

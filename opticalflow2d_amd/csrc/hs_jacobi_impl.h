@@ -89,6 +89,41 @@ __device__ __forceinline__ float2 update_px(float2 q, float gx, float gy, float 
     return make_float2(q.x - fx / den, q.y - fy / den);
 }
 
+// ---------------------------------------------------------------------------
+// fp32 division without the range-scaling steps.  The compiler expands the
+// IEEE quotient a / b as
+//   bs = div_scale(b, b, a); as, vcc = div_scale(a, b, a); r = rcp(bs)
+//   r = fma(fma(-bs, r, 1), r, r); q = as * r; q = fma(fma(-bs, q, as), r, q)
+//   q = div_fmas(fma(-bs, q, as), r, q, vcc); a / b = div_fixup(q, b, a)
+// div_scale returns its operand unchanged and clears vcc unless a or b is 0,
+// b is denormal, 1/b or a/b would be denormal, |a| < 2^-103, or a/b is within
+// 2^96 of the overflow threshold.  With b in [2^-40, 2^40) and a in 0 or
+// [2^-80, 2^50] none of these holds except a == 0, and for a == 0 (and for
+// inf / NaN operands) div_fixup returns the special value from b and a alone.
+// In that range the sequence below is therefore the compiler's sequence on
+// the same values: bit-identical quotients, with the reciprocal refinement
+// (which depends on b only) shared by every division by the same b.
+__device__ __forceinline__ float recip_refined(float b) {
+    const float r0 = __builtin_amdgcn_rcpf(b);
+    return __builtin_fmaf(__builtin_fmaf(-b, r0, 1.0f), r0, r0);
+}
+// (ax / b, ay / b) for b with refined reciprocal r, both components packed
+__device__ __forceinline__ float2 div2_unscaled(float ax, float ay, float b, float r) {
+    const v2f a = {ax, ay}, nb = {-b, -b}, rr = {r, r};
+    v2f q = a * rr;
+    v2f e = __builtin_elementwise_fma(nb, q, a);
+    q = __builtin_elementwise_fma(e, rr, q);
+    e = __builtin_elementwise_fma(nb, q, a);
+    q = __builtin_elementwise_fma(e, rr, q);
+    return make_float2(__builtin_amdgcn_div_fixupf(q.x, b, ax),
+                       __builtin_amdgcn_div_fixupf(q.y, b, ay));
+}
+// frexp exponent of v within [lo, hi] (0, inf and NaN have exponent 0)
+template <int LO, int HI>
+__device__ __forceinline__ bool exp_in(float v) {
+    return (unsigned)(__builtin_amdgcn_frexp_expf(v) - LO) <= (unsigned)(HI - LO);
+}
+
 // u rows as PXL float2 per lane
 template <int PXL>
 struct Row {
@@ -434,7 +469,7 @@ __global__ __launch_bounds__(64 * WAVES) void jacobi2_kernel(
 // now issue/latency-bound more than HBM-bound.  band0 as in jacobi2_kernel.
 // ROWS > 0: j-lines per wave fixed at compile time; ROWS == 0: `rows` (chosen
 // by the launcher so that the grid fills whole rounds of resident blocks)
-template <int ROWS, int WAVES, bool XCD = true, int MINB = 1>
+template <int ROWS, int WAVES, bool XCD = true, int MINB = 1, int UNR = 4, bool FD = true>
 __global__ __launch_bounds__(64 * WAVES, MINB) void jacobi3_kernel(
     const float2 *__restrict__ uo, float2 *__restrict__ un, const float2 *__restrict__ dI,
     const float *__restrict__ It, int P, int dimx, int nrows, int row0, int dimy, float alphasq,
@@ -453,7 +488,9 @@ __global__ __launch_bounds__(64 * WAVES, MINB) void jacobi3_kernel(
     const int band = band0 + by;
     const int jbeg = (band * WAVES + wave) * rows;
     const int jend = min(jbeg + rows, nrows);
-    double s1d = 0.0, s1p = 0.0, s2d = 0.0, s2p = 0.0, s3d = 0.0, s3p = 0.0;
+    // Logger magnitudes accumulate in fp32 per lane (<= 2 * rows values of one
+    // wave), in fp64 from the lane sums on; they only feed the convergence test
+    float s1d = 0.0f, s1p = 0.0f, s2d = 0.0f, s2p = 0.0f, s3d = 0.0f, s3p = 0.0f;
     unsigned bad = 0;
     auto cl = [&](int j) { return min(max(j, glo), ghi - 1); };
     const int xl = xin ? x : (x < 0 ? 0 : P - 2);
@@ -462,7 +499,8 @@ __global__ __launch_bounds__(64 * WAVES, MINB) void jacobi3_kernel(
     // (OpticalFlowDiffusion.cpp:78), which the three steps share
     struct G {
         Row<2> g;
-        float t[2], den[2];
+        float t[2], den[2], rcp[2];
+        bool ok;  // FD: gradients in 0 or [2^-30, 2^20), den in [2^-40, 2^40)
     };
     auto ldg = [&](int j) {
         G r;
@@ -470,9 +508,16 @@ __global__ __launch_bounds__(64 * WAVES, MINB) void jacobi3_kernel(
         const float2 tt = *reinterpret_cast<const float2 *>(It + (long)cl(j) * P + xl);
         r.t[0] = tt.x;
         r.t[1] = tt.y;
+        r.ok = true;
 #pragma unroll
-        for (int k = 0; k < 2; k++)
+        for (int k = 0; k < 2; k++) {
             r.den[k] = (alphasq + r.g.v[k].x * r.g.v[k].x) + r.g.v[k].y * r.g.v[k].y;
+            if constexpr (FD) {
+                r.rcp[k] = recip_refined(r.den[k]);
+                r.ok = r.ok && exp_in<-29, 20>(r.g.v[k].x) && exp_in<-29, 20>(r.g.v[k].y) &&
+                       exp_in<-39, 40>(r.den[k]);
+            }
+        }
         return r;
     };
     auto stepr = [&](int j, const Row<2> &m, const Row<2> &c, const Row<2> &p, const G &g,
@@ -484,33 +529,49 @@ __global__ __launch_bounds__(64 * WAVES, MINB) void jacobi3_kernel(
         right.y = dpp_from_right(c.v[0].y);
         const int jg = row0 + j;
         const bool yb = (jg == 0) || (jg == dimy - 1);
-        Row<2> o;
+        float2 q[2];
+        float sc[2];
 #pragma unroll
         for (int k = 0; k < 2; k++) {
             const float2 l = (k == 0) ? left : c.v[0];
             const float2 r = (k == 1) ? right : c.v[1];
-            float2 q;
-            q.x = (((l.x + r.x) + m.v[k].x) + p.v[k].x) / 4.0f;
-            q.y = (((l.y + r.y) + m.v[k].y) + p.v[k].y) / 4.0f;
+            q[k].x = (((l.x + r.x) + m.v[k].x) + p.v[k].x) / 4.0f;
+            q[k].y = (((l.y + r.y) + m.v[k].y) + p.v[k].y) / 4.0f;
             const int xi = x + k;
-            q = zero_if(yb || xi == 0 || xi == dimx - 1, q);
-            // update_px with the row's denominator
-            const float gx = g.g.v[k].x, gy = g.g.v[k].y;
-            const float sc = (g.t[k] + q.x * gx) + q.y * gy;
-            const float fx = gx * sc, fy = gy * sc;
+            q[k] = zero_if(yb || xi == 0 || xi == dimx - 1, q[k]);
+            sc[k] = (g.t[k] + q[k].x * g.g.v[k].x) + q[k].y * g.g.v[k].y;
             b |= (g.den[k] == 0.0f) ? 1u : 0u;
-            o.v[k] = make_float2(q.x - fx / g.den[k], q.y - fy / g.den[k]);
+        }
+        Row<2> o;
+        // sc in 0 or [2^-50, 2^30) puts the numerators gx*sc, gy*sc in the
+        // range where the unscaled division is exact (div2_unscaled)
+        if (FD && __builtin_amdgcn_ballot_w64(!(g.ok && exp_in<-49, 30>(sc[0]) &&
+                                                exp_in<-49, 30>(sc[1]))) == 0) {
+#pragma unroll
+            for (int k = 0; k < 2; k++) {
+                const float gx = g.g.v[k].x, gy = g.g.v[k].y;
+                const float2 f = div2_unscaled(gx * sc[k], gy * sc[k], g.den[k], g.rcp[k]);
+                o.v[k] = make_float2(q[k].x - f.x, q[k].y - f.y);
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < 2; k++) {
+                const float gx = g.g.v[k].x, gy = g.g.v[k].y;
+                const float fx = gx * sc[k], fy = gy * sc[k];
+                o.v[k] = make_float2(q[k].x - fx / g.den[k], q[k].y - fy / g.den[k]);
+            }
         }
         return o;
     };
     const bool in1 = x + 1 < dimx;
-    auto norms = [&](const Row<2> &nw, const Row<2> &od, double &sd, double &sp) {
-        sd += norm_d(nw.v[0].x - od.v[0].x, nw.v[0].y - od.v[0].y);
-        sp += norm_d(od.v[0].x, od.v[0].y);
-        const double d1 = norm_d(nw.v[1].x - od.v[1].x, nw.v[1].y - od.v[1].y);
-        const double p1 = norm_d(od.v[1].x, od.v[1].y);
-        sd += in1 ? d1 : 0.0;
-        sp += in1 ? p1 : 0.0;
+    auto mag = [](float a, float b) { return __builtin_amdgcn_sqrtf(a * a + b * b); };
+    auto norms = [&](const Row<2> &nw, const Row<2> &od, float &sd, float &sp) {
+        sd += mag(nw.v[0].x - od.v[0].x, nw.v[0].y - od.v[0].y);
+        sp += mag(od.v[0].x, od.v[0].y);
+        const float d1 = mag(nw.v[1].x - od.v[1].x, nw.v[1].y - od.v[1].y);
+        const float p1 = mag(od.v[1].x, od.v[1].y);
+        sd += in1 ? d1 : 0.0f;  // a select, not a product: padding may hold 0/0
+        sp += in1 ? p1 : 0.0f;
     };
     if (jbeg < nrows) {
         unsigned bx_ = 0;  // halo rows: flagged by the waves that own them
@@ -527,10 +588,12 @@ __global__ __launch_bounds__(64 * WAVES, MINB) void jacobi3_kernel(
         Row<2> wj = stepr(jbeg, p1, vj, vj1, gj, bx_);
         Row<2> nu = ldu(jbeg + 3);
         G ng = ldg(jbeg + 2);
-        for (int j = jbeg; j < jend; ++j) {
+        // one output row; the window shifts by renaming, which the unrolled
+        // copies below turn into register renames instead of moves
+        auto body = [&](int j, bool pref) __attribute__((always_inline)) {
             const Row<2> a3 = nu;  // u row j+3
             const G gj2 = ng;      // gradients row j+2
-            if (j + 1 < jend) {
+            if (pref) {
                 nu = ldu(j + 4);
                 ng = ldg(j + 3);
             }
@@ -559,25 +622,32 @@ __global__ __launch_bounds__(64 * WAVES, MINB) void jacobi3_kernel(
             wj = wj1;
             gj = gj1;
             gj1 = gj2;
+        };
+        int j = jbeg;
+        for (; j + UNR < jend; j += UNR) {
+#pragma unroll
+            for (int k = 0; k < UNR; k++) body(j + k, true);
         }
+        for (; j < jend; ++j) body(j, j + 1 < jend);
     }
+    double d1d = s1d, d1p = s1p, d2d = s2d, d2p = s2p, d3d = s3d, d3p = s3p;
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) {
-        s1d += __shfl_down(s1d, off);
-        s1p += __shfl_down(s1p, off);
-        s2d += __shfl_down(s2d, off);
-        s2p += __shfl_down(s2p, off);
-        s3d += __shfl_down(s3d, off);
-        s3p += __shfl_down(s3p, off);
+        d1d += __shfl_down(d1d, off);
+        d1p += __shfl_down(d1p, off);
+        d2d += __shfl_down(d2d, off);
+        d2p += __shfl_down(d2p, off);
+        d3d += __shfl_down(d3d, off);
+        d3p += __shfl_down(d3p, off);
     }
     __shared__ double red[6][WAVES];
     if (lane == 0) {
-        red[0][wave] = s1d;
-        red[1][wave] = s1p;
-        red[2][wave] = s2d;
-        red[3][wave] = s2p;
-        red[4][wave] = s3d;
-        red[5][wave] = s3p;
+        red[0][wave] = d1d;
+        red[1][wave] = d1p;
+        red[2][wave] = d2d;
+        red[3][wave] = d2p;
+        red[4][wave] = d3d;
+        red[5][wave] = d3p;
     }
     if (__any(bad) && lane == 0) atomicOr(status, kStatusDivZero);
     __syncthreads();

@@ -54,7 +54,9 @@ void launch_hs_jacobi2(const float2 *u_old, float2 *u_new, const float2 *dI, con
     OF2D_HIP(hipGetLastError());
 }
 
-static const auto kHsJacobi3 = &hs::jacobi3_kernel<0, kHs3Waves, true>;
+// 4 resident 4-wave blocks per CU (<= 128 VGPRs), loop unrolled 4x, unscaled
+// exact division where its range holds
+static const auto kHsJacobi3 = &hs::jacobi3_kernel<0, kHs3Waves, true, 4, 4, true>;
 
 void launch_hs_jacobi3(const float2 *u_old, float2 *u_new, const float2 *dI, const float *It,
                        int P, int dimx, int nrows, int row0, int dimy, float alphasq, int glo,
@@ -90,9 +92,9 @@ void launch_hs_jacobi(const float2 *u_old, float2 *u_new, const float2 *dI, cons
 // summation order (strided per-thread sums, wave trees, then the 16 waves in
 // order).
 __global__ __launch_bounds__(1024) void reduce_partials_kernel(const double *__restrict__ partial,
-                                                               int nblocks,
+                                                               int stride, int nblocks,
                                                                double *__restrict__ sums) {
-    const double *p = partial + (size_t)blockIdx.x * nblocks * 2;
+    const double *p = partial + (size_t)blockIdx.x * stride * 2;
     double a = 0.0, b = 0.0;
     for (int i = threadIdx.x; i < nblocks; i += 1024) {
         a += p[2 * i];
@@ -121,10 +123,24 @@ __global__ __launch_bounds__(1024) void reduce_partials_kernel(const double *__r
 }
 
 void launch_reduce_partials(const double *partial, int nblocks, int C, double *sums,
-                            hipStream_t st) {
+                            hipStream_t st, int stride) {
     if (C <= 0) return;
-    hipLaunchKernelGGL(reduce_partials_kernel, dim3(C), dim3(1024), 0, st, partial, nblocks, sums);
+    if (stride < 0) stride = nblocks;
+    hipLaunchKernelGGL(reduce_partials_kernel, dim3(C), dim3(1024), 0, st, partial, stride,
+                       nblocks, sums);
     OF2D_HIP(hipGetLastError());
+}
+
+void PartialRuns::add(int t, int len, int nblocks) {
+    if (!runs.empty() && runs.back().t0 + runs.back().len == t && runs.back().nblocks == nblocks)
+        runs.back().len += len;
+    else
+        runs.push_back({t, len, nblocks});
+}
+void PartialRuns::reduce(const double *partial, int stride, double *sums, hipStream_t st) const {
+    for (const Run &r : runs)
+        launch_reduce_partials(partial + (size_t)r.t0 * stride * 2, r.nblocks, r.len,
+                               sums + 2 * (size_t)r.t0, st, stride);
 }
 
 }  // namespace of2d

@@ -10,6 +10,8 @@
 // float4 loads of an image row are 16-B aligned.
 #pragma once
 
+#include <vector>
+
 #include <hip/hip_runtime.h>
 
 #include <cstddef>
@@ -132,8 +134,20 @@ inline int hs_partial_blocks(int P, int dimx, int nrows) {
 }
 // Sum C iterations' per-block partials in a fixed order: sums[2t+{0,1}] =
 // {sum ||diff||, sum ||prev||} for t < C.
+// Row t of `partial` starts at t * stride * 2 doubles (stride = nblocks if < 0).
 void launch_reduce_partials(const double *partial, int nblocks, int C, double *sums,
-                            hipStream_t st);
+                            hipStream_t st, int stride = -1);
+// The launches of one chunk: runs of consecutive iterations whose kernels wrote
+// the same number of block partials, so that rows are reduced over exactly the
+// blocks that wrote them (no zero fill of the partial rows per chunk).
+struct PartialRuns {
+    struct Run {
+        int t0, len, nblocks;
+    };
+    std::vector<Run> runs;
+    void add(int t, int len, int nblocks);
+    void reduce(const double *partial, int stride, double *sums, hipStream_t st) const;
+};
 
 // ---------------------------------------------------------------- fields
 void launch_d2f(const double *in, int dimx, int dimy, float *out, int P, int row_offset,

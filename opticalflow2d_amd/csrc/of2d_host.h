@@ -151,8 +151,10 @@ class Registration {
                                        double *partial2, double *partial3)>;
 
    private:
+    // nblk[k]: block partials written by step (k = 0), step2 (1), step3 (2)
     int run_chunked(Level &L, int niter, int nb, const StepFn &step, int &final_buf,
-                    const StepFn2 &step2 = nullptr, const StepFn3 &step3 = nullptr);
+                    const StepFn2 &step2 = nullptr, const StepFn3 &step3 = nullptr,
+                    const int *nblk = nullptr);
     void ensure_device();
     void estimate_level(int s);
     int loop_hs(Level &L, int niter, float alpha, int &final_buf);
@@ -168,7 +170,7 @@ class Registration {
     std::vector<int> ldx_, ldy_;
     std::vector<Level> lv_;
     bool fixed_ = false;
-    int chunk_ = 32;
+    int chunk_ = 33;  // eleven fused triples per chunk
     int device_ = -1;
     bool ready_ = false;
     hipStream_t st_ = nullptr;

@@ -276,7 +276,7 @@ void Registration::estimate_level(int s) {
 // iteration t is replayed from it with single steps (iteration t reads
 // src_of(a, t) and writes dst_of(a, t)).
 int Registration::run_chunked(Level &L, int niter, int nb, const StepFn &step, int &final_buf,
-                              const StepFn2 &step2, const StepFn3 &step3) {
+                              const StepFn2 &step2, const StepFn3 &step3, const int *nblk) {
     const double npx = (double)L.dx * L.dy;
     last_err_.clear();
     if (fixed_ && d_all_.n < 2 * (size_t)niter) {
@@ -290,23 +290,25 @@ int Registration::run_chunked(Level &L, int niter, int nb, const StepFn &step, i
         const int C = std::min(chunk_, niter - k0);
         auto part = [&](int t) { return d_partial_ + (size_t)t * nb * 2; };
         int end = -1;  // pairs: the buffer holding the chunk's last iterate
+        PartialRuns runs;  // which kernel wrote how many block partials per row
         if (step2) {
             // fused launches (triples, then a pair / single tail) alternate
-            // between the two buffers other than a; kernels with fewer blocks
-            // than nb leave zeros in the rest of their partial rows
-            OF2D_HIP(hipMemsetAsync(part(0), 0, sizeof(double) * 2 * nb * C, st_));
+            // between the two buffers other than a
             auto other = [&](int b) { return b == (a + 1) % 3 ? (a + 2) % 3 : (a + 1) % 3; };
             int cur = a, t = 0;
             while (t < C) {
                 const int nxt = other(cur);
                 if (step3 && C - t >= 3) {
                     step3(L.est[cur].p, L.est[nxt].p, part(t), part(t + 1), part(t + 2));
+                    runs.add(t, 3, nblk ? nblk[2] : nb);
                     t += 3;
                 } else if (C - t >= 2) {
                     step2(L.est[cur].p, L.est[nxt].p, part(t), part(t + 1));
+                    runs.add(t, 2, nblk ? nblk[1] : nb);
                     t += 2;
                 } else {
                     step(L.est[cur].p, L.est[nxt].p, part(t));
+                    runs.add(t, 1, nblk ? nblk[0] : nb);
                     t += 1;
                 }
                 cur = nxt;
@@ -314,16 +316,17 @@ int Registration::run_chunked(Level &L, int niter, int nb, const StepFn &step, i
             end = cur;
         } else {
             for (int t = 0; t < C; t++) step(L.est[src_of(a, t)].p, L.est[dst_of(a, t)].p, part(t));
+            runs.add(0, C, nblk ? nblk[0] : nb);
         }
         if (fixed_) {
             // no break to decide: every chunk's sums stay on the device and are
             // read back once after the loop (no host round trip per chunk)
-            launch_reduce_partials(d_partial_, nb, C, d_all_.p + 2 * (size_t)k0, st_);
+            runs.reduce(d_partial_, nb, d_all_.p + 2 * (size_t)k0, st_);
             a = step2 ? end : dst_of(a, C - 1);
             k0 += C;
             continue;
         }
-        launch_reduce_partials(d_partial_, nb, C, d_sums_, st_);
+        runs.reduce(d_partial_, nb, d_sums_, st_);
         OF2D_HIP(hipMemcpyAsync(hs_.sums, d_sums_, sizeof(double) * 2 * C, hipMemcpyDeviceToHost,
                                 st_));
         check_status();  // synchronises the stream; throws the reference's runtime_error
@@ -362,8 +365,11 @@ int Registration::run_chunked(Level &L, int niter, int nb, const StepFn &step, i
 // HS iteration loop (ImageRegistrationOpticalFlow.cpp:117-135) with fused Logger
 int Registration::loop_hs(Level &L, int niter, float alpha, int &final_buf) {
     const float alphasq = alpha * alpha;  // OpticalFlowDiffusion.cpp:70
-    // partial rows long enough for every HS kernel (zero-padded per chunk)
+    // partial rows long enough for every HS kernel; each row is reduced over
+    // the blocks of the kernel that wrote it
     const int nb = hs_partial_blocks(L.P, L.dx, L.dy);
+    const int nblk[3] = {hs_nblocks(L.P, L.dy), hs2_nblocks(L.dx, L.dy),
+                         hs3_nblocks(L.dx, L.dy)};
     const bool pairs = L.dx >= 2;
     return run_chunked(
         L, niter, nb,
@@ -383,7 +389,8 @@ int Registration::loop_hs(Level &L, int niter, float alpha, int &final_buf) {
             launch_hs_jacobi3(src, dst, L.dI.p, L.It.p, L.P, L.dx, L.dy, 0, L.dy, alphasq, -1,
                               L.dy + 1, p1, p2, p3, d_status_, st_);
         })
-              : StepFn3());
+              : StepFn3(),
+        nblk);
 }
 
 // WrapperOpticalFlow2d.cpp:105-117 -> Motion::copy_motion_to_input

@@ -55,7 +55,7 @@ struct of2d_slab {
     size_t all_cap = 0;
     unsigned *d_status = nullptr;
     of2d::HostScratch hs;
-    int chunk = 32;
+    int chunk = 33;  // eleven fused triples per chunk
     int fin = 0;  // buffer holding the final motion
     double last_ms = 0.0;
     std::vector<float> errs;
@@ -212,8 +212,11 @@ int of2d_slab_run(of2d_slab *s, int niter, int fixed_iters, int *iters_done) {
     if (!s) return OF2D_ERR_INVALID_ARGUMENT;
     return sguard(s, [&] {
         const float alphasq = s->alpha * s->alpha;
-        // partial rows long enough for every kernel; zeroed per chunk
+        // partial rows long enough for every kernel; each row is reduced over
+        // the blocks of the kernel that wrote it
         const int nb = of2d::hs_partial_blocks(s->P, s->dimx, s->nrows);
+        const int n1 = of2d::hs_nblocks(s->P, s->nrows), n2 = of2d::hs2_nblocks(s->dimx, s->nrows),
+                  n3 = of2d::hs3_nblocks(s->dimx, s->nrows);
         const double npx = (double)s->dimx * s->dimy;
         auto src_of = [](int a, int t) { return t == 0 ? a : (t % 2 == 1 ? (a + 1) % 3 : (a + 2) % 3); };
         auto dst_of = [](int a, int t) { return t % 2 == 0 ? (a + 1) % 3 : (a + 2) % 3; };
@@ -257,7 +260,6 @@ int of2d_slab_run(of2d_slab *s, int niter, int fixed_iters, int *iters_done) {
         auto single = [&](int in, int out, double *partial) {
             float2 *uin = s->u[in].p;
             halo_exchange(s, uin, 1, s->st);
-            OF2D_HIP(hipMemsetAsync(partial, 0, sizeof(double) * 2 * nb, s->st));
             of2d::launch_hs_jacobi(uin, s->u[out].p, s->dI.p, s->It.p, s->P, s->dimx, s->nrows,
                                    s->rb, s->dimy, alphasq, partial, s->d_status, s->st);
         };
@@ -280,20 +282,23 @@ int of2d_slab_run(of2d_slab *s, int niter, int fixed_iters, int *iters_done) {
             auto part = [&](int t) { return s->d_partial + (size_t)t * nb * 2; };
             // triples (then a pair / single tail) alternate between the two
             // buffers other than the chunk's start buffer a, which stays intact
-            // for a replay; kernels with fewer blocks than nb leave zeros
-            OF2D_HIP(hipMemsetAsync(part(0), 0, sizeof(double) * 2 * nb * C, s->st));
+            // for a replay
+            of2d::PartialRuns runs;
             auto other = [&](int b) { return b == (a + 1) % 3 ? (a + 2) % 3 : (a + 1) % 3; };
             int cur = a, tp = 0;
             while (tp < C) {
                 const int nxt = other(cur);
                 if (C - tp >= 3) {
                     fused(3, cur, nxt, part(tp), part(tp + 1), part(tp + 2));
+                    runs.add(tp, 3, n3);
                     tp += 3;
                 } else if (C - tp == 2) {
                     fused(2, cur, nxt, part(tp), part(tp + 1), nullptr);
+                    runs.add(tp, 2, n2);
                     tp += 2;
                 } else {
                     single(cur, nxt, part(tp));
+                    runs.add(tp, 1, n1);
                     tp += 1;
                 }
                 cur = nxt;
@@ -302,7 +307,7 @@ int of2d_slab_run(of2d_slab *s, int niter, int fixed_iters, int *iters_done) {
                 // no break to decide: keep every chunk's sums on the device and
                 // read them back once after the run (no host sync per chunk)
                 double *sums = s->d_all + 2 * (size_t)k0;
-                of2d::launch_reduce_partials(s->d_partial, nb, C, sums, s->st);
+                runs.reduce(s->d_partial, nb, sums, s->st);
                 if (s->nranks > 1)
                     OF2D_NCCL(ncclAllReduce(sums, sums, 2 * (size_t)C, ncclDouble, ncclSum,
                                             s->comm, s->st));
@@ -310,7 +315,7 @@ int of2d_slab_run(of2d_slab *s, int niter, int fixed_iters, int *iters_done) {
                 k0 += C;
                 continue;
             }
-            of2d::launch_reduce_partials(s->d_partial, nb, C, s->d_sums, s->st);
+            runs.reduce(s->d_partial, nb, s->d_sums, s->st);
             if (s->nranks > 1)
                 OF2D_NCCL(ncclAllReduce(s->d_sums, s->d_sums, 2 * (size_t)C, ncclDouble, ncclSum,
                                         s->comm, s->st));

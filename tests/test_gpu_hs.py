@@ -94,6 +94,41 @@ def test_ragged_sizes(gpu, oracle, dims):
     assert np.array_equal(w, o["warped"])
 
 
+def _bits(a):
+    return np.asarray(a, dtype=np.float32).view(np.uint32)
+
+
+@pytest.mark.parametrize("case", ["blob", "tiny", "static"])
+def test_division_paths_bitwise(gpu, oracle, case):
+    """The triple Jacobi kernel divides without div_scale where that is exact
+    (hs_jacobi_impl.h div2_unscaled: gradients in 0 or [2^-30, 2^20), the
+    denominator in [2^-40, 2^40), sc in 0 or [2^-50, 2^30)) and takes the
+    compiler's IEEE sequence in every other wave-step.  Both give the oracle's
+    bits, signs of zero included.
+      blob   It = 0 outside a 20 x 20 blob: the motion at the diffusion front is
+             far below 2^-50 (scaled path there, fast path elsewhere);
+      tiny   intensities ~1e-12: gradients below 2^-30 (scaled path everywhere);
+      static mov == ref: It = 0 and the motion stays 0 (zero numerators)."""
+    n = 200
+    ref, mov = S.texture_pair(n, seed=3)
+    if case == "blob":
+        blob = mov.copy()
+        mov = ref.copy()
+        mov[90:110, 90:110] = blob[90:110, 90:110]
+    elif case == "tiny":
+        ref, mov = ref * 1e-12, mov * 1e-12
+    else:
+        mov = ref.copy()
+    with ImageRegistration((n, n), [61], 0, 0, [0.3], fixed_iters=1) as r:
+        r.register(ref, mov)
+        m = r.motion()
+    o = oracle_run(oracle, (n, n), [61], 0, 0, [0.3], 1, ref, mov, fixed=True)
+    assert np.array_equal(_bits(m), _bits(o["motion"]))
+    if case == "blob":  # the case does reach the scaled-division range
+        a = np.abs(m[m != 0])
+        assert a.min() < 2.0 ** -60
+
+
 def test_pyramid_and_refine_fixture(gpu):
     g = golden("oracle_paths.npz")
     for name, niter, nscales, params, nrefine in [("hs_square64", [60], 0, [0.1], 1),

@@ -162,11 +162,11 @@ int run2(const Bufs &b, int iters, const char *name, double bytes) {
 }
 
 // three iterations per launch: timed per ITERATION, checked against 6 single steps
-template <int ROWS, int WAVES, int MINB = 1>
+template <int ROWS, int WAVES, int MINB = 1, int UNR = 4, bool FD = true>
 int run3(const Bufs &b, int iters, const char *name, double bytes) {
     const dim3 g = hs::grid3_for<ROWS, WAVES>(b.dimx, b.dimy);
     const dim3 gl(8 * ((g.x * g.y + 7) / 8));
-    auto k = hs::jacobi3_kernel<ROWS, WAVES, true, MINB>;
+    auto k = hs::jacobi3_kernel<ROWS, WAVES, true, MINB, UNR, FD>;
     auto k1 = hs::jacobi_kernel<32, 2, 4, true, true, false>;
     const dim3 g1 = hs::grid_for<32, 2, 4>(b.P, b.dimy);
     double *p2 = b.partial + 2 * 16384, *p3 = b.partial + 4 * 16384;
@@ -295,15 +295,17 @@ int main(int argc, char **argv) {
     if (argc > 3 && strcmp(argv[3], "pair") == 0)  // the product pair kernel (PMC runs)
         return run2<32, 4, 2, true>(b, iters, "two-step 32r 4w xcd (product)", bytes);
     if (argc > 3 && strcmp(argv[3], "triple") == 0)  // the product triple kernel (PMC runs)
-        return run3<36, 4>(b, iters, "three-step 36r 4w xcd (product at 4096^2)", bytes);
+        return run3<36, 4, 4, 4, true>(b, iters, "three-step 36r 4w xcd (product at 4096^2)", bytes);
     if (argc > 3 && strcmp(argv[3], "two") == 0) {
         int b2 = 0;
         V3(32, 2, 4, true, true, false);
         b2 |= run2<32, 4>(b, iters, "two-step 32r 4w", bytes);
-        b2 |= run3<36, 4>(b, iters, "three-step 36r 4w xcd", bytes);
-        b2 |= run3<36, 4, 5>(b, iters, "three-step 36r 4w xcd 5blk", bytes);
-        b2 |= run3<29, 4, 5>(b, iters, "three-step 29r 4w xcd 5blk", bytes);
-        b2 |= run3<29, 4>(b, iters, "three-step 29r 4w xcd", bytes);
+        b2 |= run3<36, 4, 1, 4, false>(b, iters, "three-step 36r 4w unr4", bytes);
+        b2 |= run3<36, 4, 1, 4, true>(b, iters, "three-step 36r 4w unr4 fd", bytes);
+        b2 |= run3<36, 4, 4, 4, true>(b, iters, "three-step 36r 4w unr4 fd minb4", bytes);
+        b2 |= run3<36, 4, 4, 2, true>(b, iters, "three-step 36r 4w unr2 fd minb4", bytes);
+        b2 |= run3<36, 4, 3, 4, true>(b, iters, "three-step 36r 4w unr4 fd minb3", bytes);
+        b2 |= run3<36, 4, 1, 4, false>(b, iters, "three-step 36r 4w unr4 (again)", bytes);
         b2 |= run2<32, 4, 2, true>(b, iters, "two-step 32r 4w xcd", bytes);
         b2 |= run2<32, 2, 2, true>(b, iters, "two-step 32r 2w xcd", bytes);
         b2 |= run2<16, 4, 2, true>(b, iters, "two-step 16r 4w xcd", bytes);
