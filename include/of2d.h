@@ -138,6 +138,19 @@ int of2d_slab_time_kernel(of2d_slab *s, int nlaunch, double *avg_us);
 int of2d_slab_last_run_ms(const of2d_slab *s, double *ms);
 int of2d_slab_destroy(of2d_slab *s);
 const char *of2d_slab_last_error(const of2d_slab *s);
+/* In-process slab group: the nranks slabs of one grid in ONE process, driven by
+ * one host thread per rank, exchanging the same halo lines and Logger sums by
+ * device copies (ordered with HIP events, the threads meeting at a barrier per
+ * exchange) instead of RCCL.  Same slab code and launches as the RCCL path; it
+ * lets the decomposition run on a single GPU, where RCCL refuses two ranks on
+ * one device (tests/test_gpu_slab_local.py).  nranks <= 16.  Create the group,
+ * then one slab per rank with of2d_slab_create_local; call of2d_slab_run on all
+ * ranks concurrently; destroy the slabs before the group. */
+typedef struct of2d_slab_group of2d_slab_group;
+int of2d_slab_group_create(of2d_slab_group **out, int nranks);
+int of2d_slab_group_destroy(of2d_slab_group *g);
+int of2d_slab_create_local(of2d_slab **out, int dimx, int dimy, float alpha, int rank,
+                           int nranks, int device, of2d_slab_group *g);
 
 /* ---- library info ---- */
 const char *of2d_version(void);

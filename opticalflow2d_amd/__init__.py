@@ -8,8 +8,8 @@ loop runs in hand-written gfx950 HIP kernels (``opticalflow2d_amd/csrc``).
 from ._lib import Of2dError, InvalidArgument, build, lib
 from .registration import (ImageRegistration, MotionAccumulation, OpticalFlow2d,
                            Regularisation, Verbose, set_print_sink)
-from .slab import SlabSolver, slab_bounds
+from .slab import SlabGroup, SlabSolver, slab_bounds
 
 __all__ = ["OpticalFlow2d", "ImageRegistration", "Regularisation", "Verbose",
-           "MotionAccumulation", "set_print_sink", "SlabSolver", "slab_bounds", "Of2dError",
+           "MotionAccumulation", "set_print_sink", "SlabSolver", "SlabGroup", "slab_bounds", "Of2dError",
            "InvalidArgument", "build", "lib"]

@@ -60,6 +60,10 @@ SIGNATURES = {
     "of2d_slab_last_run_ms": (C.c_int, [C.c_void_p, C.POINTER(C.c_double)]),
     "of2d_slab_destroy": (C.c_int, [C.c_void_p]),
     "of2d_slab_last_error": (C.c_char_p, [C.c_void_p]),
+    "of2d_slab_group_create": (C.c_int, [C.POINTER(C.c_void_p), C.c_int]),
+    "of2d_slab_group_destroy": (C.c_int, [C.c_void_p]),
+    "of2d_slab_create_local": (C.c_int, [C.POINTER(C.c_void_p), C.c_int, C.c_int, C.c_float,
+                                         C.c_int, C.c_int, C.c_int, C.c_void_p]),
     "of2d_version": (C.c_char_p, []),
     "of2d_device_count": (C.c_int, [C.POINTER(C.c_int)]),
 }

@@ -131,6 +131,29 @@ void launch_reduce_partials(const double *partial, int nblocks, int C, double *s
     OF2D_HIP(hipGetLastError());
 }
 
+namespace {
+struct RankPtrs {
+    const double *p[kMaxLocalRanks];
+};
+}  // namespace
+__global__ void sum_ranks_kernel(RankPtrs src, int n, long count, double *__restrict__ out) {
+    const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= count) return;
+    double a = src.p[0][i];
+    for (int r = 1; r < n; r++) a += src.p[r][i];
+    out[i] = a;
+}
+void launch_sum_ranks(const double *const *src, int n, size_t count, double *out,
+                      hipStream_t st) {
+    if (n < 1 || n > kMaxLocalRanks) throw std::invalid_argument("launch_sum_ranks: n");
+    if (count == 0) return;
+    RankPtrs p{};
+    for (int r = 0; r < n; r++) p.p[r] = src[r];
+    hipLaunchKernelGGL(sum_ranks_kernel, dim3((unsigned)((count + 255) / 256)), dim3(256), 0, st,
+                       p, n, (long)count, out);
+    OF2D_HIP(hipGetLastError());
+}
+
 void PartialRuns::add(int t, int len, int nblocks) {
     if (!runs.empty() && runs.back().t0 + runs.back().len == t && runs.back().nblocks == nblocks)
         runs.back().len += len;

@@ -134,6 +134,10 @@ inline int hs_partial_blocks(int P, int dimx, int nrows) {
 }
 // Sum C iterations' per-block partials in a fixed order: sums[2t+{0,1}] =
 // {sum ||diff||, sum ||prev||} for t < C.
+// out[i] = sum over r < n of src[r][i], added in rank order (the in-process
+// slab group's all-reduce, slab.cpp); n <= kMaxLocalRanks
+constexpr int kMaxLocalRanks = 16;
+void launch_sum_ranks(const double *const *src, int n, size_t count, double *out, hipStream_t st);
 // Row t of `partial` starts at t * stride * 2 doubles (stride = nblocks if < 0).
 void launch_reduce_partials(const double *partial, int nblocks, int C, double *sums,
                             hipStream_t st, int stride = -1);

@@ -26,8 +26,12 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <chrono>
+#include <condition_variable>
 #include <cstring>
+#include <mutex>
 #include <string>
+#include <vector>
 
 #include "../../include/of2d.h"
 #include "of2d_host.h"
@@ -47,6 +51,9 @@ struct of2d_slab {
     hipStream_t comm_st = nullptr;  // the halo exchange, overlapped with interior bands
     hipEvent_t ev_src = nullptr, ev_halo = nullptr;
     ncclComm_t comm = nullptr;
+    of2d_slab_group *grp = nullptr;  // in-process transport instead of RCCL
+    hipEvent_t ev_ready = nullptr, ev_done = nullptr;  // its exchange handshakes
+    double *d_red = nullptr;  // its all-reduce result staging
     of2d::Field<float2> u[3];
     of2d::Field<float2> dI;
     of2d::Field<float> It, Iref, Imov;
@@ -61,6 +68,33 @@ struct of2d_slab {
     std::vector<float> errs;
     std::string err;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
+};
+
+// The ranks of one grid inside ONE process, one host thread per rank: halos
+// and the Logger all-reduce move by device copies ordered with events, and the
+// host threads meet at a barrier per exchange.  Same slab code, same launches,
+// same halo lines as the RCCL path; it exists so that the decomposition can run
+// on a single GPU, where RCCL refuses two ranks on one device.
+struct of2d_slab_group {
+    int n = 0;
+    std::mutex m;
+    std::condition_variable cv;
+    int arrived = 0;
+    long gen = 0;
+    std::vector<of2d_slab *> slabs;
+    std::vector<const void *> ptr;  // per rank: the buffer published for this exchange
+    void barrier() {
+        std::unique_lock<std::mutex> lk(m);
+        const long my = gen;
+        if (++arrived == n) {
+            arrived = 0;
+            gen++;
+            cv.notify_all();
+            return;
+        }
+        if (!cv.wait_for(lk, std::chrono::seconds(60), [&] { return gen != my; }))
+            throw std::runtime_error("slab group: a rank did not reach the exchange");
+    }
 };
 
 namespace {
@@ -84,12 +118,46 @@ int sguard(of2d_slab *s, F &&f) {
     }
 }
 
+// in-process transport: every rank publishes `u` once its boundary lines are
+// final (ev_ready), pulls its neighbours' lines into its own ghost lines, and
+// does not run ahead until the neighbours have pulled from it (ev_done)
+void local_exchange(of2d_slab *s, float2 *u, int lines, size_t cnt, hipStream_t st) {
+    of2d_slab_group *g = s->grp;
+    const long P = s->P;
+    const size_t bytes = cnt * sizeof(float);
+    OF2D_HIP(hipEventRecord(s->ev_ready, st));
+    g->ptr[s->rank] = u;
+    g->barrier();
+    for (int r = 0; r < s->nranks; r++)
+        if (!g->slabs[r]) throw std::invalid_argument("slab group: not every rank was created");
+    if (s->rank > 0) {
+        const of2d_slab *up = g->slabs[s->rank - 1];
+        const float2 *src = static_cast<const float2 *>(g->ptr[s->rank - 1]);
+        OF2D_HIP(hipStreamWaitEvent(st, up->ev_ready, 0));
+        OF2D_HIP(hipMemcpyAsync(u - lines * P, src + (long)(up->nrows - lines) * P, bytes,
+                                hipMemcpyDeviceToDevice, st));
+    }
+    if (s->rank < s->nranks - 1) {
+        const of2d_slab *dn = g->slabs[s->rank + 1];
+        const float2 *src = static_cast<const float2 *>(g->ptr[s->rank + 1]);
+        OF2D_HIP(hipStreamWaitEvent(st, dn->ev_ready, 0));
+        OF2D_HIP(hipMemcpyAsync(u + (long)s->nrows * P, src, bytes, hipMemcpyDeviceToDevice,
+                                st));
+    }
+    OF2D_HIP(hipEventRecord(s->ev_done, st));
+    g->barrier();
+    if (s->rank > 0) OF2D_HIP(hipStreamWaitEvent(st, g->slabs[s->rank - 1]->ev_done, 0));
+    if (s->rank < s->nranks - 1)
+        OF2D_HIP(hipStreamWaitEvent(st, g->slabs[s->rank + 1]->ev_done, 0));
+}
+
 // `lines` (1..3) boundary j-lines to each neighbour, on stream `st`
 void halo_exchange(of2d_slab *s, float2 *u, int lines, hipStream_t st) {
     if (s->nranks == 1) return;
     const long P = s->P;
     // lines are contiguous at pitch P: 2 floats per px, the padding travels too
     const size_t cnt = 2 * ((size_t)(lines - 1) * P + (size_t)s->dimx);
+    if (s->grp) return local_exchange(s, u, lines, cnt, st);
     OF2D_NCCL(ncclGroupStart());
     if (s->rank > 0) {
         OF2D_NCCL(ncclSend(u, cnt, ncclFloat, s->rank - 1, s->comm, st));
@@ -101,6 +169,32 @@ void halo_exchange(of2d_slab *s, float2 *u, int lines, hipStream_t st) {
         OF2D_NCCL(ncclRecv(u + (long)s->nrows * P, cnt, ncclFloat, s->rank + 1, s->comm, st));
     }
     OF2D_NCCL(ncclGroupEnd());
+}
+
+// sum of `count` doubles over the ranks, in place, on stream `st`
+void allreduce_sums(of2d_slab *s, double *buf, size_t count, hipStream_t st) {
+    if (s->nranks == 1) return;
+    if (!s->grp) {
+        OF2D_NCCL(ncclAllReduce(buf, buf, count, ncclDouble, ncclSum, s->comm, st));
+        return;
+    }
+    // in-process: every rank adds all ranks' buffers in rank order into its
+    // own staging, then copies it back once every rank has read every buffer
+    of2d_slab_group *g = s->grp;
+    OF2D_HIP(hipEventRecord(s->ev_ready, st));
+    g->ptr[s->rank] = buf;
+    g->barrier();
+    std::vector<const double *> src(s->nranks);
+    for (int r = 0; r < s->nranks; r++) {
+        if (r != s->rank) OF2D_HIP(hipStreamWaitEvent(st, g->slabs[r]->ev_ready, 0));
+        src[r] = static_cast<const double *>(g->ptr[r]);
+    }
+    of2d::launch_sum_ranks(src.data(), s->nranks, count, s->d_red, st);
+    OF2D_HIP(hipEventRecord(s->ev_done, st));
+    g->barrier();
+    for (int r = 0; r < s->nranks; r++)
+        if (r != s->rank) OF2D_HIP(hipStreamWaitEvent(st, g->slabs[r]->ev_done, 0));
+    OF2D_HIP(hipMemcpyAsync(buf, s->d_red, count * sizeof(double), hipMemcpyDeviceToDevice, st));
 }
 }  // namespace
 
@@ -125,8 +219,8 @@ int of2d_rccl_get_unique_id(void *out, int len) {
     return OF2D_OK;
 }
 
-int of2d_slab_create(of2d_slab **out, int dimx, int dimy, float alpha, int rank, int nranks,
-                     int device, const void *uid, int id_len) {
+static int slab_create(of2d_slab **out, int dimx, int dimy, float alpha, int rank, int nranks,
+                       int device, const void *uid, int id_len, of2d_slab_group *grp) {
     if (!out) return OF2D_ERR_INVALID_ARGUMENT;
     *out = nullptr;
     auto *s = new of2d_slab();
@@ -163,7 +257,16 @@ int of2d_slab_create(of2d_slab **out, int dimx, int dimy, float alpha, int rank,
         OF2D_HIP(hipDeviceSynchronize());  // null-stream memset vs the non-blocking stream
         OF2D_HIP(hipMalloc(&s->d_stage, sizeof(double) * 2 * (size_t)dimx * (s->nrows + 6)));
         s->hs.ensure(s->chunk);
-        if (nranks > 1) {
+        if (grp) {
+            if (grp->n != nranks) throw std::invalid_argument("slab: group size != nranks");
+            OF2D_HIP(hipEventCreateWithFlags(&s->ev_ready, hipEventDisableTiming));
+            OF2D_HIP(hipEventCreateWithFlags(&s->ev_done, hipEventDisableTiming));
+            OF2D_HIP(hipMalloc(&s->d_red, sizeof(double) * 2 * (size_t)s->chunk));
+            std::lock_guard<std::mutex> lk(grp->m);
+            if (grp->slabs[rank]) throw std::invalid_argument("slab: rank already in the group");
+            grp->slabs[rank] = s;
+            s->grp = grp;
+        } else if (nranks > 1) {
             if (!uid || id_len < (int)sizeof(ncclUniqueId))
                 throw std::invalid_argument("slab: RCCL unique id required for nranks > 1");
             ncclUniqueId id;
@@ -178,6 +281,35 @@ int of2d_slab_create(of2d_slab **out, int dimx, int dimy, float alpha, int rank,
     }
     *out = s;
     return OF2D_OK;
+}
+
+int of2d_slab_create(of2d_slab **out, int dimx, int dimy, float alpha, int rank, int nranks,
+                     int device, const void *uid, int id_len) {
+    return slab_create(out, dimx, dimy, alpha, rank, nranks, device, uid, id_len, nullptr);
+}
+
+int of2d_slab_group_create(of2d_slab_group **out, int nranks) {
+    if (!out || nranks < 1 || nranks > of2d::kMaxLocalRanks) return OF2D_ERR_INVALID_ARGUMENT;
+    auto *g = new of2d_slab_group();
+    g->n = nranks;
+    g->slabs.assign(nranks, nullptr);
+    g->ptr.assign(nranks, nullptr);
+    *out = g;
+    return OF2D_OK;
+}
+
+int of2d_slab_group_destroy(of2d_slab_group *g) {
+    if (!g) return OF2D_ERR_INVALID_ARGUMENT;
+    for (of2d_slab *s : g->slabs)
+        if (s) return OF2D_ERR_STATE;  // destroy the slabs first
+    delete g;
+    return OF2D_OK;
+}
+
+int of2d_slab_create_local(of2d_slab **out, int dimx, int dimy, float alpha, int rank,
+                           int nranks, int device, of2d_slab_group *g) {
+    if (!g) return OF2D_ERR_INVALID_ARGUMENT;
+    return slab_create(out, dimx, dimy, alpha, rank, nranks, device, nullptr, 0, g);
 }
 
 int of2d_slab_set_images(of2d_slab *s, const double *Iref_rows, const double *Imov_rows) {
@@ -308,17 +440,13 @@ int of2d_slab_run(of2d_slab *s, int niter, int fixed_iters, int *iters_done) {
                 // read them back once after the run (no host sync per chunk)
                 double *sums = s->d_all + 2 * (size_t)k0;
                 runs.reduce(s->d_partial, nb, sums, s->st);
-                if (s->nranks > 1)
-                    OF2D_NCCL(ncclAllReduce(sums, sums, 2 * (size_t)C, ncclDouble, ncclSum,
-                                            s->comm, s->st));
+                allreduce_sums(s, sums, 2 * (size_t)C, s->st);
                 a = cur;
                 k0 += C;
                 continue;
             }
             runs.reduce(s->d_partial, nb, s->d_sums, s->st);
-            if (s->nranks > 1)
-                OF2D_NCCL(ncclAllReduce(s->d_sums, s->d_sums, 2 * (size_t)C, ncclDouble, ncclSum,
-                                        s->comm, s->st));
+            allreduce_sums(s, s->d_sums, 2 * (size_t)C, s->st);
             OF2D_HIP(hipMemcpyAsync(s->hs.sums, s->d_sums, sizeof(double) * 2 * C,
                                     hipMemcpyDeviceToHost, s->st));
             OF2D_HIP(hipMemcpyAsync(s->hs.status, s->d_status, sizeof(unsigned),
@@ -420,6 +548,13 @@ int of2d_slab_destroy(of2d_slab *s) {
     if (s->st) (void)hipStreamSynchronize(s->st);
     if (s->comm_st) (void)hipStreamSynchronize(s->comm_st);
     if (s->comm) ncclCommDestroy(s->comm);
+    if (s->grp) {
+        std::lock_guard<std::mutex> lk(s->grp->m);
+        s->grp->slabs[s->rank] = nullptr;
+    }
+    if (s->ev_ready) (void)hipEventDestroy(s->ev_ready);
+    if (s->ev_done) (void)hipEventDestroy(s->ev_done);
+    if (s->d_red) (void)hipFree(s->d_red);
     if (s->d_partial) (void)hipFree(s->d_partial);
     if (s->d_sums) (void)hipFree(s->d_sums);
     if (s->d_all) (void)hipFree(s->d_all);

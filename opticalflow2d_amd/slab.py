@@ -42,23 +42,54 @@ def rccl_unique_id() -> bytes:
     return bytes(buf)
 
 
+class SlabGroup:
+    """The ranks of one grid inside one process (``of2d_slab_group``): slabs
+    created with ``group=`` exchange halos and Logger sums by device copies
+    instead of RCCL; drive each rank's ``run`` from its own thread.  Used to run
+    the decomposition on a single GPU (RCCL refuses two ranks on one device)."""
+
+    def __init__(self, nranks: int):
+        h = C.c_void_p()
+        check(_lib.lib().of2d_slab_group_create(C.byref(h), int(nranks)),
+              "slab group: nranks out of range")
+        self.nranks = int(nranks)
+        self._h = h
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            check(_lib.lib().of2d_slab_group_destroy(self._h),
+                  "slab group: destroy its slabs first")
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 class SlabSolver:
     """One rank's slab of a global HS registration (zero initial motion, one
     level, one refine — see opticalflow2d_amd/csrc/slab.cpp)."""
 
     def __init__(self, dimx: int, dimy: int, alpha: float, rank: int = 0, nranks: int = 1,
-                 device: int = 0, unique_id: Optional[bytes] = None):
+                 device: int = 0, unique_id: Optional[bytes] = None,
+                 group: Optional[SlabGroup] = None):
         L = _lib.lib()
         self.dimx, self.dimy, self.rank, self.nranks = int(dimx), int(dimy), rank, nranks
         self.row_begin, self.row_end = slab_bounds(dimy, rank, nranks)
         h = C.c_void_p()
-        uid = None
-        n = 0
-        if unique_id is not None:
-            uid = C.create_string_buffer(unique_id, len(unique_id))
-            n = len(unique_id)
-        st = L.of2d_slab_create(C.byref(h), self.dimx, self.dimy, float(alpha), rank, nranks,
-                                device, uid, n)
+        if group is not None:
+            st = L.of2d_slab_create_local(C.byref(h), self.dimx, self.dimy, float(alpha), rank,
+                                          nranks, device, group._h)
+        else:
+            uid = None
+            n = 0
+            if unique_id is not None:
+                uid = C.create_string_buffer(unique_id, len(unique_id))
+                n = len(unique_id)
+            st = L.of2d_slab_create(C.byref(h), self.dimx, self.dimy, float(alpha), rank,
+                                    nranks, device, uid, n)
         check(st, L.of2d_slab_last_error(None).decode())
         self._h = h
 
