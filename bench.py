@@ -8,9 +8,10 @@ One step = one Horn-Schunck iteration of the reference loop
 the Logger norms over the whole grid, the per-chunk norm reduction /
 convergence read-back, and — for N > 1 — the RCCL halo exchange.  Iterations
 run in threes fused into one pass over HBM (hs::jacobi3_kernel: 28 B/px per
-launch, three iterations per launch, bit-identical to three single steps; a
-pair kernel fills a chunk's tail), with a three-j-line halo exchange per
-launch overlapped with the interior bands.  Early exit is disabled
+launch, three iterations per launch, bit-identical to three single steps;
+chunks of 33 iterations are eleven launches, and a single step or a pair fills
+the run's tail), with a three-j-line halo exchange per launch overlapped with
+the interior bands.  Early exit is disabled
 (fixed_iters) so that exactly K iterations run.
 
 Workload: N = 1 is BASELINE config 2 (Horn-Schunck 4096^2 fp32).  For N > 1

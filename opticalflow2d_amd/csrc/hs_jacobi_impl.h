@@ -124,6 +124,33 @@ __device__ __forceinline__ bool exp_in(float v) {
     return (unsigned)(__builtin_amdgcn_frexp_expf(v) - LO) <= (unsigned)(HI - LO);
 }
 
+// What the unscaled division needs from the gradients, checked once per field
+// instead of per row step: every gradient the Jacobi kernels can read (the whole
+// allocation, ghost j-lines and padding included) in 0 or [2^-30, 2^20) and its
+// denominator (alpha^2 + gx^2) + gy^2 in [2^-40, 2^40), else range_flag |= 1.
+// Also the reference's divide-by-zero test (coord2d.h:95-100) on the image
+// pixels, the only pixels whose division the reference performs: status |=
+// kStatusDivZero if a denominator is 0 — dI is fixed for the whole loop, so
+// this is the test every iteration would repeat.
+template <int = 0>
+__global__ void hs_precheck_kernel(const float2 *__restrict__ base, long count, int P, int ghost,
+                                   int dimx, int dimy, float alphasq,
+                                   unsigned *__restrict__ range_flag,
+                                   unsigned *__restrict__ status) {
+    bool bad = false, zero = false;
+    for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < count;
+         i += (long)gridDim.x * blockDim.x) {
+        const float2 g = base[i];
+        const float den = (alphasq + g.x * g.x) + g.y * g.y;
+        bad |= !(exp_in<-29, 20>(g.x) && exp_in<-29, 20>(g.y) && exp_in<-39, 40>(den));
+        const long row = i / P - ghost;
+        const int col = (int)(i % P);
+        zero |= den == 0.0f && row >= 0 && row < dimy && col < dimx;
+    }
+    if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(range_flag, 1u);
+    if (__any(zero) && (threadIdx.x & 63) == 0) atomicOr(status, kStatusDivZero);
+}
+
 // u rows as PXL float2 per lane
 template <int PXL>
 struct Row {
@@ -475,7 +502,7 @@ __global__ __launch_bounds__(64 * WAVES, MINB) void jacobi3_kernel(
     const float *__restrict__ It, int P, int dimx, int nrows, int row0, int dimy, float alphasq,
     int glo, int ghi, double *__restrict__ partial, double *__restrict__ partial2,
     double *__restrict__ partial3, unsigned *__restrict__ status, int band0, int gx, int gy,
-    int rows = ROWS) {
+    int rows = ROWS, const unsigned *__restrict__ range_flag = nullptr) {
     int bx = (int)blockIdx.x, by = (int)blockIdx.y;
     if constexpr (XCD) {
         if (!xcd_block(gx, gy, bx, by)) return;
@@ -500,23 +527,19 @@ __global__ __launch_bounds__(64 * WAVES, MINB) void jacobi3_kernel(
     struct G {
         Row<2> g;
         float t[2], den[2], rcp[2];
-        bool ok;  // FD: gradients in 0 or [2^-30, 2^20), den in [2^-40, 2^40)
     };
+    // FD: the gradient field is in the unscaled-division range (hs_precheck_kernel)
+    const bool grange = FD && range_flag && *range_flag == 0;
     auto ldg = [&](int j) {
         G r;
         r.g = load_row<2, false>(dI + (long)cl(j) * P, xl);
         const float2 tt = *reinterpret_cast<const float2 *>(It + (long)cl(j) * P + xl);
         r.t[0] = tt.x;
         r.t[1] = tt.y;
-        r.ok = true;
 #pragma unroll
         for (int k = 0; k < 2; k++) {
             r.den[k] = (alphasq + r.g.v[k].x * r.g.v[k].x) + r.g.v[k].y * r.g.v[k].y;
-            if constexpr (FD) {
-                r.rcp[k] = recip_refined(r.den[k]);
-                r.ok = r.ok && exp_in<-29, 20>(r.g.v[k].x) && exp_in<-29, 20>(r.g.v[k].y) &&
-                       exp_in<-39, 40>(r.den[k]);
-            }
+            if constexpr (FD) r.rcp[k] = recip_refined(r.den[k]);
         }
         return r;
     };
@@ -540,13 +563,14 @@ __global__ __launch_bounds__(64 * WAVES, MINB) void jacobi3_kernel(
             const int xi = x + k;
             q[k] = zero_if(yb || xi == 0 || xi == dimx - 1, q[k]);
             sc[k] = (g.t[k] + q[k].x * g.g.v[k].x) + q[k].y * g.g.v[k].y;
-            b |= (g.den[k] == 0.0f) ? 1u : 0u;
+            // FD: the zero test is hs_precheck_kernel's, once per field
+            if constexpr (!FD) b |= (g.den[k] == 0.0f) ? 1u : 0u;
         }
         Row<2> o;
         // sc in 0 or [2^-50, 2^30) puts the numerators gx*sc, gy*sc in the
         // range where the unscaled division is exact (div2_unscaled)
-        if (FD && __builtin_amdgcn_ballot_w64(!(g.ok && exp_in<-49, 30>(sc[0]) &&
-                                                exp_in<-49, 30>(sc[1]))) == 0) {
+        if (FD && grange &&
+            __builtin_amdgcn_ballot_w64(((int)exp_in<-49, 30>(sc[0]) & (int)exp_in<-49, 30>(sc[1])) == 0) == 0) {
 #pragma unroll
             for (int k = 0; k < 2; k++) {
                 const float gx = g.g.v[k].x, gy = g.g.v[k].y;

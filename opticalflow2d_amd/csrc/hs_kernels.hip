@@ -17,6 +17,8 @@
 // strip's two edge lanes load one extra float2 each.  fp32 arithmetic in the
 // reference's order, compiled with -ffp-contract=off (no FMA contraction) and
 // IEEE division, so every pixel is bit-identical to the reference.
+#include <algorithm>
+
 #include "hs_jacobi_impl.h"
 
 namespace of2d {
@@ -61,9 +63,11 @@ static const auto kHsJacobi3 = &hs::jacobi3_kernel<0, kHs3Waves, true, 4, 4, tru
 void launch_hs_jacobi3(const float2 *u_old, float2 *u_new, const float2 *dI, const float *It,
                        int P, int dimx, int nrows, int row0, int dimy, float alphasq, int glo,
                        int ghi, double *partial, double *partial2, double *partial3,
-                       unsigned *status, hipStream_t st, int band_lo, int band_hi) {
+                       unsigned *status, const unsigned *range_flag, hipStream_t st,
+                       int band_lo, int band_hi) {
     if (P % kHsStrip != 0 || nrows <= 0 || dimx > P || dimx < 2 || glo > -1 || ghi < nrows + 1)
         throw std::invalid_argument("launch_hs_jacobi3: bad geometry");
+    if (!range_flag) throw std::invalid_argument("launch_hs_jacobi3: no range flag");
     const int nb = hs3_nbands(dimx, nrows);
     if (band_lo < 0) band_lo = 0;
     if (band_hi < 0) band_hi = nb;
@@ -74,7 +78,17 @@ void launch_hs_jacobi3(const float2 *u_old, float2 *u_new, const float2 *dI, con
     const dim3 gl(8 * ((g.x * g.y + 7) / 8));
     hipLaunchKernelGGL(kHsJacobi3, gl, dim3(64 * kHs3Waves), 0, st, u_old, u_new, dI, It, P,
                        dimx, nrows, row0, dimy, alphasq, glo, ghi, partial, partial2, partial3,
-                       status, band_lo, (int)g.x, (int)g.y, hs3_rows(dimx, nrows));
+                       status, band_lo, (int)g.x, (int)g.y, hs3_rows(dimx, nrows), range_flag);
+    OF2D_HIP(hipGetLastError());
+}
+
+void launch_hs_precheck(const float2 *base, size_t count, int P, int ghost, int dimx, int dimy,
+                        float alphasq, unsigned *range_flag, unsigned *status, hipStream_t st) {
+    OF2D_HIP(hipMemsetAsync(range_flag, 0, sizeof(unsigned), st));
+    const long n = (long)count;
+    const unsigned blocks = (unsigned)std::min<long>(2048, (n + 255) / 256);
+    hipLaunchKernelGGL(hs::hs_precheck_kernel<>, dim3(blocks > 0 ? blocks : 1), dim3(256), 0, st,
+                       base, n, P, ghost, dimx, dimy, alphasq, range_flag, status);
     OF2D_HIP(hipGetLastError());
 }
 

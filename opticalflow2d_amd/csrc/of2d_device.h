@@ -122,10 +122,21 @@ inline int hs3_nblocks(int dimx, int nrows) {
     dim3 g = hs3_grid(dimx, nrows);
     return int(g.x * g.y);
 }
+// range_flag: the word launch_hs_precheck wrote for this dI (required: the
+// kernel leaves the divide-by-zero test to it)
 void launch_hs_jacobi3(const float2 *u_old, float2 *u_new, const float2 *dI, const float *It,
                        int P, int dimx, int nrows, int row0, int dimy, float alphasq, int glo,
                        int ghi, double *partial, double *partial2, double *partial3,
-                       unsigned *status, hipStream_t st, int band_lo = -1, int band_hi = -1);
+                       unsigned *status, const unsigned *range_flag, hipStream_t st,
+                       int band_lo = -1, int band_hi = -1);
+// Once per gradient field, before the triple kernel runs on it
+// (hs_jacobi_impl.h hs_precheck_kernel): zeroes *range_flag, then sets it if
+// any gradient / denominator of the allocation [base, base + count) lies
+// outside the unscaled-division range, and ORs kStatusDivZero into *status if
+// an image pixel's denominator is 0.  ghost: j-lines before row 0 in base.
+void launch_hs_precheck(const float2 *base, size_t count, int P, int ghost, int dimx, int dimy,
+                        float alphasq, unsigned *range_flag, unsigned *status, hipStream_t st);
+constexpr int kRangeFlagWord = 32;  // word of the 64-word status buffers holding range_flag
 // partial-row length that fits every HS kernel (single, pair, triple)
 inline int hs_partial_blocks(int P, int dimx, int nrows) {
     int nb = hs_nblocks(P, nrows);

@@ -371,6 +371,10 @@ int Registration::loop_hs(Level &L, int niter, float alpha, int &final_buf) {
     const int nblk[3] = {hs_nblocks(L.P, L.dy), hs2_nblocks(L.dx, L.dy),
                          hs3_nblocks(L.dx, L.dy)};
     const bool pairs = L.dx >= 2;
+    unsigned *range_flag = d_status_ + kRangeFlagWord;
+    if (pairs)
+        launch_hs_precheck(L.dI.base, L.dI.count, L.P, 1, L.dx, L.dy, alphasq, range_flag,
+                           d_status_, st_);
     return run_chunked(
         L, niter, nb,
         [&](const float2 *src, float2 *dst, double *partial) {
@@ -387,7 +391,7 @@ int Registration::loop_hs(Level &L, int niter, float alpha, int &final_buf) {
               : StepFn2(),
         pairs ? StepFn3([&](const float2 *src, float2 *dst, double *p1, double *p2, double *p3) {
             launch_hs_jacobi3(src, dst, L.dI.p, L.It.p, L.P, L.dx, L.dy, 0, L.dy, alphasq, -1,
-                              L.dy + 1, p1, p2, p3, d_status_, st_);
+                              L.dy + 1, p1, p2, p3, d_status_, range_flag, st_);
         })
               : StepFn3(),
         nblk);

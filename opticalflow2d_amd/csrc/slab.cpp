@@ -83,6 +83,7 @@ struct of2d_slab_group {
     long gen = 0;
     std::vector<of2d_slab *> slabs;
     std::vector<const void *> ptr;  // per rank: the buffer published for this exchange
+    std::vector<char> flag;          // per rank: any_rank's vote
     void barrier() {
         std::unique_lock<std::mutex> lk(m);
         const long my = gen;
@@ -169,6 +170,27 @@ void halo_exchange(of2d_slab *s, float2 *u, int lines, hipStream_t st) {
         OF2D_NCCL(ncclRecv(u + (long)s->nrows * P, cnt, ncclFloat, s->rank + 1, s->comm, st));
     }
     OF2D_NCCL(ncclGroupEnd());
+}
+
+// true on every rank if `mine` is true on any rank (host-side; synchronises)
+bool any_rank(of2d_slab *s, bool mine) {
+    if (s->nranks == 1) return mine;
+    if (s->grp) {
+        of2d_slab_group *g = s->grp;
+        g->flag[s->rank] = mine;
+        g->barrier();
+        bool any = false;
+        for (char f : g->flag) any = any || f;
+        g->barrier();  // nobody votes again before everyone has read
+        return any;
+    }
+    unsigned v = mine ? 1u : 0u;
+    unsigned *w = s->d_status + of2d::kRangeFlagWord + 1;
+    OF2D_HIP(hipMemcpyAsync(w, &v, sizeof v, hipMemcpyHostToDevice, s->st));
+    OF2D_NCCL(ncclAllReduce(w, w, 1, ncclUint32, ncclMax, s->comm, s->st));
+    OF2D_HIP(hipMemcpyAsync(&v, w, sizeof v, hipMemcpyDeviceToHost, s->st));
+    OF2D_HIP(hipStreamSynchronize(s->st));
+    return v != 0;
 }
 
 // sum of `count` doubles over the ranks, in place, on stream `st`
@@ -294,6 +316,7 @@ int of2d_slab_group_create(of2d_slab_group **out, int nranks) {
     g->n = nranks;
     g->slabs.assign(nranks, nullptr);
     g->ptr.assign(nranks, nullptr);
+    g->flag.assign(nranks, 0);
     *out = g;
     return OF2D_OK;
 }
@@ -350,6 +373,7 @@ int of2d_slab_run(of2d_slab *s, int niter, int fixed_iters, int *iters_done) {
         const int n1 = of2d::hs_nblocks(s->P, s->nrows), n2 = of2d::hs2_nblocks(s->dimx, s->nrows),
                   n3 = of2d::hs3_nblocks(s->dimx, s->nrows);
         const double npx = (double)s->dimx * s->dimy;
+        unsigned *range_flag = s->d_status + of2d::kRangeFlagWord;
         auto src_of = [](int a, int t) { return t == 0 ? a : (t % 2 == 1 ? (a + 1) % 3 : (a + 2) % 3); };
         auto dst_of = [](int a, int t) { return t % 2 == 0 ? (a + 1) % 3 : (a + 2) % 3; };
         // K (2 or 3) iterations in one pass from buffer `in` to buffer `out`.
@@ -366,7 +390,7 @@ int of2d_slab_run(of2d_slab *s, int niter, int fixed_iters, int *iters_done) {
                 if (K == 3)
                     of2d::launch_hs_jacobi3(uin, s->u[out].p, s->dI.p, s->It.p, s->P, s->dimx,
                                             s->nrows, s->rb, s->dimy, alphasq, -3, s->nrows + 3,
-                                            p1, p2, p3, s->d_status, s->st, lo, hi);
+                                            p1, p2, p3, s->d_status, range_flag, s->st, lo, hi);
                 else
                     of2d::launch_hs_jacobi2(uin, s->u[out].p, s->dI.p, s->It.p, s->P, s->dimx,
                                             s->nrows, s->rb, s->dimy, alphasq, -3, s->nrows + 3,
@@ -406,6 +430,17 @@ int of2d_slab_run(of2d_slab *s, int niter, int fixed_iters, int *iters_done) {
         }
         for (auto &f : s->u) f.zero(s->st);  // motion_est starts at zero
         OF2D_HIP(hipMemsetAsync(s->d_status, 0, sizeof(unsigned), s->st));
+        // the triple kernel's division range and the reference's divide-by-zero
+        // test (coord2d.h:95-100), once for the whole run: dI is fixed, so the
+        // test every iteration would make is known now, and all ranks throw
+        // together instead of one rank leaving the others in an exchange
+        of2d::launch_hs_precheck(s->dI.base, s->dI.count, s->P, 2, s->dimx, s->nrows, alphasq,
+                                 range_flag, s->d_status, s->st);
+        OF2D_HIP(hipMemcpyAsync(s->hs.status, s->d_status, sizeof(unsigned),
+                                hipMemcpyDeviceToHost, s->st));
+        OF2D_HIP(hipStreamSynchronize(s->st));
+        if (any_rank(s, (s->hs.status[0] & of2d::kStatusDivZero) != 0))
+            throw std::runtime_error("Divide by zero exception");
         s->errs.clear();
         OF2D_HIP(hipEventRecord(s->ev0, s->st));
         int a = 0, k0 = 0, done = -1;
@@ -524,7 +559,8 @@ int of2d_slab_time_kernel(of2d_slab *s, int nlaunch, double *avg_us) {
         auto go = [&](int k) {
             of2d::launch_hs_jacobi3(s->u[1 + (k & 1)].p, s->u[2 - (k & 1)].p, s->dI.p, s->It.p,
                                     s->P, s->dimx, s->nrows, s->rb, s->dimy, alphasq, -3,
-                                    s->nrows + 3, s->d_partial, p2, p3, s->d_status, s->st);
+                                    s->nrows + 3, s->d_partial, p2, p3, s->d_status,
+                                    s->d_status + of2d::kRangeFlagWord, s->st);
         };
         go(0);
         OF2D_HIP(hipEventRecord(s->ev0, s->st));

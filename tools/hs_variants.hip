@@ -41,6 +41,7 @@ struct Bufs {
     float *It;
     double *partial;
     unsigned *status;
+    unsigned *rflag;  // hs_precheck_kernel's range flag for dI
     int P, dimx, dimy;
 };
 
@@ -173,7 +174,7 @@ int run3(const Bufs &b, int iters, const char *name, double bytes) {
     auto launch3 = [&](const float2 *in, float2 *out) {
         hipLaunchKernelGGL(k, gl, dim3(64 * WAVES), 0, 0, in, out, b.dI, b.It, b.P, b.dimx, b.dimy,
                            0, b.dimy, 0.01f, -1, b.dimy + 1, b.partial, p2, p3, b.status, 0,
-                           (int)g.x, (int)g.y, ROWS);
+                           (int)g.x, (int)g.y, ROWS, b.rflag);
     };
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
@@ -236,6 +237,13 @@ int main(int argc, char **argv) {
     for (auto &v : h) v = (rand() / (float)RAND_MAX) - 0.5f;
     CK(hipMemcpy(based, h.data(), sizeof(float2) * b.P * rows, hipMemcpyHostToDevice));
     CK(hipMemcpy(baset, h.data(), sizeof(float) * b.P * rows, hipMemcpyHostToDevice));
+    b.rflag = b.status + 8;
+    CK(hipMemset(b.status, 0, 64));
+    hipLaunchKernelGGL(hs::hs_precheck_kernel<>, dim3(1024), dim3(256), 0, 0, based,
+                       (long)b.P * (long)rows, b.P, 1, b.dimx, b.dimy, 0.01f, b.rflag, b.status);
+    unsigned hflag = 0;
+    CK(hipMemcpy(&hflag, b.rflag, sizeof hflag, hipMemcpyDeviceToHost));
+    printf("gradient range flag %u (0: unscaled division in range)\n", hflag);
     const double bytes = 28.0 * n * n;
     printf("grid %d^2, %d launches per variant, %.1f MB per launch\n", n, iters, bytes / 1e6);
 
