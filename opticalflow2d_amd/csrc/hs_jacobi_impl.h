@@ -502,7 +502,8 @@ __global__ __launch_bounds__(64 * WAVES, MINB) void jacobi3_kernel(
     const float *__restrict__ It, int P, int dimx, int nrows, int row0, int dimy, float alphasq,
     int glo, int ghi, double *__restrict__ partial, double *__restrict__ partial2,
     double *__restrict__ partial3, unsigned *__restrict__ status, int band0, int gx, int gy,
-    int rows = ROWS, const unsigned *__restrict__ range_flag = nullptr) {
+    int rows = ROWS, const unsigned *__restrict__ range_flag = nullptr, int jlo = -1,
+    int jhi = -1) {
     int bx = (int)blockIdx.x, by = (int)blockIdx.y;
     if constexpr (XCD) {
         if (!xcd_block(gx, gy, bx, by)) return;
@@ -515,9 +516,14 @@ __global__ __launch_bounds__(64 * WAVES, MINB) void jacobi3_kernel(
     const int x = bx * kHs3Out - 4 + 2 * lane;  // this lane's px x, x+1
     const bool own = lane >= 2 && lane <= 61 && x < dimx;
     const bool xin = x >= 0 && x + 2 <= P;
+    // block row `by` of this launch covers j-lines from jlo (default: band0's
+    // first line) up to jhi (default nrows); its Logger partials go to slot
+    // (band0 + by) * gx + bx
     const int band = band0 + by;
-    const int jbeg = (band * WAVES + wave) * rows;
-    const int jend = min(jbeg + rows, nrows);
+    if (jlo < 0) jlo = band0 * WAVES * rows;
+    if (jhi < 0) jhi = nrows;
+    const int jbeg = jlo + (by * WAVES + wave) * rows;
+    const int jend = min(jbeg + rows, jhi);
     // Logger magnitudes accumulate in fp32 per lane (<= 2 * rows values of one
     // wave), in fp64 from the lane sums on; they only feed the convergence test
     float s1d = 0.0f, s1p = 0.0f, s2d = 0.0f, s2p = 0.0f, s3d = 0.0f, s3p = 0.0f;
@@ -600,7 +606,7 @@ __global__ __launch_bounds__(64 * WAVES, MINB) void jacobi3_kernel(
         sd += in1 ? d1 : 0.0f;  // a select, not a product: padding may hold 0/0
         sp += in1 ? p1 : 0.0f;
     };
-    if (jbeg < nrows) {
+    if (jbeg < jend) {
         unsigned bx_ = 0;  // halo rows: flagged by the waves that own them
         const Row<2> a0 = ldu(jbeg - 3), a1 = ldu(jbeg - 2), a2 = ldu(jbeg - 1);
         Row<2> uj = ldu(jbeg), uj1 = ldu(jbeg + 1), uj2 = ldu(jbeg + 2);

@@ -78,8 +78,30 @@ void launch_hs_jacobi3(const float2 *u_old, float2 *u_new, const float2 *dI, con
     const dim3 gl(8 * ((g.x * g.y + 7) / 8));
     hipLaunchKernelGGL(kHsJacobi3, gl, dim3(64 * kHs3Waves), 0, st, u_old, u_new, dI, It, P,
                        dimx, nrows, row0, dimy, alphasq, glo, ghi, partial, partial2, partial3,
-                       status, band_lo, (int)g.x, (int)g.y, hs3_rows(dimx, nrows), range_flag);
+                       status, band_lo, (int)g.x, (int)g.y, hs3_rows(dimx, nrows), range_flag, -1,
+                       -1);
     OF2D_HIP(hipGetLastError());
+}
+
+int launch_hs_jacobi3_window(const float2 *u_old, float2 *u_new, const float2 *dI,
+                             const float *It, int P, int dimx, int nrows, int row0, int dimy,
+                             float alphasq, int glo, int ghi, int jlo, int jhi,
+                             int rows_per_wave, int slot_band0, double *partial,
+                             double *partial2, double *partial3, unsigned *status,
+                             const unsigned *range_flag, hipStream_t st) {
+    if (P % kHsStrip != 0 || nrows <= 0 || dimx > P || dimx < 2 || glo > -1 || ghi < nrows + 1 ||
+        jlo < 0 || jhi > nrows || jlo >= jhi || rows_per_wave < 1 || slot_band0 < 0)
+        throw std::invalid_argument("launch_hs_jacobi3_window: bad geometry");
+    if (!range_flag) throw std::invalid_argument("launch_hs_jacobi3_window: no range flag");
+    const int gx = (dimx + kHs3Out - 1) / kHs3Out;
+    const int per_band = kHs3Waves * rows_per_wave;
+    const int gy = (jhi - jlo + per_band - 1) / per_band;
+    const dim3 gl(8 * ((gx * gy + 7) / 8));
+    hipLaunchKernelGGL(kHsJacobi3, gl, dim3(64 * kHs3Waves), 0, st, u_old, u_new, dI, It, P,
+                       dimx, nrows, row0, dimy, alphasq, glo, ghi, partial, partial2, partial3,
+                       status, slot_band0, gx, gy, rows_per_wave, range_flag, jlo, jhi);
+    OF2D_HIP(hipGetLastError());
+    return gy;
 }
 
 void launch_hs_precheck(const float2 *base, size_t count, int P, int ghost, int dimx, int dimy,

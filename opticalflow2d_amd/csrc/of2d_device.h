@@ -99,9 +99,11 @@ constexpr int kHs3Waves = 4;
 // register count, 256 CUs) should fill whole rounds of 1024 blocks — a grid of
 // 1120 blocks at 4096^2 with 32 j-lines ran a 9 % second round; 36 j-lines
 // (1015 blocks) is 3 % faster.  Rows per wave stay within [16, 64].
-inline int hs3_rows(int dimx, int nrows) {
+// cap: the resident blocks the launch may fill (1024 = 4 per CU on 256 CUs;
+// less when another launch is to run beside it)
+inline int hs3_rows(int dimx, int nrows, int cap = 1024) {
     const int gx = (dimx + kHs3Out - 1) / kHs3Out;
-    const int per_round = gx <= 1024 ? 1024 / gx : 1;  // bands per round of blocks
+    const int per_round = gx <= cap ? cap / gx : 1;  // bands per round of blocks
     int rounds = 1;
     for (;;) {
         const int bands = per_round * rounds;
@@ -134,6 +136,16 @@ void launch_hs_jacobi3(const float2 *u_old, float2 *u_new, const float2 *dI, con
 // any gradient / denominator of the allocation [base, base + count) lies
 // outside the unscaled-division range, and ORs kStatusDivZero into *status if
 // an image pixel's denominator is 0.  ghost: j-lines before row 0 in base.
+// The triple kernel over j-lines [jlo, jhi) of the level, rows_per_wave
+// j-lines per wave, Logger partials from slot band `slot_band0` on (slot =
+// (slot_band0 + block row) * gx + strip): the slab's interior / edge launches.
+// Returns the launch's block rows.
+int launch_hs_jacobi3_window(const float2 *u_old, float2 *u_new, const float2 *dI,
+                             const float *It, int P, int dimx, int nrows, int row0, int dimy,
+                             float alphasq, int glo, int ghi, int jlo, int jhi,
+                             int rows_per_wave, int slot_band0, double *partial,
+                             double *partial2, double *partial3, unsigned *status,
+                             const unsigned *range_flag, hipStream_t st);
 void launch_hs_precheck(const float2 *base, size_t count, int P, int ghost, int dimx, int dimy,
                         float alphasq, unsigned *range_flag, unsigned *status, hipStream_t st);
 constexpr int kRangeFlagWord = 32;  // word of the 64-word status buffers holding range_flag

@@ -49,7 +49,10 @@ struct of2d_slab {
     float alpha = 0.0f;
     hipStream_t st = nullptr;
     hipStream_t comm_st = nullptr;  // the halo exchange, overlapped with interior bands
-    hipEvent_t ev_src = nullptr, ev_halo = nullptr;
+    // split launches (slab.cpp fused): the latest work on st that comm_st must
+    // see (an interior launch, or a pair / single step) and the latest edge
+    // launches on comm_st that st must see
+    hipEvent_t ev_int = nullptr, ev_edge = nullptr;
     ncclComm_t comm = nullptr;
     of2d_slab_group *grp = nullptr;  // in-process transport instead of RCCL
     hipEvent_t ev_ready = nullptr, ev_done = nullptr;  // its exchange handshakes
@@ -218,6 +221,38 @@ void allreduce_sums(of2d_slab *s, double *buf, size_t count, hipStream_t st) {
         if (r != s->rank) OF2D_HIP(hipStreamWaitEvent(st, g->slabs[r]->ev_done, 0));
     OF2D_HIP(hipMemcpyAsync(buf, s->d_red, count * sizeof(double), hipMemcpyDeviceToDevice, st));
 }
+// Launch geometry of a slab's triples.  With neighbours and at least 3E
+// j-lines the launch is split (see fused in of2d_slab_run): interior j-lines
+// [E, nrows-E) with a block budget that leaves room for the two edge launches
+// of E = 16 j-lines (4 waves x 4 lines, one block per strip) and for the RCCL
+// send/recv kernel (kCommBlocks) to be resident beside it.  At 4096 x 4096 per
+// rank: 27 x 38-line interior bands (945 blocks) + 2 x 35 edge blocks, 104 us
+// per three iterations against 99 us for the unsplit launch
+// (tools/hs_variants split; the earlier interior-then-outer-bands order on one
+// stream took 149 us).
+struct SlabGeometry {
+    bool split = false;
+    int E = 16, re = 4;  // edge j-lines, j-lines per wave in an edge launch
+    int ri = 0, bi = 0;  // interior j-lines per wave and block rows
+    int n3 = 0;          // block partials a triple writes
+    int nb = 0;          // partial row length for every kernel of the slab
+};
+SlabGeometry slab_geometry(const of2d_slab *s) {
+    SlabGeometry g;
+    const int gx = (s->dimx + of2d::kHs3Out - 1) / of2d::kHs3Out;
+    g.split = s->nranks > 1 && s->nrows >= 3 * g.E && s->dimx >= 2;
+    if (g.split) {
+        const int ni = s->nrows - 2 * g.E;
+        constexpr int kCommBlocks = 8;
+        g.ri = of2d::hs3_rows(s->dimx, ni, std::max(gx, 1024 - 2 * gx - kCommBlocks));
+        g.bi = (ni + of2d::kHs3Waves * g.ri - 1) / (of2d::kHs3Waves * g.ri);
+        g.n3 = gx * (g.bi + 2);
+    } else {
+        g.n3 = of2d::hs3_nblocks(s->dimx, s->nrows);
+    }
+    g.nb = std::max(of2d::hs_partial_blocks(s->P, s->dimx, s->nrows), g.n3);
+    return g;
+}
 }  // namespace
 
 extern "C" {
@@ -264,14 +299,14 @@ static int slab_create(of2d_slab **out, int dimx, int dimy, float alpha, int ran
         OF2D_HIP(hipEventCreate(&s->ev0));
         OF2D_HIP(hipEventCreate(&s->ev1));
         OF2D_HIP(hipStreamCreateWithFlags(&s->comm_st, hipStreamNonBlocking));
-        OF2D_HIP(hipEventCreateWithFlags(&s->ev_src, hipEventDisableTiming));
-        OF2D_HIP(hipEventCreateWithFlags(&s->ev_halo, hipEventDisableTiming));
+        OF2D_HIP(hipEventCreateWithFlags(&s->ev_int, hipEventDisableTiming));
+        OF2D_HIP(hipEventCreateWithFlags(&s->ev_edge, hipEventDisableTiming));
         for (auto &f : s->u) f.alloc(dimx, s->nrows, 3);  // three ghost j-lines each side
         s->dI.alloc(dimx, s->nrows, 2);
         s->It.alloc(dimx, s->nrows, 2);
         s->Iref.alloc(dimx, s->nrows, 3);
         s->Imov.alloc(dimx, s->nrows, 3);
-        const int nb = of2d::hs_partial_blocks(s->P, dimx, s->nrows);
+        const int nb = slab_geometry(s).nb;
         OF2D_HIP(hipMalloc(&s->d_partial, sizeof(double) * 2 * (size_t)nb * s->chunk));
         OF2D_HIP(hipMalloc(&s->d_sums, sizeof(double) * 2 * s->chunk));
         OF2D_HIP(hipMalloc(&s->d_status, 64 * sizeof(unsigned)));
@@ -367,57 +402,70 @@ int of2d_slab_run(of2d_slab *s, int niter, int fixed_iters, int *iters_done) {
     if (!s) return OF2D_ERR_INVALID_ARGUMENT;
     return sguard(s, [&] {
         const float alphasq = s->alpha * s->alpha;
+        const SlabGeometry G = slab_geometry(s);
         // partial rows long enough for every kernel; each row is reduced over
         // the blocks of the kernel that wrote it
-        const int nb = of2d::hs_partial_blocks(s->P, s->dimx, s->nrows);
+        const int nb = G.nb;
         const int n1 = of2d::hs_nblocks(s->P, s->nrows), n2 = of2d::hs2_nblocks(s->dimx, s->nrows),
-                  n3 = of2d::hs3_nblocks(s->dimx, s->nrows);
+                  n3 = G.n3;
         const double npx = (double)s->dimx * s->dimy;
         unsigned *range_flag = s->d_status + of2d::kRangeFlagWord;
         auto src_of = [](int a, int t) { return t == 0 ? a : (t % 2 == 1 ? (a + 1) % 3 : (a + 2) % 3); };
         auto dst_of = [](int a, int t) { return t % 2 == 0 ? (a + 1) % 3 : (a + 2) % 3; };
+        // st runs after the latest edge launches / comm_st after the latest st work
+        auto join_st = [&] { OF2D_HIP(hipStreamWaitEvent(s->st, s->ev_edge, 0)); };
+        auto mark_st = [&] { OF2D_HIP(hipEventRecord(s->ev_int, s->st)); };
+        auto win3 = [&](hipStream_t st, int in, int out, int jlo, int jhi, int rpw, int slot,
+                        double *p1, double *p2, double *p3) {
+            of2d::launch_hs_jacobi3_window(s->u[in].p, s->u[out].p, s->dI.p, s->It.p, s->P,
+                                           s->dimx, s->nrows, s->rb, s->dimy, alphasq, -3,
+                                           s->nrows + 3, jlo, jhi, rpw, slot, p1, p2, p3,
+                                           s->d_status, range_flag, st);
+        };
         // K (2 or 3) iterations in one pass from buffer `in` to buffer `out`.
-        // Only the first and last row band read the ghost lines, so with
-        // neighbours the exchange runs on comm_st while the interior bands run
-        // on st: the exchange reads owned lines of `in` (no kernel writes `in`)
-        // and writes its ghost lines (read by the outer bands only, after
-        // ev_halo).
+        // One rank: one launch.  With neighbours, triples are split: the
+        // interior j-lines [E, nrows-E) on st need no halo and start at once;
+        // the exchange and the two E-line edge launches run beside them on
+        // comm_st (the interior's block budget leaves room for them), so the
+        // halo costs the edges' few row steps, not a serialised launch.  The
+        // interior of launch k reads rows E-3..E-1 of `in`, written by the
+        // edges of launch k-1 (st waits ev_edge); the edges read rows
+        // E..E+2, written by the interior of launch k-1 (comm_st waits ev_int,
+        // recorded before this launch's interior).  Pairs and single steps
+        // (chunk tails, replays) exchange and launch on st.
         auto fused = [&](int K, int in, int out, double *p1, double *p2, double *p3) {
             float2 *uin = s->u[in].p;
-            const int nbands =
-                K == 3 ? of2d::hs3_nbands(s->dimx, s->nrows) : of2d::hs2_nbands(s->nrows);
-            auto bands = [&](int lo, int hi) {
-                if (K == 3)
-                    of2d::launch_hs_jacobi3(uin, s->u[out].p, s->dI.p, s->It.p, s->P, s->dimx,
-                                            s->nrows, s->rb, s->dimy, alphasq, -3, s->nrows + 3,
-                                            p1, p2, p3, s->d_status, range_flag, s->st, lo, hi);
-                else
-                    of2d::launch_hs_jacobi2(uin, s->u[out].p, s->dI.p, s->It.p, s->P, s->dimx,
-                                            s->nrows, s->rb, s->dimy, alphasq, -3, s->nrows + 3,
-                                            p1, p2, s->d_status, s->st, lo, hi);
-            };
-            if (s->nranks == 1) {
-                bands(0, nbands);
-            } else if (nbands < 3) {
-                halo_exchange(s, uin, K, s->st);
-                bands(0, nbands);
-            } else {
-                OF2D_HIP(hipEventRecord(s->ev_src, s->st));  // `in` complete
-                OF2D_HIP(hipStreamWaitEvent(s->comm_st, s->ev_src, 0));
-                halo_exchange(s, uin, K, s->comm_st);
-                OF2D_HIP(hipEventRecord(s->ev_halo, s->comm_st));
-                bands(1, nbands - 1);
-                OF2D_HIP(hipStreamWaitEvent(s->st, s->ev_halo, 0));
-                bands(0, 1);
-                bands(nbands - 1, nbands);
+            if (K == 3 && G.split) {
+                OF2D_HIP(hipStreamWaitEvent(s->comm_st, s->ev_int, 0));
+                join_st();
+                win3(s->st, in, out, G.E, s->nrows - G.E, G.ri, 0, p1, p2, p3);
+                mark_st();
+                halo_exchange(s, uin, 3, s->comm_st);
+                win3(s->comm_st, in, out, 0, G.E, G.re, G.bi, p1, p2, p3);
+                win3(s->comm_st, in, out, s->nrows - G.E, s->nrows, G.re, G.bi + 1, p1, p2, p3);
+                OF2D_HIP(hipEventRecord(s->ev_edge, s->comm_st));
+                return;
             }
+            join_st();
+            halo_exchange(s, uin, K, s->st);
+            if (K == 3)
+                of2d::launch_hs_jacobi3(uin, s->u[out].p, s->dI.p, s->It.p, s->P, s->dimx,
+                                        s->nrows, s->rb, s->dimy, alphasq, -3, s->nrows + 3, p1,
+                                        p2, p3, s->d_status, range_flag, s->st);
+            else
+                of2d::launch_hs_jacobi2(uin, s->u[out].p, s->dI.p, s->It.p, s->P, s->dimx,
+                                        s->nrows, s->rb, s->dimy, alphasq, -3, s->nrows + 3, p1,
+                                        p2, s->d_status, s->st);
+            mark_st();
         };
         // a single step from buffer `in` to `out`
         auto single = [&](int in, int out, double *partial) {
             float2 *uin = s->u[in].p;
+            join_st();
             halo_exchange(s, uin, 1, s->st);
             of2d::launch_hs_jacobi(uin, s->u[out].p, s->dI.p, s->It.p, s->P, s->dimx, s->nrows,
                                    s->rb, s->dimy, alphasq, partial, s->d_status, s->st);
+            mark_st();
         };
         auto step = [&](int a, int t, double *partial) {
             single(src_of(a, t), dst_of(a, t), partial);
@@ -443,6 +491,9 @@ int of2d_slab_run(of2d_slab *s, int niter, int fixed_iters, int *iters_done) {
             throw std::runtime_error("Divide by zero exception");
         s->errs.clear();
         OF2D_HIP(hipEventRecord(s->ev0, s->st));
+        mark_st();  // comm_st starts after everything enqueued so far
+        OF2D_HIP(hipStreamWaitEvent(s->comm_st, s->ev_int, 0));
+        OF2D_HIP(hipEventRecord(s->ev_edge, s->comm_st));
         int a = 0, k0 = 0, done = -1;
         while (k0 < niter && done < 0) {
             const int C = std::min(s->chunk, niter - k0);
@@ -474,12 +525,14 @@ int of2d_slab_run(of2d_slab *s, int niter, int fixed_iters, int *iters_done) {
                 // no break to decide: keep every chunk's sums on the device and
                 // read them back once after the run (no host sync per chunk)
                 double *sums = s->d_all + 2 * (size_t)k0;
+                join_st();  // the edge launches' partials
                 runs.reduce(s->d_partial, nb, sums, s->st);
                 allreduce_sums(s, sums, 2 * (size_t)C, s->st);
                 a = cur;
                 k0 += C;
                 continue;
             }
+            join_st();
             runs.reduce(s->d_partial, nb, s->d_sums, s->st);
             allreduce_sums(s, s->d_sums, 2 * (size_t)C, s->st);
             OF2D_HIP(hipMemcpyAsync(s->hs.sums, s->d_sums, sizeof(double) * 2 * C,
@@ -512,6 +565,7 @@ int of2d_slab_run(of2d_slab *s, int niter, int fixed_iters, int *iters_done) {
             s->fin = a;
             done = niter;
         }
+        join_st();
         if (fixed_iters && niter > 0) {
             OF2D_HIP(hipMemcpyAsync(s->hs.sums, s->d_all, sizeof(double) * 2 * niter,
                                     hipMemcpyDeviceToHost, s->st));
@@ -598,8 +652,8 @@ int of2d_slab_destroy(of2d_slab *s) {
     if (s->d_stage) (void)hipFree(s->d_stage);
     if (s->ev0) (void)hipEventDestroy(s->ev0);
     if (s->ev1) (void)hipEventDestroy(s->ev1);
-    if (s->ev_src) (void)hipEventDestroy(s->ev_src);
-    if (s->ev_halo) (void)hipEventDestroy(s->ev_halo);
+    if (s->ev_int) (void)hipEventDestroy(s->ev_int);
+    if (s->ev_edge) (void)hipEventDestroy(s->ev_edge);
     for (auto &f : s->u) f.release();
     s->dI.release();
     s->It.release();

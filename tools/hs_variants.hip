@@ -174,7 +174,7 @@ int run3(const Bufs &b, int iters, const char *name, double bytes) {
     auto launch3 = [&](const float2 *in, float2 *out) {
         hipLaunchKernelGGL(k, gl, dim3(64 * WAVES), 0, 0, in, out, b.dI, b.It, b.P, b.dimx, b.dimy,
                            0, b.dimy, 0.01f, -1, b.dimy + 1, b.partial, p2, p3, b.status, 0,
-                           (int)g.x, (int)g.y, ROWS, b.rflag);
+                           (int)g.x, (int)g.y, ROWS, b.rflag, -1, -1);
     };
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
@@ -210,6 +210,99 @@ int run3(const Bufs &b, int iters, const char *name, double bytes) {
         }
     printf("%-28s grid=%5ux%-4u  %8.2f us/iter  %7.1f GB/s-equiv  %s\n", name, g.x, g.y, us,
            bytes / us / 1e3, bad ? "MISMATCH" : "bit-identical to 6 single steps");
+    return bad ? 1 : 0;
+}
+
+// The slab's overlapped launch (slab.cpp fused): interior j-lines [E, n-E) on
+// one stream with a block budget that leaves room for the two 16-line edge
+// launches on a second stream.  Timed per three iterations against the full
+// launch, and checked bit-identical to it.
+int run_split(const Bufs &b, int iters) {
+    using namespace of2d::hs;
+    const int gx = (b.dimx + kHs3Out - 1) / kHs3Out;
+    constexpr int E = 16, RE = E / 4;
+    const int ni = b.dimy - 2 * E;
+    const int ri = hs3_rows(b.dimx, ni, 1024 - 2 * gx);
+    const int gyi = (ni + 4 * ri - 1) / (4 * ri);
+    const int rf = hs3_rows(b.dimx, b.dimy);
+    const int gyf = (b.dimy + 4 * rf - 1) / (4 * rf);
+    auto k = jacobi3_kernel<0, 4, true, 4, 4, true>;
+    double *p2 = b.partial + 2 * 16384, *p3 = b.partial + 4 * 16384;
+    hipStream_t s1, s2;
+    CK(hipStreamCreateWithFlags(&s1, hipStreamNonBlocking));
+    CK(hipStreamCreateWithFlags(&s2, hipStreamNonBlocking));
+    hipEvent_t ei, ee, e0, e1;
+    CK(hipEventCreateWithFlags(&ei, hipEventDisableTiming));
+    CK(hipEventCreateWithFlags(&ee, hipEventDisableTiming));
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    auto win = [&](hipStream_t st, const float2 *in, float2 *out, int jlo, int jhi, int r,
+                   int slot) {
+        const int gy = (jhi - jlo + 4 * r - 1) / (4 * r);
+        hipLaunchKernelGGL(k, dim3(8 * ((gx * gy + 7) / 8)), dim3(256), 0, st, in, out, b.dI, b.It,
+                           b.P, b.dimx, b.dimy, 0, b.dimy, 0.01f, -1, b.dimy + 1, b.partial, p2,
+                           p3, b.status, slot, gx, gy, r, b.rflag, jlo, jhi);
+    };
+    auto full = [&](const float2 *in, float2 *out) { win(s1, in, out, 0, b.dimy, rf, 0); };
+    // the earlier slab scheme: interior bands, then the first and the last band,
+    // all on one stream
+    auto serial = [&](const float2 *in, float2 *out) {
+        win(s1, in, out, 4 * rf, (gyf - 1) * 4 * rf, rf, 1);
+        win(s1, in, out, 0, 4 * rf, rf, 0);
+        win(s1, in, out, (gyf - 1) * 4 * rf, b.dimy, rf, gyf - 1);
+    };
+    auto split = [&](const float2 *in, float2 *out) {
+        CK(hipStreamWaitEvent(s2, ei, 0));  // previous interior
+        CK(hipStreamWaitEvent(s1, ee, 0));  // previous edges
+        win(s1, in, out, E, b.dimy - E, ri, 0);
+        CK(hipEventRecord(ei, s1));
+        win(s2, in, out, 0, E, RE, gyi);
+        win(s2, in, out, b.dimy - E, b.dimy, RE, gyi + 1);
+        CK(hipEventRecord(ee, s2));
+    };
+    const size_t cnt = (size_t)b.P * b.dimy;
+    std::vector<float2> A(cnt), B(cnt);
+    std::vector<float2> C(cnt);
+    float ms[3];
+    for (int mode = 0; mode < 3; mode++) {
+        CK(hipDeviceSynchronize());
+        CK(hipMemset(b.u0 - b.P, 0, sizeof(float2) * (size_t)b.P * (b.dimy + 2)));
+        CK(hipMemset(b.u1 - b.P, 0, sizeof(float2) * (size_t)b.P * (b.dimy + 2)));
+        CK(hipDeviceSynchronize());
+        CK(hipEventRecord(ei, s1));
+        CK(hipEventRecord(ee, s2));
+        auto go = [&](int it) {
+            const float2 *in = (it & 1) ? b.u1 : b.u0;
+            float2 *out = (it & 1) ? b.u0 : b.u1;
+            if (mode == 0)
+                full(in, out);
+            else if (mode == 1)
+                split(in, out);
+            else
+                serial(in, out);
+        };
+        for (int it = 0; it < 2; it++) go(it);
+        CK(hipStreamWaitEvent(s1, ee, 0));
+        CK(hipStreamSynchronize(s1));
+        CK(hipMemcpy(mode == 0 ? A.data() : mode == 1 ? B.data() : C.data(), b.u0,
+                     sizeof(float2) * cnt, hipMemcpyDeviceToHost));
+        CK(hipEventRecord(e0, s1));
+        CK(hipStreamWaitEvent(s2, e0, 0));
+        for (int it = 0; it < iters; it++) go(it);
+        CK(hipStreamWaitEvent(s1, ee, 0));
+        CK(hipEventRecord(e1, s1));
+        CK(hipEventSynchronize(e1));
+        CK(hipEventElapsedTime(&ms[mode], e0, e1));
+    }
+    long bad = 0;
+    for (size_t i = 0; i < cnt; i++)
+        if (memcmp(&A[i], &B[i], sizeof(float2)) != 0 || memcmp(&A[i], &C[i], sizeof(float2)) != 0)
+            bad++;
+    printf("full launch  %3d x %d rows  %8.2f us / 3 iterations\n", gyf, rf, 1000.0 * ms[0] / iters);
+    printf("split launch %3d x %d rows + 2 x %d-line edges (second stream)  %8.2f us / 3 iterations  %s\n",
+           gyi, ri, E, 1000.0 * ms[1] / iters, bad ? "MISMATCH" : "bit-identical to the full launch");
+    printf("serial bands (interior, first, last on one stream)  %8.2f us / 3 iterations\n",
+           1000.0 * ms[2] / iters);
     return bad ? 1 : 0;
 }
 
@@ -302,6 +395,8 @@ int main(int argc, char **argv) {
     const bool product_only = argc > 3 && strcmp(argv[3], "product") == 0;
     if (argc > 3 && strcmp(argv[3], "pair") == 0)  // the product pair kernel (PMC runs)
         return run2<32, 4, 2, true>(b, iters, "two-step 32r 4w xcd (product)", bytes);
+    if (argc > 3 && strcmp(argv[3], "split") == 0)  // the slab's overlapped interior / edges
+        return run_split(b, iters);
     if (argc > 3 && strcmp(argv[3], "triple") == 0)  // the product triple kernel (PMC runs)
         return run3<36, 4, 4, 4, true>(b, iters, "three-step 36r 4w xcd (product at 4096^2)", bytes);
     if (argc > 3 && strcmp(argv[3], "two") == 0) {
