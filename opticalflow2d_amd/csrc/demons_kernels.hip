@@ -146,7 +146,8 @@ __global__ __launch_bounds__(256) void demons_force_kernel(
     if (i >= dimx) return;
     const int c = threadIdx.x + 1;
     bool zero = false;
-    for (int rr = threadIdx.y; rr < kFy; rr += 4) {
+    // the wave index is uniform (64-thread rows): scalar row arithmetic
+    for (int rr = (int)__builtin_amdgcn_readfirstlane(threadIdx.y); rr < kFy; rr += 4) {
         const int j = y0 + rr;
         if (j >= dimy) break;
         const int r = rr + 1;
@@ -340,7 +341,8 @@ __global__ __launch_bounds__(256) void smooth_compose_kernel(
     const long N = (long)dimx * dimy;
     const int i = x0 + threadIdx.x;
     if (i >= dimx) return;
-    const int r0 = threadIdx.y * (kCy / kCThreadsY);  // four consecutive j-lines per thread
+    // four consecutive j-lines per thread; the wave index is uniform
+    const int r0 = (int)__builtin_amdgcn_readfirstlane(threadIdx.y) * (kCy / kCThreadsY);
     float2 sm[4];
     bool has[4];
     conv4<KW>(tile, a, i, y0 + r0, threadIdx.x, r0, dimx, dimy, N, sm, has);
@@ -447,7 +449,7 @@ __global__ __launch_bounds__(256) void smooth_norm_kernel(const float2 *__restri
     const int i = x0 + threadIdx.x;
     double sd = 0.0, sp = 0.0;
     if (i < dimx) {
-        const int r0 = threadIdx.y * (kCy / kCThreadsY);
+        const int r0 = (int)__builtin_amdgcn_readfirstlane(threadIdx.y) * (kCy / kCThreadsY);
         float2 sm[4];
         bool has[4];
         conv4<KW>(tile, a, i, y0 + r0, threadIdx.x, r0, dimx, dimy, N, sm, has);

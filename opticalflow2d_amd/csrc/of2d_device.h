@@ -95,23 +95,29 @@ void launch_hs_jacobi2(const float2 *u_old, float2 *u_new, const float2 *dI, con
 // kernel (the first two steps also cover two / one halo rows each side).
 constexpr int kHs3Out = 120;  // output columns per wave (hs_jacobi_impl.h)
 constexpr int kHs3Waves = 4;
-// j-lines per wave: the 4-wave blocks (4 resident per CU at the kernel's
-// register count, 256 CUs) should fill whole rounds of 1024 blocks — a grid of
-// 1120 blocks at 4096^2 with 32 j-lines ran a 9 % second round; 36 j-lines
-// (1015 blocks) is 3 % faster.  Rows per wave stay within [16, 64].
-// cap: the resident blocks the launch may fill (1024 = 4 per CU on 256 CUs;
-// less when another launch is to run beside it)
+// j-lines per wave.  A block's time is about (rows + 2) row steps (the
+// prologue computes the halo rows of the first two iterations), and the 4-wave
+// blocks (4 resident per CU, 256 CUs: `cap` = 1024 block slots, less when
+// another launch is to run beside it) run in rounds, so the choice minimises
+// rounds x (rows + 2) over rows in [4, 64], fewest rows on ties.  4096^2: 36
+// (1015 blocks, one round; 32 gave 1120 blocks and a 9 % second round);
+// 16384^2: 50 (11 rounds of 1006-1024 blocks, against 59 and 9.4 rounds);
+// grids too small to fill one round get short bands and more blocks.
 inline int hs3_rows(int dimx, int nrows, int cap = 1024) {
-    const int gx = (dimx + kHs3Out - 1) / kHs3Out;
-    const int per_round = gx <= cap ? cap / gx : 1;  // bands per round of blocks
-    int rounds = 1;
-    for (;;) {
-        const int bands = per_round * rounds;
-        const int rows = (nrows + kHs3Waves * bands - 1) / (kHs3Waves * bands);
-        // below 16 j-lines per wave the 6 + 4 halo rows would dominate
-        if (rows <= 64 || bands >= nrows) return rows < 16 ? 16 : rows;
-        rounds++;
+    const long gx = (dimx + kHs3Out - 1) / kHs3Out;
+    int best = 4;
+    long best_t = -1;
+    for (int r = 4; r <= 64; r++) {
+        const long bands = (nrows + kHs3Waves * r - 1) / (kHs3Waves * r);
+        const long rounds = (gx * bands + cap - 1) / cap;
+        const long t = rounds * (r + 2);
+        if (best_t < 0 || t < best_t) {
+            best_t = t;
+            best = r;
+        }
+        if (bands == 1) break;  // more rows per wave change nothing
     }
+    return best;
 }
 inline int hs3_nbands(int dimx, int nrows) {
     const int r = kHs3Waves * hs3_rows(dimx, nrows);
