@@ -89,6 +89,8 @@ def main():
     ap.add_argument("--cpu-iters", type=int, default=20)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--timing-launches", type=int, default=200)
+    ap.add_argument("--rccl", action="store_true",
+                    help="N = 1: run the Logger all-reduces through a one-rank RCCL communicator")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -100,18 +102,24 @@ def main():
                   file=sys.stderr)
             sys.exit(2)
 
+    # libof2d (and the /opt/rocm HIP runtime and RCCL it links) loads before
+    # torch at every N: torch ships its own libamdhip64 / librccl under the same
+    # sonames, and whichever loads first serves both
+    from opticalflow2d_amd import SlabSolver, lib
+    from opticalflow2d_amd import synthetic as S
+    from opticalflow2d_amd.slab import halo_rows, rccl_unique_id
+    lib()
+
     dist = None
-    if world > 1:
+    if world > 1 or "WORLD_SIZE" in os.environ:  # launched by torch.distributed.run
         import torch.distributed as dist  # noqa: F811
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("gloo", rank=rank, world_size=world)
 
-    from opticalflow2d_amd import SlabSolver
-    from opticalflow2d_amd import synthetic as S
-    from opticalflow2d_amd.slab import halo_rows, rccl_unique_id
-
     uid = None
-    if world > 1:
+    if world == 1 and args.rccl:
+        uid = rccl_unique_id()  # one-rank communicator: the RCCL all-reduces run too
+    elif world > 1:
         obj = [rccl_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(obj, src=0)
         uid = obj[0]

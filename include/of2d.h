@@ -114,7 +114,8 @@ const char *of2d_gateway_last_error(void);
  * halo (K j-lines to each neighbour before every fused launch of K = 3, 2 or 1
  * iterations) travels over RCCL, overlapped with the interior row bands.  A
  * slab needs >= 3 j-lines.
- * nranks == 1 needs no unique id (pass NULL). */
+ * nranks == 1 needs no unique id (pass NULL); with one, a one-rank RCCL
+ * communicator carries the Logger all-reduces (exercises RCCL on one GPU). */
 int of2d_slab_bounds(int dimy, int rank, int nranks, int *row_begin, int *row_end);
 int of2d_rccl_unique_id_size(void);
 int of2d_rccl_get_unique_id(void *out, int len);

@@ -107,6 +107,9 @@ thread_local std::string g_create_err;
 template <class F>
 int sguard(of2d_slab *s, F &&f) {
     try {
+        // every entry point binds the calling thread to the slab's device (a
+        // caller may have switched it since create)
+        if (s && s->P > 0) OF2D_HIP(hipSetDevice(s->device));
         f();
         if (s) s->err.clear();
         return OF2D_OK;
@@ -177,7 +180,7 @@ void halo_exchange(of2d_slab *s, float2 *u, int lines, hipStream_t st) {
 
 // true on every rank if `mine` is true on any rank (host-side; synchronises)
 bool any_rank(of2d_slab *s, bool mine) {
-    if (s->nranks == 1) return mine;
+    if (s->nranks == 1 && !s->comm) return mine;
     if (s->grp) {
         of2d_slab_group *g = s->grp;
         g->flag[s->rank] = mine;
@@ -198,7 +201,7 @@ bool any_rank(of2d_slab *s, bool mine) {
 
 // sum of `count` doubles over the ranks, in place, on stream `st`
 void allreduce_sums(of2d_slab *s, double *buf, size_t count, hipStream_t st) {
-    if (s->nranks == 1) return;
+    if (s->nranks == 1 && !s->comm) return;
     if (!s->grp) {
         OF2D_NCCL(ncclAllReduce(buf, buf, count, ncclDouble, ncclSum, s->comm, st));
         return;
@@ -323,7 +326,9 @@ static int slab_create(of2d_slab **out, int dimx, int dimy, float alpha, int ran
             if (grp->slabs[rank]) throw std::invalid_argument("slab: rank already in the group");
             grp->slabs[rank] = s;
             s->grp = grp;
-        } else if (nranks > 1) {
+        } else if (nranks > 1 || uid) {
+            // nranks == 1 with an id: a one-rank communicator, so that the RCCL
+            // calls (init, all-reduces) run on a one-GPU box too
             if (!uid || id_len < (int)sizeof(ncclUniqueId))
                 throw std::invalid_argument("slab: RCCL unique id required for nranks > 1");
             ncclUniqueId id;

@@ -1,0 +1,78 @@
+"""The RCCL side of the row-slab solver on ONE GPU.
+
+RCCL refuses two ranks on one device, so the send/recv halo itself only runs in
+the driver's multi-GPU bench; test_gpu_slab_local.py covers the slab code with
+an in-process transport.  What one GPU can check is everything around it, in
+the process layout the multi-GPU bench uses:
+
+* ``bench.py`` launched by ``torch.distributed.run`` (gloo process group,
+  libof2d loaded before torch, rank-0 unique id, max-over-ranks time, JSON
+  line) with a one-rank RCCL communicator (``--rccl``);
+* a one-rank communicator (``ncclCommInitRank`` + the Logger ``ncclAllReduce``
+  per chunk + the divide-by-zero vote) against the communicator-free slab:
+  bit-identical motion and the same iteration count, with convergence on.
+
+Each case runs in a fresh process so the library load order is the bench's.
+"""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+ONE_RANK = r"""
+import sys, numpy as np
+sys.path.insert(0, sys.argv[1])
+from opticalflow2d_amd import SlabSolver, lib
+from opticalflow2d_amd import synthetic as S
+from opticalflow2d_amd.slab import rccl_unique_id
+lib()
+import torch.distributed  # noqa: F401  (torch after libof2d, as in bench.py)
+n = 384
+ref, mov = S.procedural_pair(n, 0, n)
+out = []
+for uid in (None, rccl_unique_id()):
+    s = SlabSolver(n, n, 0.1, 0, 1, device=0, unique_id=uid)
+    s.set_images(ref, mov)
+    done = s.run(1000, fixed_iters=False)
+    out.append((done, s.motion()))
+    s.close()
+(d0, m0), (d1, m1) = out
+assert 1 < d0 <= 1000, d0
+assert d0 == d1, (d0, d1)
+assert np.array_equal(m0.view(np.uint64), m1.view(np.uint64))
+print("ONE-RANK-OK", d0)
+"""
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def test_one_rank_communicator_matches_plain_slab():
+    r = subprocess.run([sys.executable, "-c", ONE_RANK, ROOT], capture_output=True, text=True,
+                       timeout=240)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    assert "ONE-RANK-OK" in r.stdout
+
+
+def test_bench_under_torch_distributed_run():
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(ROOT, "bench.py"), "--gpus", "1", "--steps", "99", "--warmup", "3",
+           "--size", "1024", "--no-cpu-baseline", "--rccl", "--timing-launches", "5"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    res = json.loads(lines[0])
+    assert res["n_gpus"] == 1 and res["steps"] == 99 and res["value"] > 0
+    assert res["roofline"]["avg_launch_us"] > 0

@@ -8,7 +8,11 @@ loads, 8-B It loads, 16-B stores), so it calibrates the counters for this
 pattern (MI355X_MICROARCH.md: FETCH_SIZE under-reports wide streaming reads
 by 2x on gfx950; other widths are uncalibrated).  Writes
 profiles/hs_traffic.json with the corrected bytes per launch.
-usage: pmc_traffic.py <fetch_counter_collection.csv> <write_counter_collection.csv> [n]
+usage: pmc_traffic.py [--out F] <fetch_counter_collection.csv> <write_counter_collection.csv> [n]
+                      [--bench <fetch_csv> <write_csv>]
+With --bench the kernel measured is the product triple kernel as bench.py
+launches it (two more --pmc passes over `bench.py`), corrected with the
+probe's calibration from the harness passes.
 """
 import csv
 import json
@@ -30,8 +34,13 @@ def per_kernel(path, counter):
 def main():
     args = sys.argv[1:]
     out_path = None
+    bench = None
     if args and args[0] == "--out":
         out_path, args = args[1], args[2:]
+    if "--bench" in args:
+        i = args.index("--bench")
+        bench = (args[i + 1], args[i + 2])
+        args = args[:i] + args[i + 3:]
     fetch_csv, write_csv = args[0], args[1]
     n = int(args[2]) if len(args) > 2 else 4096
     P = (n + 255) // 256 * 256
@@ -46,6 +55,17 @@ def main():
     probe_write_true = 8.0 * px
     fcal = probe_read_true / (fetch[probe] * 1024.0)
     wcal = probe_write_true / (write[probe] * 1024.0)
+    source = ("rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes) on tools/hs_variants, "
+              "calibrated on the probe kernel's known bytes")
+    if bench:
+        bf = per_kernel(bench[0], "FETCH_SIZE")
+        bw = per_kernel(bench[1], "WRITE_SIZE")
+        jac = [k for k in bf if "jacobi3_kernel" in k][0]
+        fetch[jac], write[jac] = bf[jac], bw[jac]
+        per_launch = 3
+        source = ("rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes) over bench.py's own "
+                  "launches of the product kernel, calibrated on the probe kernel's known bytes "
+                  "(tools/hs_variants passes in the same session)")
     rd = fetch[jac] * 1024.0 * fcal
     wr = write[jac] * 1024.0 * wcal
     alg = 28.0 * n * n
@@ -62,8 +82,7 @@ def main():
         "algorithmic_bytes_per_launch": alg,
         "iterations_per_launch": per_launch,
         "traffic_over_algorithmic": (rd + wr) / alg,
-        "source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes) on tools/hs_variants, "
-                  "calibrated on the probe kernel's known bytes",
+        "source": source,
     }
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     if out_path is None:  # on the GPU box write under gpurun_out/ (merged back), copy by hand
