@@ -83,8 +83,10 @@ def load_traffic():
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=1000)
-    ap.add_argument("--warmup", type=int, default=50)
+    # the default warm-up runs past the clock transient of the first ~40 ms of
+    # sustained load (profiles/r01_v14_bench_warmup.log: W=50 times the dip)
+    ap.add_argument("--steps", type=int, default=3000)
+    ap.add_argument("--warmup", type=int, default=1500)
     ap.add_argument("--size", type=int, default=4096, help="dimx and rows per GPU")
     ap.add_argument("--cpu-iters", type=int, default=20)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -156,8 +158,13 @@ def main():
         elapsed = float(t.item())
     assert done == args.steps
 
-    # dominant kernel: average launch duration from HIP events on its own stream
-    avg_us = solver.time_kernel(args.timing_launches)
+    # dominant kernel: average duration per launch over the timed region, from
+    # the HIP events the solver records around the run on its own stream (the
+    # run is triple launches except a pair / single step per run tail; the
+    # per-chunk partial reductions between them are included)
+    avg_us = gpu_ms * 1000.0 * ITERS_PER_LAUNCH / args.steps
+    # and back-to-back launches of the kernel alone, after the run
+    iso_us = solver.time_kernel(args.timing_launches)
     px_rank = dimx * (solver.row_end - solver.row_begin)
     achieved = BYTES_PER_PX_LAUNCH * px_rank / (avg_us * 1e-6) / 1e9
     traffic = load_traffic()
@@ -197,13 +204,16 @@ def main():
             },
             "roofline": {
                 "bound": "hbm",
-                "kernel": "of2d::hs::jacobi3_kernel<0,4,true,4,4,true>",
+                "kernel": "of2d::hs::jacobi3_kernel<0,4,true,4,4,true,1>",
                 "iterations_per_launch": ITERS_PER_LAUNCH,
                 "achieved": round(achieved, 1),
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "avg_launch_us": round(avg_us, 3),
+                "avg_launch_source": "HIP events around the timed run on the solver's stream "
+                                     "(gpu ms x 3 / steps)",
+                "isolated_launch_us": round(iso_us, 3),
                 "bytes_per_launch": BYTES_PER_PX_LAUNCH * px_rank,
                 "traffic": (traffic or {}).get("bytes_per_launch"),
                 # the unfused reference algorithm's 28 B per pixel-iteration at the

@@ -20,6 +20,13 @@
 
 #include "of2d_device.h"
 
+// Diagnostic hooks of the triple kernel (the tuning harness defines them to
+// stamp each wave's start / end; the product build leaves them empty)
+#ifndef OF2D_HS3_STAMP_BEGIN
+#define OF2D_HS3_STAMP_BEGIN
+#define OF2D_HS3_STAMP_END
+#endif
+
 namespace of2d {
 namespace hs {
 
@@ -496,7 +503,56 @@ __global__ __launch_bounds__(64 * WAVES) void jacobi2_kernel(
 // now issue/latency-bound more than HBM-bound.  band0 as in jacobi2_kernel.
 // ROWS > 0: j-lines per wave fixed at compile time; ROWS == 0: `rows` (chosen
 // by the launcher so that the grid fills whole rounds of resident blocks)
-template <int ROWS, int WAVES, bool XCD = true, int MINB = 1, int UNR = 4, bool FD = true>
+// Issue priority by progress (PRIO > 0).  The SIMD arbiter issues VALU by
+// priority, then age, so with equal priorities the four co-resident waves of a
+// SIMD finish in dispatch order and the youngest runs its last rows with the
+// SIMD nearly empty (tools/hs_variants stamps).  Waves that have done less
+// of their band run at higher priority, which keeps the four abreast.
+template <int PRIO>
+__device__ __forceinline__ void progress_prio(int done, int total) {
+    if constexpr (PRIO == 1) {
+        const int q = (done * 16) / total;  // scalar
+        if (q < 8)
+            __builtin_amdgcn_s_setprio(3);
+        else if (q < 12)
+            __builtin_amdgcn_s_setprio(2);
+        else if (q < 14)
+            __builtin_amdgcn_s_setprio(1);
+        else
+            __builtin_amdgcn_s_setprio(0);
+    } else if constexpr (PRIO == 3) {
+        const int q = (done * 3) / total;
+        if (q < 1)
+            __builtin_amdgcn_s_setprio(2);
+        else if (q < 2)
+            __builtin_amdgcn_s_setprio(1);
+        else
+            __builtin_amdgcn_s_setprio(0);
+    } else if constexpr (PRIO == 4) {
+        const int q = (done * 20) / total;
+        if (q < 6)
+            __builtin_amdgcn_s_setprio(3);
+        else if (q < 11)
+            __builtin_amdgcn_s_setprio(2);
+        else if (q < 16)
+            __builtin_amdgcn_s_setprio(1);
+        else
+            __builtin_amdgcn_s_setprio(0);
+    } else if constexpr (PRIO == 2) {
+        const int q = (done * 4) / total;
+        if (q < 1)
+            __builtin_amdgcn_s_setprio(3);
+        else if (q < 2)
+            __builtin_amdgcn_s_setprio(2);
+        else if (q < 3)
+            __builtin_amdgcn_s_setprio(1);
+        else
+            __builtin_amdgcn_s_setprio(0);
+    }
+}
+
+template <int ROWS, int WAVES, bool XCD = true, int MINB = 1, int UNR = 4, bool FD = true,
+          int PRIO = 0>
 __global__ __launch_bounds__(64 * WAVES, MINB) void jacobi3_kernel(
     const float2 *__restrict__ uo, float2 *__restrict__ un, const float2 *__restrict__ dI,
     const float *__restrict__ It, int P, int dimx, int nrows, int row0, int dimy, float alphasq,
@@ -504,6 +560,7 @@ __global__ __launch_bounds__(64 * WAVES, MINB) void jacobi3_kernel(
     double *__restrict__ partial3, unsigned *__restrict__ status, int band0, int gx, int gy,
     int rows = ROWS, const unsigned *__restrict__ range_flag = nullptr, int jlo = -1,
     int jhi = -1) {
+    OF2D_HS3_STAMP_BEGIN
     int bx = (int)blockIdx.x, by = (int)blockIdx.y;
     if constexpr (XCD) {
         if (!xcd_block(gx, gy, bx, by)) return;
@@ -658,11 +715,13 @@ __global__ __launch_bounds__(64 * WAVES, MINB) void jacobi3_kernel(
         };
         int j = jbeg;
         for (; j + UNR < jend; j += UNR) {
+            progress_prio<PRIO>(j - jbeg, jend - jbeg);
 #pragma unroll
             for (int k = 0; k < UNR; k++) body(j + k, true);
         }
         for (; j < jend; ++j) body(j, j + 1 < jend);
     }
+    OF2D_HS3_STAMP_END
     double d1d = s1d, d1p = s1p, d2d = s2d, d2p = s2p, d3d = s3d, d3p = s3p;
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) {

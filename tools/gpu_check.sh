@@ -19,5 +19,5 @@ step tests 600 python -m pytest tests -m gpu -x -q ; rc=$?
 step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit $?
 step bench 600 python bench.py || exit $?
 R=$PWD
-step prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/$OUT/prof" -o hs -- python3 "$R/bench.py" --steps 300 --warmup 20 --no-cpu-baseline || exit $?
+step prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/$OUT/prof" -o hs -- python3 "$R/bench.py" --no-cpu-baseline || exit $?
 echo ALL-DONE

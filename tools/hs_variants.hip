@@ -7,11 +7,27 @@
 //         -I opticalflow2d_amd/csrc tools/hs_variants.hip -o tools/hs_variants
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <cmath>
+#include <map>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <vector>
 
+// wave start / end stamps of the triple kernel (mode "stamps"): 100 MHz
+// s_memrealtime, XCC id and HW_ID, one record of 4 words per wave
+__device__ unsigned long long *g_stamps = nullptr;
+#define OF2D_HS3_STAMP_BEGIN const unsigned long long stamp0_ = __builtin_amdgcn_s_memrealtime();
+#define OF2D_HS3_STAMP_END                                                              \
+    if (g_stamps && (threadIdx.x & 63) == 0) {                                          \
+        const unsigned long long t1_ = __builtin_amdgcn_s_memrealtime();                \
+        const unsigned w_ = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);        \
+        g_stamps[4 * w_] = stamp0_;                                                     \
+        g_stamps[4 * w_ + 1] = t1_;                                                     \
+        g_stamps[4 * w_ + 2] = __builtin_amdgcn_s_getreg((3 << 11) | 20);              \
+        g_stamps[4 * w_ + 3] = __builtin_amdgcn_s_getreg((31 << 11) | 4);              \
+    }
 #include "hs_jacobi_impl.h"
 
 using namespace of2d;
@@ -306,6 +322,180 @@ int run_split(const Bufs &b, int iters) {
     return bad ? 1 : 0;
 }
 
+// One stamped launch of the product triple kernel (runtime rows per wave, as
+// launch_hs_jacobi3 picks them) after a warm-up: when each wave starts and
+// ends, so the tail (waves idle while the slowest finish) can be read off.
+template <int PRIO>
+int run_stamps(const Bufs &b) {
+    using namespace of2d::hs;
+    const int gx = (b.dimx + kHs3Out - 1) / kHs3Out;
+    const int r = hs3_rows(b.dimx, b.dimy);
+    const int gy = (b.dimy + 4 * r - 1) / (4 * r);
+    const int nblk = 8 * ((gx * gy + 7) / 8);
+    auto k = jacobi3_kernel<0, 4, true, 4, 4, true, PRIO>;
+    double *p2 = b.partial + 2 * 16384, *p3 = b.partial + 4 * 16384;
+    auto go = [&](int it) {
+        hipLaunchKernelGGL(k, dim3(nblk), dim3(256), 0, 0, (it & 1) ? b.u1 : b.u0,
+                           (it & 1) ? b.u0 : b.u1, b.dI, b.It, b.P, b.dimx, b.dimy, 0, b.dimy,
+                           0.01f, -1, b.dimy + 1, b.partial, p2, p3, b.status, 0, gx, gy, r,
+                           b.rflag, -1, -1);
+    };
+    const size_t nw = (size_t)nblk * 4;
+    unsigned long long *d;
+    CK(hipMalloc(&d, sizeof(unsigned long long) * 4 * nw));
+    CK(hipMemset(d, 0, sizeof(unsigned long long) * 4 * nw));
+    for (int it = 0; it < 40; it++) go(it);
+    CK(hipDeviceSynchronize());
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    CK(hipEventRecord(e0, 0));
+    for (int it = 0; it < 100; it++) go(it);
+    CK(hipEventRecord(e1, 0));
+    CK(hipEventSynchronize(e1));
+    float ms;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    std::vector<unsigned long long> h(4 * nw);
+    printf("stamps PRIO=%d: %d x %d blocks (%d rows per wave), %zu waves; %.2f us per launch "
+           "(100 launches, events)\n", PRIO, gx, gy, r, nw, 10.0 * ms);
+    for (int rep = 0; rep < 3; rep++) {
+        CK(hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), &d, sizeof d));
+        go(rep);
+        CK(hipDeviceSynchronize());
+        unsigned long long *z = nullptr;
+        CK(hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), &z, sizeof z));
+        CK(hipMemcpy(h.data(), d, sizeof(unsigned long long) * 4 * nw, hipMemcpyDeviceToHost));
+        unsigned long long t0 = ~0ull, t1 = 0;
+        std::vector<double> st, en, du;
+        double xsum[8] = {0}, xmax[8] = {0};
+        int xn[8] = {0};
+        for (size_t w = 0; w < nw; w++)
+            if (h[4 * w + 1]) {
+                t0 = std::min(t0, h[4 * w]);
+                t1 = std::max(t1, h[4 * w + 1]);
+            }
+        for (size_t w = 0; w < nw; w++) {
+            if (!h[4 * w + 1]) continue;
+            const double a = (h[4 * w] - t0) * 0.01, e = (h[4 * w + 1] - t0) * 0.01;  // us
+            st.push_back(a);
+            en.push_back(e);
+            du.push_back(e - a);
+            const int x = (int)(h[4 * w + 2] & 7);
+            xsum[x] += e - a;
+            xmax[x] = std::max(xmax[x], e);
+            xn[x]++;
+        }
+        auto pct = [](std::vector<double> v, double p) {
+            std::sort(v.begin(), v.end());
+            return v[(size_t)(p * (v.size() - 1))];
+        };
+        printf(" launch %d: span %.1f us, %zu waves stamped\n", rep, (t1 - t0) * 0.01, du.size());
+        printf("  start  p0 %.1f p50 %.1f p90 %.1f p100 %.1f\n", pct(st, 0), pct(st, .5),
+               pct(st, .9), pct(st, 1));
+        printf("  end    p0 %.1f p10 %.1f p50 %.1f p90 %.1f p100 %.1f\n", pct(en, 0),
+               pct(en, .1), pct(en, .5), pct(en, .9), pct(en, 1));
+        printf("  dur    p0 %.1f p10 %.1f p50 %.1f p90 %.1f p100 %.1f\n", pct(du, 0),
+               pct(du, .1), pct(du, .5), pct(du, .9), pct(du, 1));
+        double busy = 0;
+        for (double v : du) busy += v;
+        printf("  wave-slot occupancy over the span: %.3f\n", busy / (du.size() * (t1 - t0) * 0.01));
+        if (rep == 2) {  // mean duration by strip, by band, and the spread inside a CU
+            std::vector<double> sb(gx, 0), sg(gy, 0);
+            std::vector<int> nb(gx, 0), ng(gy, 0);
+            std::map<unsigned, std::vector<double>> cu;
+            const int per = (gx * gy + 7) / 8;
+            for (size_t w = 0; w < nw; w++) {
+                if (!h[4 * w + 1]) continue;
+                const int blk = (int)(w / 4), L = (blk % 8) * per + blk / 8;
+                const double dd = (h[4 * w + 1] - h[4 * w]) * 0.01;
+                sb[L % gx] += dd;
+                nb[L % gx]++;
+                sg[L / gx] += dd;
+                ng[L / gx]++;
+                const unsigned hw = (unsigned)h[4 * w + 3];
+                cu[((unsigned)h[4 * w + 2] << 16) | (hw >> 8)].push_back(dd);
+            }
+            printf("  by strip:");
+            for (int i = 0; i < gx; i++) printf(" %.0f", nb[i] ? sb[i] / nb[i] : 0.0);
+            printf("\n  by band:");
+            for (int i = 0; i < gy; i++) printf(" %.0f", ng[i] ? sg[i] / ng[i] : 0.0);
+            double within = 0, across = 0, gm = 0;
+            int nn = 0;
+            std::vector<double> cm;
+            for (auto &kv : cu) {
+                double m = 0;
+                for (double v : kv.second) m += v;
+                m /= kv.second.size();
+                cm.push_back(m);
+                for (double v : kv.second) within += (v - m) * (v - m), nn++;
+                gm += m;
+            }
+            gm /= cm.size();
+            for (double m : cm) across += (m - gm) * (m - gm);
+            printf("\n  %zu CUs: std within a CU %.1f us, std of CU means %.1f us\n", cm.size(),
+                   sqrt(within / nn), sqrt(across / cm.size()));
+        }
+        for (int x = 0; x < 8; x++)
+            if (xn[x])
+                printf("  xcc %d: %4d waves, mean dur %.1f us, last end %.1f us\n", x, xn[x],
+                       xsum[x] / xn[x], xmax[x]);
+    }
+    CK(hipFree(d));
+    return 0;
+}
+
+// Back-to-back launches of the product triple kernel with the progress
+// priority schemes, interleaved in rounds so clock drift hits all alike.
+template <int PRIO>
+float time_prio(const Bufs &b, int nl) {
+    using namespace of2d::hs;
+    const int gx = (b.dimx + kHs3Out - 1) / kHs3Out;
+    const int r = hs3_rows(b.dimx, b.dimy);
+    const int gy = (b.dimy + 4 * r - 1) / (4 * r);
+    const int nblk = 8 * ((gx * gy + 7) / 8);
+    auto k = jacobi3_kernel<0, 4, true, 4, 4, true, PRIO>;
+    double *p2 = b.partial + 2 * 16384, *p3 = b.partial + 4 * 16384;
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    auto go = [&](int it) {
+        hipLaunchKernelGGL(k, dim3(nblk), dim3(256), 0, 0, (it & 1) ? b.u1 : b.u0,
+                           (it & 1) ? b.u0 : b.u1, b.dI, b.It, b.P, b.dimx, b.dimy, 0, b.dimy,
+                           0.01f, -1, b.dimy + 1, b.partial, p2, p3, b.status, 0, gx, gy, r,
+                           b.rflag, -1, -1);
+    };
+    for (int it = 0; it < 4; it++) go(it);
+    CK(hipEventRecord(e0, 0));
+    for (int it = 0; it < nl; it++) go(it);
+    CK(hipEventRecord(e1, 0));
+    CK(hipEventSynchronize(e1));
+    float ms;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    CK(hipEventDestroy(e0));
+    CK(hipEventDestroy(e1));
+    return 1000.0f * ms / nl;
+}
+
+int run_prio(const Bufs &b) {
+    const char *names[] = {"prio0", "prio1", "prio2", "prio3", "prio4"};
+    std::vector<std::vector<float>> t(5);
+    for (int round = 0; round < 6; round++) {
+        t[0].push_back(time_prio<0>(b, 200));
+        t[1].push_back(time_prio<1>(b, 200));
+        t[2].push_back(time_prio<2>(b, 200));
+        t[3].push_back(time_prio<3>(b, 200));
+        t[4].push_back(time_prio<4>(b, 200));
+    }
+    for (int v = 0; v < 5; v++) {
+        printf("%s:", names[v]);
+        for (float x : t[v]) printf(" %.2f", x);
+        std::vector<float> s = t[v];
+        std::sort(s.begin(), s.end());
+        printf("  median %.2f us/launch\n", s[s.size() / 2]);
+    }
+    return 0;
+}
+
 int main(int argc, char **argv) {
     const int n = argc > 1 ? atoi(argv[1]) : 4096;
     const int iters = argc > 2 ? atoi(argv[2]) : 200;
@@ -395,6 +585,9 @@ int main(int argc, char **argv) {
     const bool product_only = argc > 3 && strcmp(argv[3], "product") == 0;
     if (argc > 3 && strcmp(argv[3], "pair") == 0)  // the product pair kernel (PMC runs)
         return run2<32, 4, 2, true>(b, iters, "two-step 32r 4w xcd (product)", bytes);
+    if (argc > 3 && strcmp(argv[3], "prio") == 0) return run_prio(b);
+    if (argc > 3 && strcmp(argv[3], "stamps") == 0)
+        return run_stamps<0>(b) | run_stamps<1>(b) | run_stamps<2>(b) | run_stamps<0>(b);
     if (argc > 3 && strcmp(argv[3], "split") == 0)  // the slab's overlapped interior / edges
         return run_split(b, iters);
     if (argc > 3 && strcmp(argv[3], "triple") == 0)  // the product triple kernel (PMC runs)
