@@ -1,110 +1,69 @@
 // demons_kernels.hip — Thirion's / diffeomorphic Demons iteration for gfx950.
 //
-// DemonsThirions::get_update (src/regularization/Demons/DemonsThirions.cpp:18-42),
-// per iteration, in three passes over HBM:
-//   K1 demons_force_kernel   Iwar = warp2d(Imov, u) at the pixel and its four
-//                            neighbours (Image.cpp:119-182), dI = grad(Iwar),
-//                            It = Iwar - Iref (IterativeSolver.cpp:22-56),
+// DemonsThirions::get_update (src/regularization/Demons/DemonsThirions.cpp:18-42)
+// per iteration:
+//   K1 force                 Iwar = warp2d(Imov, u) (Image.cpp:119-182),
+//                            dI = grad(Iwar), It = Iwar - Iref
+//                            (IterativeSolver.cpp:22-56),
 //                            c = -dI*It / (|dI|^2 + It^2 si^2/sx^2) (Demons.cpp:34-63)
-//                            -> corr.  24 B/px + gathers.
-//   K2 smooth_compose_kernel corr <- corr (*) G(sigma_fluid)   (Field.tpp:209-269)
-//                            then u_mid = accumulate(u, corr)  (Motion.cpp:113-178)
-//                            or u + corr (Addition) -> u_mid.  24 B/px + gathers.
+//   K2 smooth + update       c <- c (*) G(sigma_fluid)   (Field.tpp:209-269)
+//                            then u_mid = accumulate(u, c) (Motion.cpp:113-178)
+//                            or u + c (Addition)
 //   K3 smooth_norm_kernel    u_new = u_mid (*) G(sigma_diffusion) plus the
 //                            Logger partials against u (prev).  24 B/px.
-// The Gaussian smoothing is the reference's DIRECT kw x kw convolution, staged
-// through LDS, with its exact semantics: a tap is valid iff its LINEAR index
-// lies in [0, N) (so taps past an x-edge wrap into the neighbouring j-line),
-// the sum runs ii (x) outer / jj (y) inner in fp32 with (float) weights, and
-// it is normalised by the fp64 sum of the valid weights cast to float.  A
-// separable form cannot reproduce that rounding; the direct form is still
-// HBM-bound at kw = 5 (25 LDS reads of 8 B per output pixel), so the exact
-// form is the one shipped.
+// K1 + K2 run as ONE kernel (demons_fused_kernel) on every tile whose
+// convolution taps stay inside the image's x range: the warped image and the
+// correction of the tile plus its halo live only in LDS, so the pass reads u,
+// Imov, Iref and writes u_mid (24 B/px) instead of 48 B/px through a corr
+// field.  The edge tile columns, whose taps wrap into the neighbouring j-line,
+// take the unfused force + smooth_compose kernels.
+// The Gaussian smoothing is the reference's DIRECT kw x kw convolution with
+// its exact semantics: a tap is valid iff its LINEAR index lies in [0, N) (so
+// taps past an x-edge wrap into the neighbouring j-line), the sum runs ii (x)
+// outer / jj (y) inner in fp32 with (float) weights, and it is normalised by
+// the fp64 sum of the valid weights cast to float.  A separable form cannot
+// reproduce that rounding, so the direct form is the one shipped; its x and y
+// components are summed as one packed pair (v_pk_mul_f32 + v_pk_add_f32 round
+// exactly like the scalar multiply and add).
 #include "of2d_device.h"
 
 namespace of2d {
 
 namespace {
 constexpr int kCx = 64;  // conv tile: 64 px wide
-constexpr int kCy = 16;  // 16 j-lines high (4 per thread row)
 constexpr int kCThreadsY = 4;
-static_assert(kCy / kCThreadsY == 4, "conv4 computes four j-lines per thread");
+// j-lines per thread of the product smoothing kernels (the tile is
+// kCThreadsY * kCr j-lines high): a taller tile loads fewer halo rows per
+// output and shares each LDS tap column between more outputs
+constexpr int kCr = 8;
+typedef float v2f __attribute__((ext_vector_type(2)));
 
-// warp2d value of Imov at pixel (a, b) with motion u (Image.cpp:137-174)
-__device__ __forceinline__ float warped_at(const float *__restrict__ Imov,
-                                           const float2 *__restrict__ u, int a, int b, int dimx,
-                                           int dimy, int P) {
-    const long idx = (long)b * P + a;
-    const float2 m = u[idx];
-    float out = Imov[idx];
-    const float px = (float)a + m.x;
-    const int dx = (int)floorf(px);
-    const float fx = px - (float)dx;
-    const float py = (float)b + m.y;
-    const int dy = (int)floorf(py);
-    const float fy = py - (float)dy;
-    if (!(dx < 0 || dx >= dimx || dy < 0 || dy >= dimy)) {
-        const float *q = Imov + (long)dy * P + dx;
-        float val = (q[0] * (1 - fx)) * (1 - fy);
-        float w = (1 - fx) * (1 - fy);
-        const bool ax = dx < dimx - 1, ay = dy < dimy - 1;
-        if (ax) {
-            val += (q[1] * fx) * (1 - fy);
-            w += fx * (1 - fy);
-        }
-        if (ay) {
-            val += (q[P] * (1 - fx)) * fy;
-            w += (1 - fx) * fy;
-        }
-        if (ax && ay) {
-            val += (q[P + 1] * fx) * fy;
-            w += fx * fy;
-        }
-        if (w != 0) out = val / w;
-    }
-    return out;
-}
-}  // namespace
-
-// Block: 64 x 4 threads, a 64 x kFy output tile (kFy/4 j-lines per thread).
-// The warped image is computed ONCE per pixel of the tile plus a one-pixel
-// halo into LDS (1.16 warps per output pixel instead of 5), then the central
-// differences, It and the force come from LDS.
-constexpr int kFy = 16;
-__global__ __launch_bounds__(256) void demons_force_kernel(
-    const float *__restrict__ Iref, const float *__restrict__ Imov, const float2 *__restrict__ u,
-    float2 *__restrict__ corr, int dimx, int dimy, int P, float sigma_isq, float sigma_xsq,
-    unsigned *__restrict__ status) {
-    constexpr int TW = 64 + 2, TH = kFy + 2;
-    __shared__ float w[TH][TW];
-    const int x0 = blockIdx.x * 64, y0 = blockIdx.y * kFy;
-    const int tid = threadIdx.y * 64 + threadIdx.x;
-    // warp the tile + halo, all loads of a thread's slots issued together
-    // (the same arithmetic as warped_at / Image.cpp:137-174)
-    constexpr int NS = (TW * TH + 255) / 256;
-    float2 m[NS];
-    float own[NS];
-    long idx[NS];
-    bool in[NS];
+// warp2d values of Imov at B pixels (a[q], b[q]) with motion u
+// (Image.cpp:137-174); in[q] = the pixel is valid and inside the image (res[q]
+// is meaningful only then).  Every load of the batch is issued before any is
+// used.
+template <int B>
+__device__ __forceinline__ void warp_batch(const float *__restrict__ Imov,
+                                           const float2 *__restrict__ u, const int a[B],
+                                           const int b[B], const bool valid[B], int dimx, int dimy,
+                                           int P, float res[B], bool in[B]) {
+    float2 m[B];
+    float own[B];
 #pragma unroll
-    for (int q = 0; q < NS; q++) {
-        const int s = tid + 256 * q, r = s / TW, c = s - r * TW;
-        const int a = x0 - 1 + c, b = y0 - 1 + r;
-        in[q] = s < TW * TH && a >= 0 && a < dimx && b >= 0 && b < dimy;
-        idx[q] = (long)b * P + a;
-        m[q] = in[q] ? u[idx[q]] : make_float2(0.0f, 0.0f);
-        own[q] = in[q] ? Imov[idx[q]] : 0.0f;
+    for (int q = 0; q < B; q++) {
+        in[q] = valid[q] && a[q] >= 0 && a[q] < dimx && b[q] >= 0 && b[q] < dimy;
+        const long idx = (long)b[q] * P + a[q];
+        m[q] = in[q] ? u[idx] : make_float2(0.0f, 0.0f);
+        own[q] = in[q] ? Imov[idx] : 0.0f;
     }
-    float t00[NS], t10[NS], t01[NS], t11[NS], fx[NS], fy[NS];
-    bool ok[NS], ax[NS], ay[NS];
+    float t00[B], t10[B], t01[B], t11[B], fx[B], fy[B];
+    bool ok[B], ax[B], ay[B];
 #pragma unroll
-    for (int q = 0; q < NS; q++) {
-        const int s = tid + 256 * q, r = s / TW, c = s - r * TW;
-        const int a = x0 - 1 + c, b = y0 - 1 + r;
-        const float px = (float)a + m[q].x;
+    for (int q = 0; q < B; q++) {
+        const float px = (float)a[q] + m[q].x;
         const int dx = (int)floorf(px);
         fx[q] = px - (float)dx;
-        const float py = (float)b + m[q].y;
+        const float py = (float)b[q] + m[q].y;
         const int dy = (int)floorf(py);
         fy[q] = py - (float)dy;
         ok[q] = in[q] && !(dx < 0 || dx >= dimx || dy < 0 || dy >= dimy);
@@ -117,9 +76,7 @@ __global__ __launch_bounds__(256) void demons_force_kernel(
         t11[q] = ok[q] && ax[q] && ay[q] ? g[P + 1] : 0.0f;
     }
 #pragma unroll
-    for (int q = 0; q < NS; q++) {
-        if (!in[q]) continue;
-        const int s = tid + 256 * q, r = s / TW, c = s - r * TW;
+    for (int q = 0; q < B; q++) {
         float out = own[q];
         if (ok[q]) {
             const float gx = fx[q], gy = fy[q];
@@ -139,7 +96,58 @@ __global__ __launch_bounds__(256) void demons_force_kernel(
             }
             if (wt != 0) out = val / wt;
         }
-        w[r][c] = out;
+        res[q] = out;
+    }
+}
+
+// Demons.cpp:57: dI * It / (dI.x^2 + dI.y^2 + It*It*sigma_isq/sigma_xsq) * -1
+__device__ __forceinline__ float2 demons_corr(float gx, float gy, float it, float sigma_isq,
+                                              float sigma_xsq, bool &zero) {
+    const float den = (gx * gx + gy * gy) + ((it * it) * sigma_isq) / sigma_xsq;
+    zero |= den == 0.0f;
+    return make_float2(((gx * it) / den) * -1.0f, ((gy * it) / den) * -1.0f);
+}
+
+// x tile of a launch over a subset of the tile columns: block columns
+// [0, ntl) are tiles [0, ntl), the others the last tiles of a gxt-tile row
+__device__ __forceinline__ int tile_x(int ntl, int gxt) {
+    const int b = (int)blockIdx.x;
+    return b < ntl ? b : gxt - ((int)gridDim.x - b);
+}
+}  // namespace
+
+// Block: 64 x 4 threads, a 64 x kFy output tile (kFy/4 j-lines per thread).
+// The warped image is computed ONCE per pixel of the tile plus a one-pixel
+// halo into LDS (1.16 warps per output pixel instead of 5), then the central
+// differences, It and the force come from LDS.
+constexpr int kFy = 16;
+__global__ __launch_bounds__(256) void demons_force_kernel(
+    const float *__restrict__ Iref, const float *__restrict__ Imov, const float2 *__restrict__ u,
+    float2 *__restrict__ corr, int dimx, int dimy, int P, float sigma_isq, float sigma_xsq,
+    unsigned *__restrict__ status, int ntl, int gxt) {
+    constexpr int TW = 64 + 2, TH = kFy + 2;
+    __shared__ float w[TH][TW];
+    const int x0 = tile_x(ntl, gxt) * 64, y0 = blockIdx.y * kFy;
+    const int tid = threadIdx.y * 64 + threadIdx.x;
+    // warp the tile + halo (slots outside the image are never read)
+    constexpr int NS = (TW * TH + 255) / 256;
+    {
+        int a[NS], b[NS];
+        bool valid[NS], in[NS];
+        float res[NS];
+#pragma unroll
+        for (int q = 0; q < NS; q++) {
+            const int s = tid + 256 * q, r = s / TW;
+            a[q] = x0 - 1 + (s - r * TW);
+            b[q] = y0 - 1 + r;
+            valid[q] = s < TW * TH;
+        }
+        warp_batch<NS>(Imov, u, a, b, valid, dimx, dimy, P, res, in);
+#pragma unroll
+        for (int q = 0; q < NS; q++) {
+            const int s = tid + 256 * q, r = s / TW;
+            if (in[q]) w[r][s - r * TW] = res[q];
+        }
     }
     __syncthreads();
     const int i = x0 + threadIdx.x;
@@ -166,11 +174,7 @@ __global__ __launch_bounds__(256) void demons_force_kernel(
         else
             gy = (w[r + 1][c] - w[r - 1][c]) / 2.0f;
         const long idx = (long)j * P + i;
-        const float it = w0 - Iref[idx];
-        // Demons.cpp:57: dI * It / (dI.x^2 + dI.y^2 + It*It*sigma_isq/sigma_xsq) * -1
-        const float den = (gx * gx + gy * gy) + ((it * it) * sigma_isq) / sigma_xsq;
-        zero |= den == 0.0f;
-        corr[idx] = make_float2(((gx * it) / den) * -1.0f, ((gy * it) / den) * -1.0f);
+        corr[idx] = demons_corr(gx, gy, w0 - Iref[idx], sigma_isq, sigma_xsq, zero);
     }
     if (zero) atomicOr(status, kStatusDivZero);
 }
@@ -178,17 +182,17 @@ __global__ __launch_bounds__(256) void demons_force_kernel(
 void launch_demons_force(const float *Iref, const float *Imov, const float2 *u, float2 *corr,
                          int dimx, int dimy, int P, float sigma_isq, float sigma_xsq,
                          unsigned *status, hipStream_t st) {
-    hipLaunchKernelGGL(demons_force_kernel, dim3((dimx + 63) / 64, (dimy + kFy - 1) / kFy),
-                       dim3(64, 4), 0, st, Iref, Imov, u, corr, dimx, dimy, P, sigma_isq,
-                       sigma_xsq, status);
+    const int gx = (dimx + 63) / 64;
+    hipLaunchKernelGGL(demons_force_kernel, dim3(gx, (dimy + kFy - 1) / kFy), dim3(64, 4), 0, st,
+                       Iref, Imov, u, corr, dimx, dimy, P, sigma_isq, sigma_xsq, status, gx, gx);
     OF2D_HIP(hipGetLastError());
 }
 
 // ------------------------------------------------------------------ convolution
-// One LDS tile of (kCx + 2cx) x (kCy + 2cy) float2 addressed by LINEAR index:
-// slot (r, c) holds field[L] with L = (y0 - cy + r) * dimx + (x0 - cx + c), the
-// reference's idx + ii*step.x + jj*step.y (Field.tpp:254), zero where L is
-// outside [0, N).
+// One LDS tile of (kCx + 2cx) x (kCThreadsY * R + 2cy) float2 addressed by
+// LINEAR index: slot (r, c) holds field[L] with L = (y0 - cy + r) * dimx +
+// (x0 - cx + c), the reference's idx + ii*step.x + jj*step.y (Field.tpp:254),
+// zero where L is outside [0, N).
 struct ConvArgs {
     const float *kf;   // (float) k[idxkernel], kw*kw, idx = (ii+cx) + (jj+cy)*kw
     const double *kd;  // k[idxkernel] as double (boundary weight sums)
@@ -196,19 +200,26 @@ struct ConvArgs {
     double wfull;  // sum of all weights in the reference's order (interior pixels)
 };
 
-template <int KW>
+template <int KW, int R = kCr>
 __device__ __forceinline__ void conv_load_tile(float2 *tile, const float2 *__restrict__ f,
                                                int dimx, int dimy, int P, int x0, int y0,
                                                int cx_rt, int cy_rt) {
+    constexpr int CY = kCThreadsY * R;  // tile height without the halo
     const int cx = KW > 0 ? (KW - 1) / 2 : cx_rt, cy = KW > 0 ? (KW - 1) / 2 : cy_rt;
-    const int TW = kCx + 2 * cx, TH = kCy + 2 * cy;
+    const int TW = kCx + 2 * cx, TH = CY + 2 * cy;
     const long N = (long)dimx * dimy;
     const int tid = threadIdx.y * 64 + threadIdx.x;
+    // x-interior tile (block-uniform): no tap column leaves [0, dimx), so L is
+    // in [0, N) iff its j-line is
+    const bool xin = x0 - cx >= 0 && x0 + kCx + cx <= dimx;
     // slot (r, c) <- f[L], L = row * dimx + col with col within cx of [0, dimx):
     // the j-line of L is row - 1, row or row + 1 (no 64-bit division)
     auto fetch = [&](int s) {
         const int r = s / TW, c = s - r * TW;
         int row = y0 - cy + r, col = x0 - cx + c;
+        if (xin)
+            return (unsigned)row < (unsigned)dimy ? f[(long)row * P + col]
+                                                  : make_float2(0.0f, 0.0f);
         while (col < 0) {  // once unless cx > dimx
             col += dimx;
             row -= 1;
@@ -222,7 +233,7 @@ __device__ __forceinline__ void conv_load_tile(float2 *tile, const float2 *__res
     };
     if constexpr (KW > 0) {
         // compile-time tile: every load of the thread in flight at once
-        constexpr int TWc = kCx + 2 * ((KW - 1) / 2), THc = kCy + 2 * ((KW - 1) / 2);
+        constexpr int TWc = kCx + 2 * ((KW - 1) / 2), THc = CY + 2 * ((KW - 1) / 2);
         constexpr int NS = (TWc * THc + 255) / 256;
         float2 v[NS];
 #pragma unroll
@@ -285,138 +296,142 @@ __device__ __forceinline__ bool conv_px(const float2 *tile, const ConvArgs &a, i
     return true;
 }
 
-// The convolution at four consecutive j-lines j0..j0+3 of column i.  When the
-// width is known and all four pixels are interior, the 4 + 2c tile values of
-// each tap column are read once and shared by the four outputs (each output
-// still sums ii outer / jj inner, the reference's order); otherwise per pixel.
-template <int KW>
-__device__ __forceinline__ void conv4(const float2 *tile, const ConvArgs &a, int i, int j0,
-                                      int tx, int ty0, int dimx, int dimy, long N, float2 res[4],
-                                      bool has[4]) {
+// The convolution at R consecutive j-lines j0..j0+R-1 of column i.  When the
+// width is known and all R pixels are interior, the R + 2c tile values of
+// each tap column are read once and shared by the R outputs (each output
+// still sums ii outer / jj inner, the reference's order), x and y as one
+// packed pair (PK) or as two scalars; otherwise per pixel.
+template <int KW, int R, bool PK>
+__device__ __forceinline__ void convR(const float2 *tile, const ConvArgs &a, int i, int j0,
+                                      int tx, int ty0, int dimx, int dimy, long N, float2 res[R],
+                                      bool has[R]) {
     if constexpr (KW > 0) {
         constexpr int c = (KW - 1) / 2, TW = kCx + 2 * c;
-        const long lin0 = (long)j0 * dimx + i, lin3 = (long)(j0 + 3) * dimx + i;
-        if (j0 + 3 < dimy && lin0 - c - (long)c * dimx >= 0 && lin3 + c + (long)c * dimx < N) {
-            float vx[4] = {0.0f, 0.0f, 0.0f, 0.0f}, vy[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+        const long lin0 = (long)j0 * dimx + i, linl = (long)(j0 + R - 1) * dimx + i;
+        if (j0 + R - 1 < dimy && lin0 - c - (long)c * dimx >= 0 && linl + c + (long)c * dimx < N) {
+            v2f acc[R];
+#pragma unroll
+            for (int k = 0; k < R; k++) acc[k] = v2f{0.0f, 0.0f};
 #pragma unroll
             for (int ii = -c; ii <= c; ii++) {
-                float2 col[4 + 2 * c];
+                v2f col[R + 2 * c];
 #pragma unroll
-                for (int q = 0; q < 4 + 2 * c; q++) col[q] = tile[(ty0 + q) * TW + (tx + c + ii)];
+                for (int q = 0; q < R + 2 * c; q++) {
+                    const float2 t = tile[(ty0 + q) * TW + (tx + c + ii)];
+                    col[q] = v2f{t.x, t.y};
+                }
 #pragma unroll
-                for (int k = 0; k < 4; k++)
+                for (int k = 0; k < R; k++)
 #pragma unroll
                     for (int jj = -c; jj <= c; jj++) {
                         const float kk = a.kf[(ii + c) + (jj + c) * KW];
-                        vx[k] = vx[k] + col[k + c + jj].x * kk;
-                        vy[k] = vy[k] + col[k + c + jj].y * kk;
+                        if constexpr (PK) {
+                            acc[k] = acc[k] + col[k + c + jj] * v2f{kk, kk};
+                        } else {
+                            acc[k].x = acc[k].x + col[k + c + jj].x * kk;
+                            acc[k].y = acc[k].y + col[k + c + jj].y * kk;
+                        }
                     }
             }
             const float wf = (float)a.wfull;
 #pragma unroll
-            for (int k = 0; k < 4; k++) {
+            for (int k = 0; k < R; k++) {
                 has[k] = a.wfull != 0;
-                res[k] = make_float2(vx[k] / wf, vy[k] / wf);
+                res[k] = make_float2(acc[k].x / wf, acc[k].y / wf);
             }
             return;
         }
     }
 #pragma unroll
-    for (int k = 0; k < 4; k++) {
+    for (int k = 0; k < R; k++) {
         has[k] = false;
         if (j0 + k < dimy) has[k] = conv_px<KW>(tile, a, i, j0 + k, tx, ty0 + k, dimx, N, res[k]);
     }
 }
 
-// mode 0: Composition (Motion::accumulate), 1: Addition (Field::operator+=),
-// 2: neither (DemonsThirions.cpp:33-38 with another value), 3: store corr only
-template <int KW>
-__global__ __launch_bounds__(256) void smooth_compose_kernel(
-    const float2 *__restrict__ corr, const float2 *__restrict__ u, float2 *__restrict__ out,
-    int dimx, int dimy, int P, ConvArgs a, int mode) {
-    extern __shared__ __attribute__((aligned(16))) float2 tile[];
-    const int x0 = blockIdx.x * kCx, y0 = blockIdx.y * kCy;
-    conv_load_tile<KW>(tile, corr, dimx, dimy, P, x0, y0, a.cx, a.cy);
-    __syncthreads();
-    const long N = (long)dimx * dimy;
-    const int i = x0 + threadIdx.x;
-    if (i >= dimx) return;
-    // four consecutive j-lines per thread; the wave index is uniform
-    const int r0 = (int)__builtin_amdgcn_readfirstlane(threadIdx.y) * (kCy / kCThreadsY);
-    float2 sm[4];
-    bool has[4];
-    conv4<KW>(tile, a, i, y0 + r0, threadIdx.x, r0, dimx, dimy, N, sm, has);
-    float2 cv[4];
+// Motion::accumulate (Motion.cpp:113-178) at pixels (i, j0..j0+G-1) with
+// increments cv: u(x) <- c(x) + u_old(x + c(x)), bilinear with in-range taps
+// renormalised; out of range keeps u_old(x).  Every gather of the G pixels is
+// issued before any is used.
+template <int G>
+__device__ __forceinline__ void compose_px(const float2 *__restrict__ u, int i, int j0, int dimx,
+                                           int dimy, int P, const float2 cv[G], float2 o[G]) {
+    float2 own[G], t00[G], t10[G], t01[G], t11[G];
+    float fx[G], fy[G];
+    bool ok[G], ax[G], ay[G];
 #pragma unroll
-    for (int k = 0; k < 4; k++) {
-        const int j = y0 + r0 + k;
-        cv[k] = make_float2(0.0f, 0.0f);
-        if (j < dimy) cv[k] = has[k] ? sm[k] : corr[(long)j * P + i];
+    for (int k = 0; k < G; k++) {
+        const int j = j0 + k;
+        const bool in = j < dimy;
+        own[k] = in ? u[(long)j * P + i] : make_float2(0.0f, 0.0f);
+        const float px = (float)i + cv[k].x;
+        const int dx = (int)floorf(px);
+        fx[k] = px - (float)dx;
+        const float py = (float)j + cv[k].y;
+        const int dy = (int)floorf(py);
+        fy[k] = py - (float)dy;
+        ok[k] = in && !(dx < 0 || dx >= dimx || dy < 0 || dy >= dimy);
+        ax[k] = dx < dimx - 1;
+        ay[k] = dy < dimy - 1;
+        const float2 *b = u + (long)dy * P + dx;
+        const float2 z = make_float2(0.0f, 0.0f);
+        t00[k] = ok[k] ? b[0] : z;
+        t10[k] = ok[k] && ax[k] ? b[1] : z;
+        t01[k] = ok[k] && ay[k] ? b[P] : z;
+        t11[k] = ok[k] && ax[k] && ay[k] ? b[P + 1] : z;
     }
-    if (mode == 0) {
-        // Motion::accumulate (Motion.cpp:113-178): u(x) <- c(x) + u_old(x + c(x)),
-        // bilinear with in-range taps renormalised; out of range keeps u_old(x).
-        // All gathers of the four pixels are issued before any is used.
-        float2 own[4], t00[4], t10[4], t01[4], t11[4];
-        float fx[4], fy[4];
-        bool ok[4], ax[4], ay[4];
 #pragma unroll
-        for (int k = 0; k < 4; k++) {
-            const int j = y0 + r0 + k;
-            const bool in = j < dimy;
-            own[k] = in ? u[(long)j * P + i] : make_float2(0.0f, 0.0f);
-            const float px = (float)i + cv[k].x;
-            const int dx = (int)floorf(px);
-            fx[k] = px - (float)dx;
-            const float py = (float)j + cv[k].y;
-            const int dy = (int)floorf(py);
-            fy[k] = py - (float)dy;
-            ok[k] = in && !(dx < 0 || dx >= dimx || dy < 0 || dy >= dimy);
-            ax[k] = dx < dimx - 1;
-            ay[k] = dy < dimy - 1;
-            const float2 *b = u + (long)dy * P + dx;
-            const float2 z = make_float2(0.0f, 0.0f);
-            t00[k] = ok[k] ? b[0] : z;
-            t10[k] = ok[k] && ax[k] ? b[1] : z;
-            t01[k] = ok[k] && ay[k] ? b[P] : z;
-            t11[k] = ok[k] && ax[k] && ay[k] ? b[P + 1] : z;
-        }
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            const int j = y0 + r0 + k;
-            if (j >= dimy) break;
-            const float2 c = cv[k];
-            float2 o = own[k];
-            if (ok[k]) {
-                o = c;
-                const float gx = fx[k], gy = fy[k];
-                float vx = (t00[k].x * (1 - gx)) * (1 - gy);
-                float vy = (t00[k].y * (1 - gx)) * (1 - gy);
-                float w = (1 - gx) * (1 - gy);
-                if (ax[k]) {
-                    vx = vx + (t10[k].x * gx) * (1 - gy);
-                    vy = vy + (t10[k].y * gx) * (1 - gy);
-                    w += gx * (1 - gy);
-                }
-                if (ay[k]) {
-                    vx = vx + (t01[k].x * (1 - gx)) * gy;
-                    vy = vy + (t01[k].y * (1 - gx)) * gy;
-                    w += (1 - gx) * gy;
-                }
-                if (ax[k] && ay[k]) {
-                    vx = vx + (t11[k].x * gx) * gy;
-                    vy = vy + (t11[k].y * gx) * gy;
-                    w += gx * gy;
-                }
-                if (w != 0) o = make_float2(c.x + vx / w, c.y + vy / w);
+    for (int k = 0; k < G; k++) {
+        const float2 c = cv[k];
+        o[k] = own[k];
+        if (ok[k]) {
+            o[k] = c;
+            const float gx = fx[k], gy = fy[k];
+            const v2f wx0 = v2f{1 - gx, 1 - gx}, wx1 = v2f{gx, gx};
+            const v2f wy0 = v2f{1 - gy, 1 - gy}, wy1 = v2f{gy, gy};
+            // (t * wx) * wy per component, added in the reference's tap order
+            v2f v = (v2f{t00[k].x, t00[k].y} * wx0) * wy0;
+            float w = (1 - gx) * (1 - gy);
+            if (ax[k]) {
+                v = v + (v2f{t10[k].x, t10[k].y} * wx1) * wy0;
+                w += gx * (1 - gy);
             }
-            out[(long)j * P + i] = o;
+            if (ay[k]) {
+                v = v + (v2f{t01[k].x, t01[k].y} * wx0) * wy1;
+                w += (1 - gx) * gy;
+            }
+            if (ax[k] && ay[k]) {
+                v = v + (v2f{t11[k].x, t11[k].y} * wx1) * wy1;
+                w += gx * gy;
+            }
+            if (w != 0) o[k] = make_float2(c.x + v.x / w, c.y + v.y / w);
+        }
+    }
+}
+
+// the motion update of DemonsThirions.cpp:33-38 at (i, j0..j0+R-1) from the
+// smoothed correction cv.  mode 0: Composition (Motion::accumulate), 1:
+// Addition (Field::operator+=), 2: neither (another enum value), 3: store the
+// smoothed correction itself (diffeomorphic: exp and compose follow)
+template <int R>
+__device__ __forceinline__ void store_update(const float2 *__restrict__ u,
+                                             float2 *__restrict__ out, int i, int j0, int dimx,
+                                             int dimy, int P, const float2 cv[R], int mode) {
+    static_assert(R % 4 == 0, "compose batches of four");
+    if (mode == 0) {
+#pragma unroll
+        for (int h = 0; h < R; h += 4) {
+            float2 o[4];
+            compose_px<4>(u, i, j0 + h, dimx, dimy, P, cv + h, o);
+#pragma unroll
+            for (int k = 0; k < 4; k++)
+                if (j0 + h + k < dimy) out[(long)(j0 + h + k) * P + i] = o[k];
         }
         return;
     }
 #pragma unroll
-    for (int k = 0; k < 4; k++) {
-        const int j = y0 + r0 + k;
+    for (int k = 0; k < R; k++) {
+        const int j = j0 + k;
         if (j >= dimy) break;
         const long idx = (long)j * P + i;
         const float2 c = cv[k];
@@ -433,28 +448,159 @@ __global__ __launch_bounds__(256) void smooth_compose_kernel(
     }
 }
 
+// K2 from a correction field in HBM: smoothing + motion update (store_update)
+template <int KW, int R = kCr, bool PK = true>
+__global__ __launch_bounds__(256) void smooth_compose_kernel(
+    const float2 *__restrict__ corr, const float2 *__restrict__ u, float2 *__restrict__ out,
+    int dimx, int dimy, int P, ConvArgs a, int mode, int ntl, int gxt) {
+    extern __shared__ __attribute__((aligned(16))) float2 tile[];
+    constexpr int CY = kCThreadsY * R;
+    const int x0 = tile_x(ntl, gxt) * kCx, y0 = blockIdx.y * CY;
+    conv_load_tile<KW, R>(tile, corr, dimx, dimy, P, x0, y0, a.cx, a.cy);
+    __syncthreads();
+    const long N = (long)dimx * dimy;
+    const int i = x0 + threadIdx.x;
+    if (i >= dimx) return;
+    // R consecutive j-lines per thread; the wave index is uniform
+    const int r0 = (int)__builtin_amdgcn_readfirstlane(threadIdx.y) * R;
+    float2 sm[R];
+    bool has[R];
+    convR<KW, R, PK>(tile, a, i, y0 + r0, threadIdx.x, r0, dimx, dimy, N, sm, has);
+    float2 cv[R];
+#pragma unroll
+    for (int k = 0; k < R; k++) {
+        const int j = y0 + r0 + k;
+        cv[k] = make_float2(0.0f, 0.0f);
+        if (j < dimy) cv[k] = has[k] ? sm[k] : corr[(long)j * P + i];
+    }
+    store_update<R>(u, out, i, y0 + r0, dimx, dimy, P, cv, mode);
+}
+
+// K1 + K2 for an x-interior tile (x0 - c >= 0, x0 + 64 + c <= dimx: no tap
+// wraps into another j-line).  1. the warped image over the tile plus a
+// (c + 1)-pixel halo into LDS; 2. the correction over the tile plus a c-pixel
+// halo into LDS (the halo is recomputed by the neighbouring tiles); 3. the
+// sigma_fluid convolution and the motion update.  Per pixel the arithmetic of
+// demons_force_kernel + smooth_compose_kernel: bit-identical.
+template <int KW, int R>
+__global__ __launch_bounds__(256) void demons_fused_kernel(
+    const float *__restrict__ Iref, const float *__restrict__ Imov, const float2 *__restrict__ u,
+    float2 *__restrict__ out, int dimx, int dimy, int P, float sigma_isq, float sigma_xsq,
+    ConvArgs ca, int mode, unsigned *__restrict__ status, int bx0) {
+    constexpr int c = (KW - 1) / 2;
+    constexpr int CY = kCThreadsY * R;
+    constexpr int CW = kCx + 2 * c, CH = CY + 2 * c;  // correction tile
+    constexpr int WW = CW + 2, WH = CH + 2;           // warped-image tile
+    __shared__ float wt[WH * WW];
+    __shared__ __attribute__((aligned(16))) float2 ct[CH * CW];
+    const int x0 = ((int)blockIdx.x + bx0) * kCx, y0 = blockIdx.y * CY;
+    const int tid = threadIdx.y * 64 + threadIdx.x;
+    {
+        // 1. slot s <-> pixel (x0 - c - 1 + s % WW, y0 - c - 1 + s / WW), in
+        // batches of BW slots per thread
+        constexpr int NW = (WW * WH + 255) / 256, BW = 6;
+#pragma unroll
+        for (int q0 = 0; q0 < NW; q0 += BW) {
+            int a[BW], b[BW];
+            bool valid[BW], in[BW];
+            float res[BW];
+#pragma unroll
+            for (int q = 0; q < BW; q++) {
+                const int s = tid + 256 * (q0 + q), r = s / WW;
+                a[q] = x0 - c - 1 + (s - r * WW);
+                b[q] = y0 - c - 1 + r;
+                valid[q] = q0 + q < NW && s < WW * WH;
+            }
+            warp_batch<BW>(Imov, u, a, b, valid, dimx, dimy, P, res, in);
+#pragma unroll
+            for (int q = 0; q < BW; q++)
+                if (valid[q]) wt[tid + 256 * (q0 + q)] = in[q] ? res[q] : 0.0f;
+        }
+    }
+    // Iref of the correction slots, loaded while the warp tile completes
+    constexpr int NC = (CW * CH + 255) / 256;
+    float iref[NC];
+#pragma unroll
+    for (int q = 0; q < NC; q++) {
+        const int s = tid + 256 * q, r = s / CW;
+        const int i = x0 - c + (s - r * CW), j = y0 - c + r;
+        iref[q] = (s < CW * CH && (unsigned)j < (unsigned)dimy) ? Iref[(long)j * P + i] : 0.0f;
+    }
+    __syncthreads();
+    {
+        // 2. slot s <-> pixel (x0 - c + s % CW, y0 - c + s / CW); j-lines
+        // outside the image hold 0 (their linear index is outside [0, N))
+        bool zero = false;
+#pragma unroll
+        for (int q = 0; q < NC; q++) {
+            const int s = tid + 256 * q;
+            if (s < CW * CH) {
+                const int r = s / CW, cc = s - r * CW;
+                const int i = x0 - c + cc, j = y0 - c + r;
+                float2 cv = make_float2(0.0f, 0.0f);
+                if ((unsigned)j < (unsigned)dimy) {
+                    const float *w = wt + (r + 1) * WW + (cc + 1);
+                    const float w0 = w[0];
+                    float gx, gy;
+                    if (i == 0)
+                        gx = w[1] - w0;
+                    else if (i == dimx - 1)
+                        gx = w0 - w[-1];
+                    else
+                        gx = (w[1] - w[-1]) / 2.0f;
+                    if (j == 0)
+                        gy = w[WW] - w0;
+                    else if (j == dimy - 1)
+                        gy = w0 - w[-WW];
+                    else
+                        gy = (w[WW] - w[-WW]) / 2.0f;
+                    cv = demons_corr(gx, gy, w0 - iref[q], sigma_isq, sigma_xsq, zero);
+                }
+                ct[s] = cv;
+            }
+        }
+        if (zero) atomicOr(status, kStatusDivZero);
+    }
+    __syncthreads();
+    // 3. R consecutive j-lines per thread (every column is inside the image)
+    const long N = (long)dimx * dimy;
+    const int i = x0 + threadIdx.x;
+    const int r0 = (int)__builtin_amdgcn_readfirstlane(threadIdx.y) * R;
+    float2 sm[R];
+    bool has[R];
+    convR<KW, R, true>(ct, ca, i, y0 + r0, threadIdx.x, r0, dimx, dimy, N, sm, has);
+    float2 cv[R];
+#pragma unroll
+    for (int k = 0; k < R; k++) {
+        cv[k] = make_float2(0.0f, 0.0f);
+        if (y0 + r0 + k < dimy) cv[k] = has[k] ? sm[k] : ct[(r0 + k + c) * CW + threadIdx.x + c];
+    }
+    store_update<R>(u, out, i, y0 + r0, dimx, dimy, P, cv, mode);
+}
+
 // u_new = u_mid (*) G(sigma_diffusion); Logger partials sum ||u_new - prev||,
 // sum ||prev|| per block (fixed order)
-template <int KW>
+template <int KW, int R = kCr, bool PK = true>
 __global__ __launch_bounds__(256) void smooth_norm_kernel(const float2 *__restrict__ umid,
                                                           const float2 *__restrict__ prev,
                                                           float2 *__restrict__ out, int dimx,
                                                           int dimy, int P, ConvArgs a,
                                                           double *__restrict__ partial) {
     extern __shared__ __attribute__((aligned(16))) float2 tile[];
-    const int x0 = blockIdx.x * kCx, y0 = blockIdx.y * kCy;
-    conv_load_tile<KW>(tile, umid, dimx, dimy, P, x0, y0, a.cx, a.cy);
+    constexpr int CY = kCThreadsY * R;
+    const int x0 = blockIdx.x * kCx, y0 = blockIdx.y * CY;
+    conv_load_tile<KW, R>(tile, umid, dimx, dimy, P, x0, y0, a.cx, a.cy);
     __syncthreads();
     const long N = (long)dimx * dimy;
     const int i = x0 + threadIdx.x;
     double sd = 0.0, sp = 0.0;
     if (i < dimx) {
-        const int r0 = (int)__builtin_amdgcn_readfirstlane(threadIdx.y) * (kCy / kCThreadsY);
-        float2 sm[4];
-        bool has[4];
-        conv4<KW>(tile, a, i, y0 + r0, threadIdx.x, r0, dimx, dimy, N, sm, has);
+        const int r0 = (int)__builtin_amdgcn_readfirstlane(threadIdx.y) * R;
+        float2 sm[R];
+        bool has[R];
+        convR<KW, R, PK>(tile, a, i, y0 + r0, threadIdx.x, r0, dimx, dimy, N, sm, has);
 #pragma unroll
-        for (int k = 0; k < 4; k++) {
+        for (int k = 0; k < R; k++) {
             const int j = y0 + r0 + k;
             if (j >= dimy) break;
             const long idx = (long)j * P + i;
@@ -484,29 +630,88 @@ __global__ __launch_bounds__(256) void smooth_norm_kernel(const float2 *__restri
     }
 }
 
-inline size_t conv_lds_bytes(int cx, int cy) {
-    return sizeof(float2) * (size_t)(kCx + 2 * cx) * (kCy + 2 * cy);
+inline size_t conv_lds_bytes(int cx, int cy, int R = kCr) {
+    return sizeof(float2) * (size_t)(kCx + 2 * cx) * (kCThreadsY * R + 2 * cy);
 }
-dim3 conv_grid(int dimx, int dimy) { return dim3((dimx + kCx - 1) / kCx, (dimy + kCy - 1) / kCy); }
+inline dim3 conv_grid_r(int dimx, int dimy, int R) {
+    return dim3((dimx + kCx - 1) / kCx, (dimy + kCThreadsY * R - 1) / (kCThreadsY * R));
+}
+dim3 conv_grid(int dimx, int dimy) { return conv_grid_r(dimx, dimy, kCr); }
 int conv_nblocks(int dimx, int dimy) {
     const dim3 g = conv_grid(dimx, dimy);
     return int(g.x * g.y);
 }
 
-void launch_smooth_compose(const float2 *corr, const float2 *u, float2 *out, int dimx, int dimy,
-                           int P, const float *kf, const double *kd, int kw, double wfull,
-                           int mode, hipStream_t st) {
-    const int c = (kw - 1) / 2;
-    ConvArgs a{kf, kd, kw, c, c, wfull};
+namespace {
+// smooth_compose over `gridx` block columns: tiles [0, ntl) and the last
+// gridx - ntl tiles of the gxt-tile row
+void smooth_compose_tiles(const float2 *corr, const float2 *u, float2 *out, int dimx, int dimy,
+                          int P, const ConvArgs &a, int mode, int gridx, int ntl, int gxt,
+                          hipStream_t st) {
+    const dim3 g(gridx, conv_grid(dimx, dimy).y);
     auto go = [&](auto kern) {
-        hipLaunchKernelGGL(kern, conv_grid(dimx, dimy), dim3(64, kCThreadsY),
-                           conv_lds_bytes(c, c), st, corr, u, out, dimx, dimy, P, a, mode);
+        hipLaunchKernelGGL(kern, g, dim3(64, kCThreadsY), conv_lds_bytes(a.cx, a.cy), st, corr, u,
+                           out, dimx, dimy, P, a, mode, ntl, gxt);
     };
-    switch (kw) {
+    switch (a.kw) {
         case 3: go(smooth_compose_kernel<3>); break;
         case 5: go(smooth_compose_kernel<5>); break;
         case 7: go(smooth_compose_kernel<7>); break;
         default: go(smooth_compose_kernel<0>); break;
+    }
+    OF2D_HIP(hipGetLastError());
+}
+}  // namespace
+
+void launch_smooth_compose(const float2 *corr, const float2 *u, float2 *out, int dimx, int dimy,
+                           int P, const float *kf, const double *kd, int kw, double wfull,
+                           int mode, hipStream_t st) {
+    const int c = (kw - 1) / 2;
+    const ConvArgs a{kf, kd, kw, c, c, wfull};
+    const int gx = conv_grid(dimx, dimy).x;
+    smooth_compose_tiles(corr, u, out, dimx, dimy, P, a, mode, gx, gx, gx, st);
+}
+
+int demons_edge_tiles(int dimx, int kw, int *nl, int *nr) {
+    const int c = (kw - 1) / 2, gx = (dimx + kCx - 1) / kCx;
+    int l = 0, r = 0;
+    while (l < gx && kCx * l - c < 0) l++;
+    while (r < gx - l && kCx * (gx - 1 - r) + kCx + c > dimx) r++;
+    if (nl) *nl = l;
+    if (nr) *nr = r;
+    return gx - l - r;  // x-interior tiles
+}
+
+void launch_demons_update(const float *Iref, const float *Imov, const float2 *u, float2 *corr,
+                          float2 *out, int dimx, int dimy, int P, float sigma_isq,
+                          float sigma_xsq, const float *kf, const double *kd, int kw,
+                          double wfull, int mode, unsigned *status, hipStream_t st) {
+    const int c = (kw - 1) / 2;
+    const ConvArgs a{kf, kd, kw, c, c, wfull};
+    int nl = 0, nr = 0;
+    const int ni = demons_edge_tiles(dimx, kw, &nl, &nr);
+    const int gx = (dimx + kCx - 1) / kCx;
+    if (!(kw == 3 || kw == 5 || kw == 7) || ni < 2) {
+        launch_demons_force(Iref, Imov, u, corr, dimx, dimy, P, sigma_isq, sigma_xsq, status, st);
+        smooth_compose_tiles(corr, u, out, dimx, dimy, P, a, mode, gx, gx, gx, st);
+        return;
+    }
+    // the correction the edge tiles' convolutions read: tile columns
+    // [0, nl + 1) and [gx - nr - 1, gx) (wrapped taps reach the far edge)
+    hipLaunchKernelGGL(demons_force_kernel, dim3(nl + nr + 2, (dimy + kFy - 1) / kFy), dim3(64, 4),
+                       0, st, Iref, Imov, u, corr, dimx, dimy, P, sigma_isq, sigma_xsq, status,
+                       nl + 1, gx);
+    OF2D_HIP(hipGetLastError());
+    smooth_compose_tiles(corr, u, out, dimx, dimy, P, a, mode, nl + nr, nl, gx, st);
+    const dim3 g(ni, conv_grid(dimx, dimy).y);
+    auto go = [&](auto kern) {
+        hipLaunchKernelGGL(kern, g, dim3(64, kCThreadsY), 0, st, Iref, Imov, u, out, dimx, dimy, P,
+                           sigma_isq, sigma_xsq, a, mode, status, nl);
+    };
+    switch (kw) {
+        case 3: go(demons_fused_kernel<3, kCr>); break;
+        case 5: go(demons_fused_kernel<5, kCr>); break;
+        default: go(demons_fused_kernel<7, kCr>); break;
     }
     OF2D_HIP(hipGetLastError());
 }

@@ -551,8 +551,10 @@ __device__ __forceinline__ void progress_prio(int done, int total) {
     }
 }
 
+// DIAG (tuning harness only): 1 skips the Logger magnitudes, to price them;
+// 2 loads the gradients non-temporally too (Infinity Cache residency probe)
 template <int ROWS, int WAVES, bool XCD = true, int MINB = 1, int UNR = 4, bool FD = true,
-          int PRIO = 0>
+          int PRIO = 0, int DIAG = 0>
 __global__ __launch_bounds__(64 * WAVES, MINB) void jacobi3_kernel(
     const float2 *__restrict__ uo, float2 *__restrict__ un, const float2 *__restrict__ dI,
     const float *__restrict__ It, int P, int dimx, int nrows, int row0, int dimy, float alphasq,
@@ -598,8 +600,8 @@ __global__ __launch_bounds__(64 * WAVES, MINB) void jacobi3_kernel(
     const bool grange = FD && range_flag && *range_flag == 0;
     auto ldg = [&](int j) {
         G r;
-        r.g = load_row<2, false>(dI + (long)cl(j) * P, xl);
-        const float2 tt = *reinterpret_cast<const float2 *>(It + (long)cl(j) * P + xl);
+        r.g = load_row<2, DIAG == 2>(dI + (long)cl(j) * P, xl);
+        const float2 tt = ld2<DIAG == 2>(reinterpret_cast<const float2 *>(It + (long)cl(j) * P + xl));
         r.t[0] = tt.x;
         r.t[1] = tt.y;
 #pragma unroll
@@ -692,9 +694,11 @@ __global__ __launch_bounds__(64 * WAVES, MINB) void jacobi3_kernel(
             const Row<2> wj1 = stepr(j + 1, vj, vj1, vj2, gj1, b1);  // u2 row j+1
             const Row<2> z = stepr(j, wm1, wj, wj1, gj, b3);         // u3 row j
             if (own) {
-                norms(vj, uj, s1d, s1p);
-                norms(wj, vj, s2d, s2p);
-                norms(z, wj, s3d, s3p);
+                if constexpr (DIAG != 1) {
+                    norms(vj, uj, s1d, s1p);
+                    norms(wj, vj, s2d, s2p);
+                    norms(z, wj, s3d, s3p);
+                }
                 bad |= b3;  // the denominator depends on dI only: one test per pixel
                 float2 *dst = un + (long)j * P + x;
                 if (x + 2 <= dimx)

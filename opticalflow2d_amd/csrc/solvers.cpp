@@ -124,16 +124,14 @@ int Registration::loop_demons(Level &L, int niter, int &final_buf) {
     return run_chunked(
         L, niter, nb,
         [&](const float2 *src, float2 *dst, double *partial) {
-            launch_demons_force(L.Iref.p, L.Iaux.p, src, L.corr.p, L.dx, L.dy, L.P, sigma_isq,
-                                sigma_xsq, d_status_, st_);
+            // force, correspondence->convolute and the motion update in one
+            // pass over the x-interior tiles (diffeomorphic: the smoothed
+            // correspondence itself, then exp() and motion->accumulate)
+            launch_demons_update(L.Iref.p, L.Iaux.p, src, L.corr.p, L.tmp.p, L.dx, L.dy, L.P,
+                                 sigma_isq, sigma_xsq, K.kf, K.kd, kw, K.wfull_fluid,
+                                 diffeo ? 3 : mode, d_status_, st_);
             const float2 *umid = L.tmp.p;
-            if (!diffeo) {
-                launch_smooth_compose(L.corr.p, src, L.tmp.p, L.dx, L.dy, L.P, K.kf, K.kd, kw,
-                                      K.wfull_fluid, mode, st_);
-            } else {
-                // correspondence->convolute; correspondence->exp(); motion->accumulate
-                launch_smooth_compose(L.corr.p, src, L.tmp.p, L.dx, L.dy, L.P, K.kf, K.kd, kw,
-                                      K.wfull_fluid, 3, st_);
+            if (diffeo) {
                 float2 *cexp = nullptr;
                 launch_motion_exp(L.tmp.p, L.force.p, L.dx, L.dy, L.P, nsq_max, d_scalar_ + 16,
                                   nparts, reinterpret_cast<int *>(d_scalar_), d_scalar_ + 1,

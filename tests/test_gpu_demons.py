@@ -48,6 +48,30 @@ def test_thirion_kernel_widths_and_accumulation(gpu, oracle, kw, accum):
     assert np.array_equal(g["warped"], w["warped"])
 
 
+@pytest.mark.parametrize("nx,kw,accum", [(321, 5, 0), (387, 7, 0), (388, 3, 1), (450, 5, 2)])
+def test_thirion_fused_tiles(gpu, oracle, nx, kw, accum):
+    """Widths at which the fused force + smoothing + update kernel runs on the
+    x-interior tiles and the edge tile columns take the unfused kernels: two
+    right edge columns (321: the last tile holds one column, so the tile before
+    it also reaches past dimx), one (387, 388, 450), every accumulation mode."""
+    ref, mov = S.texture_pair(nx, seed=nx + kw, ny=150)
+    params = [1.0, 0.25, 1.5, 2.5, kw, accum]
+    g, w = both(oracle, (nx, 150), [6], 0, 3, params, 1, ref, mov, fixed_iters=1)
+    assert g["iters"] == w["iters"]
+    assert np.array_equal(g["motion"], w["motion"])
+    assert np.array_equal(g["warped"], w["warped"])
+
+
+def test_diffeomorphic_demons_fused_tiles(gpu, oracle):
+    """Diffeomorphic Demons on a grid wide enough for the fused update (mode 3:
+    the smoothed correction itself, then exp and composition)."""
+    ref, mov = S.texture_pair(330, seed=9, ny=120)
+    g, w = both(oracle, (330, 120), [5], 0, 4, [1.0, 2.0, 1.0, 1.0, 5], 1, ref, mov * 3.0,
+                fixed_iters=1)
+    assert g["iters"] == w["iters"]
+    assert np.array_equal(g["motion"], w["motion"])
+
+
 def test_thirion_pyramid_refine(gpu, oracle):
     ref, mov = S.texture_pair(128, seed=4, ny=96)
     g, w = both(oracle, (128, 96), [15, 10], 1, 3, [1.0, 0.25, 2.0, 2.0, 5, 0], 2, ref, mov)

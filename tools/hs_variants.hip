@@ -446,14 +446,14 @@ int run_stamps(const Bufs &b) {
 
 // Back-to-back launches of the product triple kernel with the progress
 // priority schemes, interleaved in rounds so clock drift hits all alike.
-template <int PRIO>
+template <int PRIO, int DIAG = 0>
 float time_prio(const Bufs &b, int nl) {
     using namespace of2d::hs;
     const int gx = (b.dimx + kHs3Out - 1) / kHs3Out;
     const int r = hs3_rows(b.dimx, b.dimy);
     const int gy = (b.dimy + 4 * r - 1) / (4 * r);
     const int nblk = 8 * ((gx * gy + 7) / 8);
-    auto k = jacobi3_kernel<0, 4, true, 4, 4, true, PRIO>;
+    auto k = jacobi3_kernel<0, 4, true, 4, 4, true, PRIO, DIAG>;
     double *p2 = b.partial + 2 * 16384, *p3 = b.partial + 4 * 16384;
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
@@ -477,16 +477,17 @@ float time_prio(const Bufs &b, int nl) {
 }
 
 int run_prio(const Bufs &b) {
-    const char *names[] = {"prio0", "prio1", "prio2", "prio3", "prio4"};
-    std::vector<std::vector<float>> t(5);
+    const char *names[] = {"prio0", "prio1", "prio2", "prio1 no-logger", "prio0 no-logger", "prio1 nt-grad"};
+    std::vector<std::vector<float>> t(6);
     for (int round = 0; round < 6; round++) {
         t[0].push_back(time_prio<0>(b, 200));
         t[1].push_back(time_prio<1>(b, 200));
         t[2].push_back(time_prio<2>(b, 200));
-        t[3].push_back(time_prio<3>(b, 200));
-        t[4].push_back(time_prio<4>(b, 200));
+        t[3].push_back(time_prio<1, 1>(b, 200));
+        t[4].push_back(time_prio<0, 1>(b, 200));
+        t[5].push_back(time_prio<1, 2>(b, 200));
     }
-    for (int v = 0; v < 5; v++) {
+    for (int v = 0; v < 6; v++) {
         printf("%s:", names[v]);
         for (float x : t[v]) printf(" %.2f", x);
         std::vector<float> s = t[v];
