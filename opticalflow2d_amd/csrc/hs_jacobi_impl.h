@@ -763,6 +763,242 @@ __global__ __launch_bounds__(64 * WAVES, MINB) void jacobi3_kernel(
     }
 }
 
+// FOUR Jacobi iterations per pass (K = 4), bit-identical to four single steps.
+// Same strip geometry as jacobi3_kernel: 128-px strips, 120 output columns;
+// the two halo lanes on each side (4 px) are exactly the halo four steps
+// consume (u1 is exact at lane 0 px 1 and lane 63 px 0, u2 at lane 1 px 0 /
+// lane 62 px 1, u3 at lane 1 px 1 / lane 62 px 0).  Per row step j: one u0
+// row (j+4) and one gradient row (j+3) in, u1(j+3), u2(j+2), u3(j+1), u4(j),
+// one u4 row out.  Register window: u0 rows j..j+3, u1 j..j+2, u2 j..j+1,
+// u3 j-1..j, gradient rows j..j+2 (+ one prefetched row of each).  Logger
+// partials of the four iterations: partial .. partial4.
+template <int ROWS, int WAVES, bool XCD = true, int MINB = 1, int UNR = 4, int PRIO = 0>
+__global__ __launch_bounds__(64 * WAVES, MINB) void jacobi4_kernel(
+    const float2 *__restrict__ uo, float2 *__restrict__ un, const float2 *__restrict__ dI,
+    const float *__restrict__ It, int P, int dimx, int nrows, int row0, int dimy, float alphasq,
+    int glo, int ghi, double *__restrict__ partial, double *__restrict__ partial2,
+    double *__restrict__ partial3, double *__restrict__ partial4, unsigned *__restrict__ status,
+    int band0, int gx, int gy, int rows = ROWS, const unsigned *__restrict__ range_flag = nullptr,
+    int jlo = -1, int jhi = -1) {
+    int bx = (int)blockIdx.x, by = (int)blockIdx.y;
+    if constexpr (XCD) {
+        if (!xcd_block(gx, gy, bx, by)) return;
+    }
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int x = bx * kHs3Out - 4 + 2 * lane;
+    const bool own = lane >= 2 && lane <= 61 && x < dimx;
+    const bool xin = x >= 0 && x + 2 <= P;
+    const int band = band0 + by;
+    if (jlo < 0) jlo = band0 * WAVES * rows;
+    if (jhi < 0) jhi = nrows;
+    const int jbeg = jlo + (by * WAVES + wave) * rows;
+    const int jend = min(jbeg + rows, jhi);
+    float s1d = 0.0f, s1p = 0.0f, s2d = 0.0f, s2p = 0.0f, s3d = 0.0f, s3p = 0.0f, s4d = 0.0f,
+          s4p = 0.0f;
+    unsigned bad = 0;
+    auto cl = [&](int j) { return min(max(j, glo), ghi - 1); };
+    const int xl = xin ? x : (x < 0 ? 0 : P - 2);
+    auto ldu = [&](int j) { return load_row<2, true>(uo + (long)cl(j) * P, xl); };
+    struct G {
+        Row<2> g;
+        float t[2], den[2], rcp[2];
+    };
+    const bool grange = range_flag && *range_flag == 0;
+    // a gradient row is loaded raw (dI, It) and completed with the shared
+    // denominator and its reciprocal at first use, so the prefetched row holds
+    // 6 registers instead of 10
+    struct GR {
+        Row<2> g;
+        float2 t;
+    };
+    auto ldgr = [&](int j) {
+        GR r;
+        r.g = load_row<2, false>(dI + (long)cl(j) * P, xl);
+        r.t = ld2<false>(reinterpret_cast<const float2 *>(It + (long)cl(j) * P + xl));
+        return r;
+    };
+    auto fin = [&](const GR &a) {
+        G r;
+        r.g = a.g;
+        r.t[0] = a.t.x;
+        r.t[1] = a.t.y;
+#pragma unroll
+        for (int k = 0; k < 2; k++) {
+            r.den[k] = (alphasq + r.g.v[k].x * r.g.v[k].x) + r.g.v[k].y * r.g.v[k].y;
+            r.rcp[k] = recip_refined(r.den[k]);
+        }
+        return r;
+    };
+    auto ldg = [&](int j) { return fin(ldgr(j)); };
+    // one row of one iteration (the arithmetic of jacobi3_kernel's stepr with
+    // the divide-by-zero test left to hs_precheck_kernel)
+    auto stepr = [&](int j, const Row<2> &m, const Row<2> &c, const Row<2> &p, const G &g) {
+        float2 left, right;
+        left.x = dpp_from_left(c.v[1].x);
+        left.y = dpp_from_left(c.v[1].y);
+        right.x = dpp_from_right(c.v[0].x);
+        right.y = dpp_from_right(c.v[0].y);
+        const int jg = row0 + j;
+        const bool yb = (jg == 0) || (jg == dimy - 1);
+        float2 q[2];
+        float sc[2];
+#pragma unroll
+        for (int k = 0; k < 2; k++) {
+            const float2 l = (k == 0) ? left : c.v[0];
+            const float2 r = (k == 1) ? right : c.v[1];
+            q[k].x = (((l.x + r.x) + m.v[k].x) + p.v[k].x) / 4.0f;
+            q[k].y = (((l.y + r.y) + m.v[k].y) + p.v[k].y) / 4.0f;
+            const int xi = x + k;
+            q[k] = zero_if(yb || xi == 0 || xi == dimx - 1, q[k]);
+            sc[k] = (g.t[k] + q[k].x * g.g.v[k].x) + q[k].y * g.g.v[k].y;
+        }
+        Row<2> o;
+        if (grange &&
+            __builtin_amdgcn_ballot_w64(((int)exp_in<-49, 30>(sc[0]) & (int)exp_in<-49, 30>(sc[1])) == 0) == 0) {
+#pragma unroll
+            for (int k = 0; k < 2; k++) {
+                const float gx = g.g.v[k].x, gy = g.g.v[k].y;
+                const float2 f = div2_unscaled(gx * sc[k], gy * sc[k], g.den[k], g.rcp[k]);
+                o.v[k] = make_float2(q[k].x - f.x, q[k].y - f.y);
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < 2; k++) {
+                const float gx = g.g.v[k].x, gy = g.g.v[k].y;
+                const float fx = gx * sc[k], fy = gy * sc[k];
+                o.v[k] = make_float2(q[k].x - fx / g.den[k], q[k].y - fy / g.den[k]);
+            }
+        }
+        return o;
+    };
+    const bool in1 = x + 1 < dimx;
+    auto mag = [](float a, float b) { return __builtin_amdgcn_sqrtf(a * a + b * b); };
+    auto norms = [&](const Row<2> &nw, const Row<2> &od, float &sd, float &sp) {
+        sd += mag(nw.v[0].x - od.v[0].x, nw.v[0].y - od.v[0].y);
+        sp += mag(od.v[0].x, od.v[0].y);
+        const float d1 = mag(nw.v[1].x - od.v[1].x, nw.v[1].y - od.v[1].y);
+        const float p1 = mag(od.v[1].x, od.v[1].y);
+        sd += in1 ? d1 : 0.0f;
+        sp += in1 ? p1 : 0.0f;
+    };
+    if (jbeg < jend) {
+        // each iteration's Logger norms are taken where its row is produced
+        // (iteration 1 at row j+3, 2 at j+2, 3 at j+1, 4 at j), so the window
+        // holds only the rows the stencils still read
+        Row<2> uj2, uj3;  // u0 rows j+2 .. j+3
+        Row<2> vj1, vj2;  // u1 rows j+1 .. j+2
+        Row<2> wj, wj1;   // u2 rows j .. j+1
+        Row<2> xm1, xj;   // u3 rows j-1 .. j
+        G gj, gj1, gj2;   // gradient rows j .. j+2
+        {
+            const Row<2> a0 = ldu(jbeg - 4), a1 = ldu(jbeg - 3), a2 = ldu(jbeg - 2),
+                         a3 = ldu(jbeg - 1);
+            const Row<2> uj = ldu(jbeg), uj1 = ldu(jbeg + 1);
+            uj2 = ldu(jbeg + 2);
+            uj3 = ldu(jbeg + 3);
+            const G gm3 = ldg(jbeg - 3), gm2 = ldg(jbeg - 2), gm1 = ldg(jbeg - 1);
+            gj = ldg(jbeg);
+            gj1 = ldg(jbeg + 1);
+            gj2 = ldg(jbeg + 2);
+            // u1 rows jbeg-3 .. jbeg+2, u2 rows jbeg-2 .. jbeg+1, u3 rows jbeg-1 .. jbeg
+            const Row<2> pm3 = stepr(jbeg - 3, a0, a1, a2, gm3);
+            const Row<2> pm2 = stepr(jbeg - 2, a1, a2, a3, gm2);
+            const Row<2> pm1 = stepr(jbeg - 1, a2, a3, uj, gm1);
+            const Row<2> vj = stepr(jbeg, a3, uj, uj1, gj);
+            vj1 = stepr(jbeg + 1, uj, uj1, uj2, gj1);
+            vj2 = stepr(jbeg + 2, uj1, uj2, uj3, gj2);
+            const Row<2> qm2 = stepr(jbeg - 2, pm3, pm2, pm1, gm2);
+            const Row<2> qm1 = stepr(jbeg - 1, pm2, pm1, vj, gm1);
+            wj = stepr(jbeg, pm1, vj, vj1, gj);
+            wj1 = stepr(jbeg + 1, vj, vj1, vj2, gj1);
+            xm1 = stepr(jbeg - 1, qm2, qm1, wj, gm1);
+            xj = stepr(jbeg, qm1, wj, wj1, gj);
+            if (own) {  // iteration 1 rows jbeg .. jbeg+2, 2 rows jbeg .. jbeg+1, 3 row jbeg
+                norms(vj, uj, s1d, s1p);
+                norms(wj, vj, s2d, s2p);
+                norms(xj, wj, s3d, s3p);
+                if (jbeg + 1 < jend) {
+                    norms(vj1, uj1, s1d, s1p);
+                    norms(wj1, vj1, s2d, s2p);
+                }
+                if (jbeg + 2 < jend) norms(vj2, uj2, s1d, s1p);
+            }
+        }
+        Row<2> nu = ldu(jbeg + 4);
+        GR ng = ldgr(jbeg + 3);
+        auto body = [&](int j, bool pref) __attribute__((always_inline)) {
+            const Row<2> a4 = nu;  // u0 row j+4
+            const G gj3 = fin(ng);  // gradients row j+3
+            if (pref) {
+                nu = ldu(j + 5);
+                ng = ldgr(j + 4);
+            }
+            const Row<2> vj3 = stepr(j + 3, uj2, uj3, a4, gj3);  // u1 row j+3
+            const Row<2> wj2 = stepr(j + 2, vj1, vj2, vj3, gj2);  // u2 row j+2
+            const Row<2> xj1 = stepr(j + 1, wj, wj1, wj2, gj1);   // u3 row j+1
+            const Row<2> z = stepr(j, xm1, xj, xj1, gj);          // u4 row j
+            if (own) {
+                if (j + 3 < jend) norms(vj3, uj3, s1d, s1p);
+                if (j + 2 < jend) norms(wj2, vj2, s2d, s2p);
+                if (j + 1 < jend) norms(xj1, wj1, s3d, s3p);
+                norms(z, xj, s4d, s4p);
+                float2 *dst = un + (long)j * P + x;
+                if (x + 2 <= dimx)
+                    st4<true>(reinterpret_cast<float4 *>(dst),
+                              make_float4(z.v[0].x, z.v[0].y, z.v[1].x, z.v[1].y));
+                else
+                    dst[0] = z.v[0];
+            }
+            uj2 = uj3;
+            uj3 = a4;
+            vj1 = vj2;
+            vj2 = vj3;
+            wj = wj1;
+            wj1 = wj2;
+            xm1 = xj;
+            xj = xj1;
+            gj = gj1;
+            gj1 = gj2;
+            gj2 = gj3;
+        };
+        int j = jbeg;
+        for (; j + UNR < jend; j += UNR) {
+            progress_prio<PRIO>(j - jbeg, jend - jbeg);
+#pragma unroll
+            for (int k = 0; k < UNR; k++) body(j + k, true);
+        }
+        for (; j < jend; ++j) body(j, j + 1 < jend);
+    }
+    double d[8] = {s1d, s1p, s2d, s2p, s3d, s3p, s4d, s4p};
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1)
+#pragma unroll
+        for (int q = 0; q < 8; q++) d[q] += __shfl_down(d[q], off);
+    __shared__ double red[8][WAVES];
+    if (lane == 0)
+#pragma unroll
+        for (int q = 0; q < 8; q++) red[q][wave] = d[q];
+    if (__any(bad) && lane == 0) atomicOr(status, kStatusDivZero);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double r[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+        for (int w = 0; w < WAVES; ++w)
+#pragma unroll
+            for (int q = 0; q < 8; q++) r[q] += red[q][w];
+        const long blk = (long)band * gx + bx;
+        partial[2 * blk] = r[0];
+        partial[2 * blk + 1] = r[1];
+        partial2[2 * blk] = r[2];
+        partial2[2 * blk + 1] = r[3];
+        partial3[2 * blk] = r[4];
+        partial3[2 * blk + 1] = r[5];
+        partial4[2 * blk] = r[6];
+        partial4[2 * blk + 1] = r[7];
+    }
+}
+
 template <int ROWS, int WAVES>
 inline dim3 grid3_for(int dimx, int nrows) {
     return dim3((dimx + kHs3Out - 1) / kHs3Out, (nrows + ROWS * WAVES - 1) / (ROWS * WAVES));

@@ -229,6 +229,74 @@ int run3(const Bufs &b, int iters, const char *name, double bytes) {
     return bad ? 1 : 0;
 }
 
+template <int PRIO, int DIAG = 0>
+float time_prio(const Bufs &b, int nl);
+
+// the product triple kernel (PRIO 1) timed per iteration
+int run3p(const Bufs &b, int iters, const char *name, double bytes) {
+    const int gx = (b.dimx + kHs3Out - 1) / kHs3Out;
+    const int r = hs3_rows(b.dimx, b.dimy);
+    const int gy = (b.dimy + 4 * r - 1) / (4 * r);
+    const int nl = iters / 3;
+    const float us = time_prio<1>(b, nl) / 3.0f;
+    printf("%-34s %4d blocks r=%-3d %8.2f us/iter (%6.2f us/launch)\n", name, 8 * ((gx * gy + 7) / 8),
+           r, us, 3 * us);
+    return 0;
+}
+
+// four iterations per launch (jacobi4_kernel), `r` j-lines per wave: timed per
+// ITERATION, checked against 8 single steps
+template <int WAVES, int MINB, int PRIO = 1, int UNR = 4>
+int run4(const Bufs &b, int iters, int r, const char *name, double bytes) {
+    const int gx = (b.dimx + kHs3Out - 1) / kHs3Out;
+    const int gy = (b.dimy + WAVES * r - 1) / (WAVES * r);
+    const dim3 gl(8 * ((gx * gy + 7) / 8));
+    auto k = hs::jacobi4_kernel<0, WAVES, true, MINB, UNR, PRIO>;
+    auto k1 = hs::jacobi_kernel<32, 2, 4, true, true, false>;
+    const dim3 g1 = hs::grid_for<32, 2, 4>(b.P, b.dimy);
+    double *p2 = b.partial + 2 * 16384, *p3 = b.partial + 4 * 16384, *p4 = b.partial + 6 * 16384;
+    auto launch4 = [&](const float2 *in, float2 *out) {
+        hipLaunchKernelGGL(k, gl, dim3(64 * WAVES), 0, 0, in, out, b.dI, b.It, b.P, b.dimx, b.dimy,
+                           0, b.dimy, 0.01f, -1, b.dimy + 1, b.partial, p2, p3, p4, b.status, 0,
+                           gx, gy, r, b.rflag, -1, -1);
+    };
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    CK(hipMemset(b.u0 - b.P, 0, sizeof(float2) * (size_t)b.P * (b.dimy + 2)));
+    for (int it = 0; it < 3; it++) launch4((it & 1) ? b.u1 : b.u0, (it & 1) ? b.u0 : b.u1);
+    CK(hipEventRecord(e0, 0));
+    const int nl = iters / 4;
+    for (int it = 0; it < nl; it++) launch4((it & 1) ? b.u1 : b.u0, (it & 1) ? b.u0 : b.u1);
+    CK(hipEventRecord(e1, 0));
+    CK(hipEventSynchronize(e1));
+    float ms;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    const double us = 1000.0 * ms / (4 * nl);
+    const size_t cnt = (size_t)b.P * b.dimy;
+    std::vector<float2> A(cnt), B(cnt);
+    CK(hipMemset(b.u0 - b.P, 0, sizeof(float2) * (size_t)b.P * (b.dimy + 2)));
+    CK(hipMemset(b.u1 - b.P, 0, sizeof(float2) * (size_t)b.P * (b.dimy + 2)));
+    for (int it = 0; it < 8; it++)
+        hipLaunchKernelGGL(k1, g1, dim3(256), 0, 0, (it & 1) ? b.u1 : b.u0, (it & 1) ? b.u0 : b.u1,
+                           b.dI, b.It, b.P, b.dimx, b.dimy, 0, b.dimy, 0.01f, b.partial, b.status);
+    CK(hipMemcpy(A.data(), b.u0, sizeof(float2) * cnt, hipMemcpyDeviceToHost));
+    CK(hipMemset(b.u0 - b.P, 0, sizeof(float2) * (size_t)b.P * (b.dimy + 2)));
+    CK(hipMemset(b.u1 - b.P, 0, sizeof(float2) * (size_t)b.P * (b.dimy + 2)));
+    for (int it = 0; it < 2; it++) launch4((it & 1) ? b.u1 : b.u0, (it & 1) ? b.u0 : b.u1);
+    CK(hipMemcpy(B.data(), b.u0, sizeof(float2) * cnt, hipMemcpyDeviceToHost));
+    long bad = 0;
+    for (int j = 0; j < b.dimy; j++)
+        for (int i = 0; i < b.dimx; i++) {
+            const float2 x = A[(size_t)j * b.P + i], y = B[(size_t)j * b.P + i];
+            if (memcmp(&x, &y, sizeof x) != 0 && bad++ < 3)
+                printf("   mismatch at (%d,%d): %.9g %.9g vs %.9g %.9g\n", i, j, x.x, x.y, y.x, y.y);
+        }
+    printf("%-34s %4u blocks r=%-3d %8.2f us/iter (%6.2f us/launch)  %s\n", name, gl.x, r, us,
+           4 * us, bad ? "MISMATCH" : "bit-identical to 8 single steps");
+    return bad ? 1 : 0;
+}
+
 // The slab's overlapped launch (slab.cpp fused): interior j-lines [E, n-E) on
 // one stream with a block budget that leaves room for the two 16-line edge
 // launches on a second stream.  Timed per three iterations against the full
@@ -446,7 +514,7 @@ int run_stamps(const Bufs &b) {
 
 // Back-to-back launches of the product triple kernel with the progress
 // priority schemes, interleaved in rounds so clock drift hits all alike.
-template <int PRIO, int DIAG = 0>
+template <int PRIO, int DIAG>
 float time_prio(const Bufs &b, int nl) {
     using namespace of2d::hs;
     const int gx = (b.dimx + kHs3Out - 1) / kHs3Out;
@@ -519,8 +587,26 @@ int main(int argc, char **argv) {
     std::vector<float> h((size_t)b.P * rows * 2);
     srand(1);
     for (auto &v : h) v = (rand() / (float)RAND_MAX) - 0.5f;
-    CK(hipMemcpy(based, h.data(), sizeof(float2) * b.P * rows, hipMemcpyHostToDevice));
-    CK(hipMemcpy(baset, h.data(), sizeof(float) * b.P * rows, hipMemcpyHostToDevice));
+    if (getenv("HV_TEX")) {  // bench-like inputs: gradients of a smooth texture pair
+        auto tex = [](double x, double y) {
+            return 0.5 + 0.1 * (sin(0.11 * x + 0.07 * y) + sin(0.05 * x - 0.13 * y + 1.0) +
+                                sin(0.23 * x + 0.19 * y + 2.0));
+        };
+        std::vector<float> g((size_t)b.P * rows * 2, 0.0f), t((size_t)b.P * rows, 0.0f);
+        for (int j = 0; j < n; j++)
+            for (int i = 0; i < n; i++) {
+                const size_t o = (size_t)(j + 1) * b.P + i;
+                g[2 * o] = (float)((tex(i + 1 - 1.5, j + 0.75) - tex(i - 1 - 1.5, j + 0.75)) / 2);
+                g[2 * o + 1] = (float)((tex(i - 1.5, j + 1 + 0.75) - tex(i - 1.5, j - 1 + 0.75)) / 2);
+                t[o] = (float)(tex(i - 1.5, j + 0.75) - tex(i, j));
+            }
+        CK(hipMemcpy(based, g.data(), sizeof(float2) * b.P * rows, hipMemcpyHostToDevice));
+        CK(hipMemcpy(baset, t.data(), sizeof(float) * b.P * rows, hipMemcpyHostToDevice));
+        printf("inputs: smooth texture pair (HV_TEX)\n");
+    } else {
+        CK(hipMemcpy(based, h.data(), sizeof(float2) * b.P * rows, hipMemcpyHostToDevice));
+        CK(hipMemcpy(baset, h.data(), sizeof(float) * b.P * rows, hipMemcpyHostToDevice));
+    }
     b.rflag = b.status + 8;
     CK(hipMemset(b.status, 0, 64));
     hipLaunchKernelGGL(hs::hs_precheck_kernel<>, dim3(1024), dim3(256), 0, 0, based,
@@ -593,6 +679,25 @@ int main(int argc, char **argv) {
         return run_split(b, iters);
     if (argc > 3 && strcmp(argv[3], "triple") == 0)  // the product triple kernel (PMC runs)
         return run3<36, 4, 4, 4, true>(b, iters, "three-step 36r 4w xcd (product at 4096^2)", bytes);
+    if (argc > 3 && strcmp(argv[3], "quad") == 0) {  // four iterations per launch vs the triple
+        int b4 = 0;
+        for (int w = 0; w < 3; w++)  // past the clock transient of sustained load
+            run3<36, 4, 4, 4, true>(b, iters, "(warm-up) three-step", bytes);
+        for (int round = 0; round < 2; round++) {
+            b4 |= run3<36, 4, 4, 4, true>(b, iters, "three-step 36r 4w prio0", bytes);
+            b4 |= run3p(b, iters, "three-step (product, prio1)", bytes);
+            b4 |= run4<4, 4>(b, iters, 36, "four-step 4w minb4", bytes);
+            b4 |= run4<4, 4>(b, iters, 32, "four-step 4w minb4", bytes);
+            b4 |= run4<4, 4>(b, iters, 48, "four-step 4w minb4", bytes);
+            b4 |= run4<4, 3>(b, iters, 36, "four-step 4w minb3", bytes);
+            b4 |= run4<4, 3>(b, iters, 48, "four-step 4w minb3", bytes);
+            b4 |= run4<4, 3>(b, iters, 64, "four-step 4w minb3", bytes);
+            b4 |= run4<4, 4, 1, 2>(b, iters, 36, "four-step 4w minb4 unr2", bytes);
+            b4 |= run4<4, 4, 1, 1>(b, iters, 36, "four-step 4w minb4 unr1", bytes);
+            b4 |= run4<4, 3, 1, 2>(b, iters, 36, "four-step 4w minb3 unr2", bytes);
+        }
+        return b4;
+    }
     if (argc > 3 && strcmp(argv[3], "two") == 0) {
         int b2 = 0;
         V3(32, 2, 4, true, true, false);
