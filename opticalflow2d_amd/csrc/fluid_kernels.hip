@@ -390,36 +390,71 @@ void launch_sor(float4 *vb, int dimx, int dimy, int P, float mu, float lambda, f
     OF2D_HIP(hipGetLastError());
 }
 
+// Row-major <-> skewed transfer of a 64 (i) x 32 (j) pixel tile through LDS.
+// In the skewed array the tile's pixels lie on local rows s = 2 ii + jj in
+// [0, 158), each row a run of at most 16 consecutive columns; a quarter-wave
+// (16 lanes) takes one such run, so every skewed access is a contiguous
+// 256-B segment (row-major iteration would put each lane of a wave on its own
+// skewed row: 64 separate 16-B transactions per wave access).  LDS address
+// of (ii, jj) in a [32][64] tile advances by -127 slots per lane along a run:
+// 16 lanes on distinct banks.  Block dim3(64, 4).
+constexpr int kSkI = 64, kSkJ = 32;
+static_assert(kSkJ == kFieldRows && kSkI == 64, "field kernels tile 64 x kFieldRows");
+template <class F>
+__device__ __forceinline__ void skew_tile_for_each(int i0, int j0, int dimx, int dimy, F f) {
+    const int q = threadIdx.x >> 4, k = threadIdx.x & 15;
+#pragma unroll
+    for (int it = 0; it < 10; it++) {
+        const int s = 16 * it + 4 * (int)threadIdx.y + q;  // < 2 * 63 + 31 + 1 = 158
+        const int ii = max(0, (s - 30) >> 1) + k;         // ceil((s - 31) / 2) + k
+        const int jj = s - 2 * ii;
+        if (s < 2 * (kSkI - 1) + kSkJ && ii < kSkI && jj >= 0 && jj < kSkJ && i0 + ii < dimx &&
+            j0 + jj < dimy)
+            f(ii, jj);
+    }
+}
+
 // vb.zw <- force(u, dI, It) (OpticalFlow.cpp:15-39); with pack_v also vb.xy <- v.
 // Column 0 (never relaxed) is the ghost column of strip 0: its values go to
 // granule region 0 with this sweep's epoch.
-__global__ void sor_pack_kernel(float4 *__restrict__ vb, const float2 *__restrict__ u,
-                                const float2 *__restrict__ dI, const float *__restrict__ It,
-                                const float2 *__restrict__ v, int dimx, int dimy, int P,
-                                v4u *__restrict__ H, unsigned epoch) {
-    const int i = blockIdx.x * 64 + threadIdx.x, j = blockIdx.y * 4 + threadIdx.y;
-    if (i >= dimx || j >= dimy) return;
-    const long idx = (long)j * P + i;
-    const float2 m = u[idx], g = dI[idx];
-    const float sc = (It[idx] + m.x * g.x) + m.y * g.y;
-    const float2 b = make_float2(g.x * sc, g.y * sc);
-    const long sk = sor_index(i, j, P);
-    float2 x;
-    if (v) {
-        x = v[idx];
-        vb[sk] = make_float4(x.x, x.y, b.x, b.y);
-    } else {
-        reinterpret_cast<float2 *>(vb + sk)[1] = b;
-        x = reinterpret_cast<const float2 *>(vb + sk)[0];
+__global__ __launch_bounds__(256) void sor_pack_kernel(float4 *__restrict__ vb,
+                                                        const float2 *__restrict__ u,
+                                                        const float2 *__restrict__ dI,
+                                                        const float *__restrict__ It,
+                                                        const float2 *__restrict__ v, int dimx,
+                                                        int dimy, int P, v4u *__restrict__ H,
+                                                        unsigned epoch) {
+    __shared__ float4 tile[kSkJ][kSkI];
+    const int i0 = blockIdx.x * kSkI, j0 = blockIdx.y * kSkJ;
+    const int i = i0 + threadIdx.x;
+    for (int r = threadIdx.y; r < kSkJ; r += 4) {
+        const int j = j0 + r;
+        if (i >= dimx || j >= dimy) break;
+        const long idx = (long)j * P + i;
+        const float2 m = u[idx], g = dI[idx];
+        const float sc = (It[idx] + m.x * g.x) + m.y * g.y;
+        float2 x = v ? v[idx] : make_float2(0.0f, 0.0f);
+        tile[r][threadIdx.x] = make_float4(x.x, x.y, g.x * sc, g.y * sc);
+        if (i == 0 && H) {
+            if (!v) x = reinterpret_cast<const float2 *>(vb + sor_index(0, j, P))[0];
+            H[kSorPadRows + j] = v4u{epoch, __float_as_uint(x.x), __float_as_uint(x.y), epoch};
+        }
     }
-    if (i == 0 && H)
-        H[kSorPadRows + j] = v4u{epoch, __float_as_uint(x.x), __float_as_uint(x.y), epoch};
+    __syncthreads();
+    skew_tile_for_each(i0, j0, dimx, dimy, [&](int ii, int jj) {
+        const float4 q = tile[jj][ii];
+        float4 *dst = vb + sor_index(i0 + ii, j0 + jj, P);
+        if (v)
+            *dst = q;
+        else
+            reinterpret_cast<float2 *>(dst)[1] = make_float2(q.z, q.w);
+    });
 }
 void launch_sor_pack(float4 *vb, const float2 *u, const float2 *dI, const float *It,
                      const float2 *v, int dimx, int dimy, int P, void *H, unsigned epoch,
                      hipStream_t st) {
-    hipLaunchKernelGGL(sor_pack_kernel, dim3((dimx + 63) / 64, (dimy + 3) / 4), dim3(64, 4), 0,
-                       st, vb, u, dI, It, v, dimx, dimy, P, (v4u *)H, epoch);
+    hipLaunchKernelGGL(sor_pack_kernel, dim3((dimx + kSkI - 1) / kSkI, (dimy + kSkJ - 1) / kSkJ),
+                       dim3(64, 4), 0, st, vb, u, dI, It, v, dimx, dimy, P, (v4u *)H, epoch);
     OF2D_HIP(hipGetLastError());
 }
 
@@ -450,14 +485,19 @@ __global__ __launch_bounds__(256) void increment_kernel(const float2 *__restrict
                                                         const float4 *__restrict__ vel,
                                                         float2 *__restrict__ R, int dimx, int dimy,
                                                         int P, float *__restrict__ part) {
-    const int i = blockIdx.x * 64 + threadIdx.x;
+    __shared__ float2 vt[kSkJ][kSkI];  // the tile's velocities, read along skewed rows
+    const int i0 = blockIdx.x * kSkI, j0 = blockIdx.y * kFieldRows;
+    skew_tile_for_each(i0, j0, dimx, dimy, [&](int ii, int jj) {
+        vt[jj][ii] = reinterpret_cast<const float2 *>(vel + sor_index(i0 + ii, j0 + jj, P))[0];
+    });
+    __syncthreads();
+    const int i = i0 + threadIdx.x;
     float m = 0.0f;
     for (int k = 0; k < kFieldRows / 4; k++) {
-        const int j = blockIdx.y * kFieldRows + 4 * k + threadIdx.y;
+        const int j = j0 + 4 * k + threadIdx.y;
         if (i >= dimx || j >= dimy) break;
         const long idx = (long)j * P + i;
-        const float4 vq = vel[sor_index(i, j, P)];
-        const float2 v = make_float2(vq.x, vq.y);
+        const float2 v = vt[4 * k + threadIdx.y][threadIdx.x];
         const Grad2 d = motion_gradients(u, idx, i, j, dimx, dimy, P);
         // (v - dudx*v.x) - dudy*v.y
         const float2 r = make_float2((v.x - d.dx.x * v.x) - d.dy.x * v.y,
@@ -546,14 +586,19 @@ __global__ __launch_bounds__(256) void logger_kernel(const float4 *__restrict__ 
                                                      float2 *__restrict__ prev, int dimx,
                                                      int dimy, int P,
                                                      double *__restrict__ partial) {
-    const int i = blockIdx.x * 64 + threadIdx.x;
+    __shared__ float2 vt[kSkJ][kSkI];  // as increment_kernel
+    const int i0 = blockIdx.x * kSkI, j0 = blockIdx.y * kFieldRows;
+    skew_tile_for_each(i0, j0, dimx, dimy, [&](int ii, int jj) {
+        vt[jj][ii] = reinterpret_cast<const float2 *>(vb + sor_index(i0 + ii, j0 + jj, P))[0];
+    });
+    __syncthreads();
+    const int i = i0 + threadIdx.x;
     double sd = 0.0, sp = 0.0;
     for (int k = 0; k < kFieldRows / 4; k++) {
-        const int j = blockIdx.y * kFieldRows + 4 * k + threadIdx.y;
+        const int j = j0 + 4 * k + threadIdx.y;
         if (i >= dimx || j >= dimy) break;
         const long idx = (long)j * P + i;
-        const float4 q = vb[sor_index(i, j, P)];
-        const float2 m = make_float2(q.x, q.y), pv = prev[idx];
+        const float2 m = vt[4 * k + threadIdx.y][threadIdx.x], pv = prev[idx];
         u[idx] = m;
         const float ex = m.x - pv.x, ey = m.y - pv.y;
         sd += (double)__builtin_sqrtf(ex * ex + ey * ey);
