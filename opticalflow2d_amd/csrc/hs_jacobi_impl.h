@@ -553,8 +553,12 @@ __device__ __forceinline__ void progress_prio(int done, int total) {
 
 // DIAG (tuning harness only): 1 skips the Logger magnitudes, to price them;
 // 2 loads the gradients non-temporally too (Infinity Cache residency probe)
+// OPT 1: border masks behind a wave-uniform branch (only strips and rows that
+// touch the image border apply them), the division range test on min / max of
+// |sc| (zeros take the IEEE path), the x-neighbour lane shifts folded into the
+// first add of each sum (v_add_f32 with DPP)
 template <int ROWS, int WAVES, bool XCD = true, int MINB = 1, int UNR = 4, bool FD = true,
-          int PRIO = 0, int DIAG = 0>
+          int PRIO = 0, int DIAG = 0, int OPT = 0>
 __global__ __launch_bounds__(64 * WAVES, MINB) void jacobi3_kernel(
     const float2 *__restrict__ uo, float2 *__restrict__ un, const float2 *__restrict__ dI,
     const float *__restrict__ It, int P, int dimx, int nrows, int row0, int dimy, float alphasq,
@@ -611,8 +615,59 @@ __global__ __launch_bounds__(64 * WAVES, MINB) void jacobi3_kernel(
         }
         return r;
     };
+    // any lane of this wave on an x-border pixel (OPT 1): wave-uniform
+    const bool xedge_w = __builtin_amdgcn_ballot_w64(x == 0 || x == dimx - 1 || x + 1 == 0 ||
+                                                     x + 1 == dimx - 1) != 0;
+    auto stepr_opt = [&](int j, const Row<2> &m, const Row<2> &c, const Row<2> &p, const G &g) {
+        // (l + r) per component with the lane shift folded into the add
+        // (the empty asm keeps the SLP vectorizer from pairing x and y into a
+        // packed add, which has no DPP form; the adds then absorb the moves)
+        float sx0 = dpp_from_left(c.v[1].x) + c.v[1].x;
+        float sy0 = dpp_from_left(c.v[1].y) + c.v[1].y;
+        float sx1 = dpp_from_right(c.v[0].x) + c.v[0].x;
+        float sy1 = dpp_from_right(c.v[0].y) + c.v[0].y;
+        asm("" : "+v"(sx0), "+v"(sy0), "+v"(sx1), "+v"(sy1));
+        const int jg = row0 + j;
+        const bool yb = (jg == 0) || (jg == dimy - 1);
+        v2f q[2];
+        q[0] = ((v2f{sx0, sy0} + v2f{m.v[0].x, m.v[0].y}) + v2f{p.v[0].x, p.v[0].y}) / 4.0f;
+        q[1] = ((v2f{sx1, sy1} + v2f{m.v[1].x, m.v[1].y}) + v2f{p.v[1].x, p.v[1].y}) / 4.0f;
+        if (yb || xedge_w) {
+#pragma unroll
+            for (int k = 0; k < 2; k++) {
+                const int xi = x + k;
+                const float2 z = zero_if(yb || xi == 0 || xi == dimx - 1, make_float2(q[k].x, q[k].y));
+                q[k] = v2f{z.x, z.y};
+            }
+        }
+        float sc[2];
+#pragma unroll
+        for (int k = 0; k < 2; k++) {
+            const v2f pr = q[k] * v2f{g.g.v[k].x, g.g.v[k].y};
+            sc[k] = (g.t[k] + pr.x) + pr.y;
+        }
+        Row<2> o;
+        const float mn = fminf(fabsf(sc[0]), fabsf(sc[1])), mx = fmaxf(fabsf(sc[0]), fabsf(sc[1]));
+        if (grange && __builtin_amdgcn_ballot_w64(!(mn >= 0x1p-50f && mx < 0x1p30f)) == 0) {
+#pragma unroll
+            for (int k = 0; k < 2; k++) {
+                const float gx = g.g.v[k].x, gy = g.g.v[k].y;
+                const float2 f = div2_unscaled(gx * sc[k], gy * sc[k], g.den[k], g.rcp[k]);
+                o.v[k] = make_float2(q[k].x - f.x, q[k].y - f.y);
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < 2; k++) {
+                const float gx = g.g.v[k].x, gy = g.g.v[k].y;
+                const float fx = gx * sc[k], fy = gy * sc[k];
+                o.v[k] = make_float2(q[k].x - fx / g.den[k], q[k].y - fy / g.den[k]);
+            }
+        }
+        return o;
+    };
     auto stepr = [&](int j, const Row<2> &m, const Row<2> &c, const Row<2> &p, const G &g,
                      unsigned &b) {
+        if constexpr (OPT == 1) return stepr_opt(j, m, c, p, g);
         float2 left, right;
         left.x = dpp_from_left(c.v[1].x);
         left.y = dpp_from_left(c.v[1].y);
