@@ -204,7 +204,7 @@ def main():
             },
             "roofline": {
                 "bound": "hbm",
-                "kernel": "of2d::hs::jacobi3_kernel<0,4,true,4,4,true,1>",
+                "kernel": "of2d::hs::jacobi3_kernel<0,4,true,4,4,true,1,0,1,true>",
                 "iterations_per_launch": ITERS_PER_LAUNCH,
                 "achieved": round(achieved, 1),
                 "peak": HBM_PEAK_GBS,

@@ -19,6 +19,7 @@
 #pragma once
 
 #include "of2d_device.h"
+#include <type_traits>
 
 // Diagnostic hooks of the triple kernel (the tuning harness defines them to
 // stamp each wave's start / end; the product build leaves them empty)
@@ -557,8 +558,15 @@ __device__ __forceinline__ void progress_prio(int done, int total) {
 // touch the image border apply them), the division range test on min / max of
 // |sc| (zeros take the IEEE path), the x-neighbour lane shifts folded into the
 // first add of each sum (v_add_f32 with DPP)
+// ALT: odd waves march their band upward (from its last j-line to its first),
+// even waves downward, so the two waves on either side of every band boundary
+// of a block read the shared halo j-lines at about the same time (both at the
+// start or both at the end of their bands) and the second read hits in L2;
+// with one direction the halo rows of a band boundary are read a whole band
+// apart, from HBM twice.  The stencil is symmetric in j and every output
+// depends only on input values: bit-identical either way.
 template <int ROWS, int WAVES, bool XCD = true, int MINB = 1, int UNR = 4, bool FD = true,
-          int PRIO = 0, int DIAG = 0, int OPT = 0>
+          int PRIO = 0, int DIAG = 0, int OPT = 0, bool ALT = false>
 __global__ __launch_bounds__(64 * WAVES, MINB) void jacobi3_kernel(
     const float2 *__restrict__ uo, float2 *__restrict__ un, const float2 *__restrict__ dI,
     const float *__restrict__ It, int P, int dimx, int nrows, int row0, int dimy, float alphasq,
@@ -720,34 +728,44 @@ __global__ __launch_bounds__(64 * WAVES, MINB) void jacobi3_kernel(
         sd += in1 ? d1 : 0.0f;  // a select, not a product: padding may hold 0/0
         sp += in1 ? p1 : 0.0f;
     };
-    if (jbeg < jend) {
+    // one band, marched in direction D (+1: j-lines jbeg..jend-1, -1: jend-1..jbeg);
+    // position s of the march is j-line J(s), "ahead" is the next position
+    auto march = [&](auto dirc) __attribute__((always_inline)) {
+        constexpr int D = decltype(dirc)::value;
+        const int n = jend - jbeg;
+        auto J = [&](int sp) { return D > 0 ? jbeg + sp : jend - 1 - sp; };
+        // stepr with the j-1 / j+1 rows taken from behind / ahead by direction
+        auto S = [&](int sp, const Row<2> &bh, const Row<2> &c, const Row<2> &ah, const G &g,
+                     unsigned &b) {
+            return D > 0 ? stepr(J(sp), bh, c, ah, g, b) : stepr(J(sp), ah, c, bh, g, b);
+        };
         unsigned bx_ = 0;  // halo rows: flagged by the waves that own them
-        const Row<2> a0 = ldu(jbeg - 3), a1 = ldu(jbeg - 2), a2 = ldu(jbeg - 1);
-        Row<2> uj = ldu(jbeg), uj1 = ldu(jbeg + 1), uj2 = ldu(jbeg + 2);
-        const G gm2 = ldg(jbeg - 2), gm1 = ldg(jbeg - 1);
-        G gj = ldg(jbeg), gj1 = ldg(jbeg + 1);
-        // u1 rows jbeg-2 .. jbeg+1, u2 rows jbeg-1, jbeg
-        const Row<2> p0 = stepr(jbeg - 2, a0, a1, a2, gm2, bx_);
-        const Row<2> p1 = stepr(jbeg - 1, a1, a2, uj, gm1, bx_);
-        Row<2> vj = stepr(jbeg, a2, uj, uj1, gj, bx_);
-        Row<2> vj1 = stepr(jbeg + 1, uj, uj1, uj2, gj1, bx_);
-        Row<2> wm1 = stepr(jbeg - 1, p0, p1, vj, gm1, bx_);
-        Row<2> wj = stepr(jbeg, p1, vj, vj1, gj, bx_);
-        Row<2> nu = ldu(jbeg + 3);
-        G ng = ldg(jbeg + 2);
+        const Row<2> a0 = ldu(J(-3)), a1 = ldu(J(-2)), a2 = ldu(J(-1));
+        Row<2> uj = ldu(J(0)), uj1 = ldu(J(1)), uj2 = ldu(J(2));
+        const G gm2 = ldg(J(-2)), gm1 = ldg(J(-1));
+        G gj = ldg(J(0)), gj1 = ldg(J(1));
+        // u1 at positions -2 .. 1, u2 at -1, 0
+        const Row<2> p0 = S(-2, a0, a1, a2, gm2, bx_);
+        const Row<2> p1 = S(-1, a1, a2, uj, gm1, bx_);
+        Row<2> vj = S(0, a2, uj, uj1, gj, bx_);
+        Row<2> vj1 = S(1, uj, uj1, uj2, gj1, bx_);
+        Row<2> wm1 = S(-1, p0, p1, vj, gm1, bx_);
+        Row<2> wj = S(0, p1, vj, vj1, gj, bx_);
+        Row<2> nu = ldu(J(3));
+        G ng = ldg(J(2));
         // one output row; the window shifts by renaming, which the unrolled
         // copies below turn into register renames instead of moves
-        auto body = [&](int j, bool pref) __attribute__((always_inline)) {
-            const Row<2> a3 = nu;  // u row j+3
-            const G gj2 = ng;      // gradients row j+2
+        auto body = [&](int sp, bool pref) __attribute__((always_inline)) {
+            const Row<2> a3 = nu;  // u at position sp+3
+            const G gj2 = ng;      // gradients at position sp+2
             if (pref) {
-                nu = ldu(j + 4);
-                ng = ldg(j + 3);
+                nu = ldu(J(sp + 4));
+                ng = ldg(J(sp + 3));
             }
             unsigned b1 = 0, b3 = 0;
-            const Row<2> vj2 = stepr(j + 2, uj1, uj2, a3, gj2, b1);  // u1 row j+2
-            const Row<2> wj1 = stepr(j + 1, vj, vj1, vj2, gj1, b1);  // u2 row j+1
-            const Row<2> z = stepr(j, wm1, wj, wj1, gj, b3);         // u3 row j
+            const Row<2> vj2 = S(sp + 2, uj1, uj2, a3, gj2, b1);  // u1
+            const Row<2> wj1 = S(sp + 1, vj, vj1, vj2, gj1, b1);  // u2
+            const Row<2> z = S(sp, wm1, wj, wj1, gj, b3);         // u3
             if (own) {
                 if constexpr (DIAG != 1) {
                     norms(vj, uj, s1d, s1p);
@@ -755,7 +773,7 @@ __global__ __launch_bounds__(64 * WAVES, MINB) void jacobi3_kernel(
                     norms(z, wj, s3d, s3p);
                 }
                 bad |= b3;  // the denominator depends on dI only: one test per pixel
-                float2 *dst = un + (long)j * P + x;
+                float2 *dst = un + (long)J(sp) * P + x;
                 if (x + 2 <= dimx)
                     st4<true>(reinterpret_cast<float4 *>(dst),
                               make_float4(z.v[0].x, z.v[0].y, z.v[1].x, z.v[1].y));
@@ -772,13 +790,19 @@ __global__ __launch_bounds__(64 * WAVES, MINB) void jacobi3_kernel(
             gj = gj1;
             gj1 = gj2;
         };
-        int j = jbeg;
-        for (; j + UNR < jend; j += UNR) {
-            progress_prio<PRIO>(j - jbeg, jend - jbeg);
+        int sp = 0;
+        for (; sp + UNR < n; sp += UNR) {
+            progress_prio<PRIO>(sp, n);
 #pragma unroll
-            for (int k = 0; k < UNR; k++) body(j + k, true);
+            for (int k = 0; k < UNR; k++) body(sp + k, true);
         }
-        for (; j < jend; ++j) body(j, j + 1 < jend);
+        for (; sp < n; ++sp) body(sp, sp + 1 < n);
+    };
+    if (jbeg < jend) {
+        if (ALT && (wave & 1))
+            march(std::integral_constant<int, -1>{});
+        else
+            march(std::integral_constant<int, 1>{});
     }
     OF2D_HS3_STAMP_END
     double d1d = s1d, d1p = s1p, d2d = s2d, d2p = s2p, d3d = s3d, d3p = s3p;

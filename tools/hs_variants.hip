@@ -229,7 +229,7 @@ int run3(const Bufs &b, int iters, const char *name, double bytes) {
     return bad ? 1 : 0;
 }
 
-template <int PRIO, int DIAG = 0, int OPT = 0>
+template <int PRIO, int DIAG = 0, int OPT = 0, bool ALT = false>
 float time_prio(const Bufs &b, int nl);
 
 // the product triple kernel (PRIO 1) timed per iteration
@@ -514,14 +514,14 @@ int run_stamps(const Bufs &b) {
 
 // Back-to-back launches of the product triple kernel with the progress
 // priority schemes, interleaved in rounds so clock drift hits all alike.
-template <int PRIO, int DIAG, int OPT>
+template <int PRIO, int DIAG, int OPT, bool ALT>
 float time_prio(const Bufs &b, int nl) {
     using namespace of2d::hs;
     const int gx = (b.dimx + kHs3Out - 1) / kHs3Out;
     const int r = hs3_rows(b.dimx, b.dimy);
     const int gy = (b.dimy + 4 * r - 1) / (4 * r);
     const int nblk = 8 * ((gx * gy + 7) / 8);
-    auto k = jacobi3_kernel<0, 4, true, 4, 4, true, PRIO, DIAG, OPT>;
+    auto k = jacobi3_kernel<0, 4, true, 4, 4, true, PRIO, DIAG, OPT, ALT>;
     double *p2 = b.partial + 2 * 16384, *p3 = b.partial + 4 * 16384;
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
@@ -687,34 +687,42 @@ int main(int argc, char **argv) {
         double *p2 = b.partial + 2 * 16384, *p3 = b.partial + 4 * 16384;
         const size_t cnt = (size_t)b.P * (b.dimy + 2);
         std::vector<float2> A(cnt), B(cnt);
-        for (int o = 0; o < 2; o++) {
+        typedef void (*K3)(const float2 *, float2 *, const float2 *, const float *, int, int, int,
+                           int, int, float, int, int, double *, double *, double *, unsigned *,
+                           int, int, int, int, const unsigned *, int, int);
+        const K3 ks[3] = {hs::jacobi3_kernel<0, 4, true, 4, 4, true, 1, 0, 0, false>,
+                          hs::jacobi3_kernel<0, 4, true, 4, 4, true, 1, 0, 0, true>,
+                          hs::jacobi3_kernel<0, 4, true, 4, 4, true, 1, 0, 1, true>};
+        const char *kn[3] = {"product", "ALT (alternating march)", "ALT + OPT 1"};
+        bool same = true;
+        for (int o = 0; o < 3; o++) {
             CK(hipMemset(b.u0 - b.P, 0, sizeof(float2) * cnt));
             CK(hipMemset(b.u1 - b.P, 0, sizeof(float2) * cnt));
-            for (int it = 0; it < 7; it++) {
-                auto k = o ? hs::jacobi3_kernel<0, 4, true, 4, 4, true, 1, 0, 1>
-                           : hs::jacobi3_kernel<0, 4, true, 4, 4, true, 1, 0, 0>;
-                hipLaunchKernelGGL(k, dim3(8 * ((gx * gy + 7) / 8)), dim3(256), 0, 0,
+            for (int it = 0; it < 7; it++)
+                hipLaunchKernelGGL(ks[o], dim3(8 * ((gx * gy + 7) / 8)), dim3(256), 0, 0,
                                    (it & 1) ? b.u1 : b.u0, (it & 1) ? b.u0 : b.u1, b.dI, b.It, b.P,
                                    b.dimx, b.dimy, 0, b.dimy, 0.01f, -1, b.dimy + 1, b.partial, p2,
                                    p3, b.status, 0, gx, gy, r, b.rflag, -1, -1);
-            }
             CK(hipMemcpy(o ? B.data() : A.data(), b.u1 - b.P, sizeof(float2) * cnt,
                          hipMemcpyDeviceToHost));
+            if (o) {
+                const bool eq = memcmp(A.data(), B.data(), sizeof(float2) * cnt) == 0;
+                printf("%s after 21 iterations: %s\n", kn[o], eq ? "bit-identical to the product" : "MISMATCH");
+                same = same && eq;
+            }
         }
-        const bool same = memcmp(A.data(), B.data(), sizeof(float2) * cnt) == 0;
-        printf("OPT 1 after 21 iterations: %s\n", same ? "bit-identical to OPT 0" : "MISMATCH");
         for (int w = 0; w < 3; w++) time_prio<1>(b, 200);
-        std::vector<float> t0, t1;
+        std::vector<float> t[3];
         for (int round = 0; round < 6; round++) {
-            t0.push_back(time_prio<1, 0, 0>(b, 200));
-            t1.push_back(time_prio<1, 0, 1>(b, 200));
+            t[0].push_back(time_prio<1, 0, 0, false>(b, 200));
+            t[1].push_back(time_prio<1, 0, 0, true>(b, 200));
+            t[2].push_back(time_prio<1, 0, 1, true>(b, 200));
         }
-        for (int v = 0; v < 2; v++) {
-            std::vector<float> &t = v ? t1 : t0;
-            printf("OPT %d:", v);
-            for (float x : t) printf(" %.2f", x);
-            std::sort(t.begin(), t.end());
-            printf("  median %.2f us/launch\n", t[t.size() / 2]);
+        for (int v = 0; v < 3; v++) {
+            printf("%-26s:", kn[v]);
+            for (float x : t[v]) printf(" %.2f", x);
+            std::sort(t[v].begin(), t[v].end());
+            printf("  median %.2f us/launch\n", t[v][t[v].size() / 2]);
         }
         return same ? 0 : 1;
     }
