@@ -444,10 +444,12 @@ __global__ __launch_bounds__(256) void sor_pack_kernel(float4 *__restrict__ vb,
     skew_tile_for_each(i0, j0, dimx, dimy, [&](int ii, int jj) {
         const float4 q = tile[jj][ii];
         float4 *dst = vb + sor_index(i0 + ii, j0 + jj, P);
-        if (v)
+        if (v) {
             *dst = q;
-        else
-            reinterpret_cast<float2 *>(dst)[1] = make_float2(q.z, q.w);
+        } else {  // whole 16-B granules (a masked 8-B store per granule measured slower)
+            const float4 o = *dst;
+            *dst = make_float4(o.x, o.y, q.z, q.w);
+        }
     });
 }
 void launch_sor_pack(float4 *vb, const float2 *u, const float2 *dI, const float *It,
