@@ -7,7 +7,7 @@ export TMPDIR=/tmp
 R=$PWD
 CFG=${1:-3}
 mkdir -p gpurun_out/pmc_cfg
-for c in FETCH_SIZE WRITE_SIZE SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_INSTS_LDS SQ_ACTIVE_INST_LDS SQ_INSTS_VMEM_RD; do
+for c in ${PMC_COUNTERS:-FETCH_SIZE WRITE_SIZE SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_INSTS_LDS SQ_ACTIVE_INST_LDS SQ_INSTS_VMEM_RD}; do
   timeout -k 10 300 rocprofv3 --pmc $c --output-format csv -d "$R/gpurun_out/pmc_cfg/$c" -o c -- python3 "$R/bench_configs.py" --configs $CFG --iters 5 > gpurun_out/pmc_cfg/$c.log 2>&1
   rc=$?
   echo "$c rc=$rc"
