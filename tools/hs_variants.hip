@@ -304,13 +304,15 @@ int run4(const Bufs &b, int iters, int r, const char *name, double bytes) {
 int run_split(const Bufs &b, int iters) {
     using namespace of2d::hs;
     const int gx = (b.dimx + kHs3Out - 1) / kHs3Out;
-    constexpr int E = 16, RE = E / 4;
+    // edge j-lines (HV_E, a multiple of 4; the product uses 16) and the
+    // interior's block budget as slab_geometry sets it (8 slots for RCCL)
+    const int E = getenv("HV_E") ? atoi(getenv("HV_E")) : 16, RE = E / 4;
     const int ni = b.dimy - 2 * E;
-    const int ri = hs3_rows(b.dimx, ni, 1024 - 2 * gx);
+    const int ri = hs3_rows(b.dimx, ni, 1024 - 2 * gx - 8);
     const int gyi = (ni + 4 * ri - 1) / (4 * ri);
     const int rf = hs3_rows(b.dimx, b.dimy);
     const int gyf = (b.dimy + 4 * rf - 1) / (4 * rf);
-    auto k = jacobi3_kernel<0, 4, true, 4, 4, true>;
+    auto k = jacobi3_kernel<0, 4, true, 4, 4, true, 1, 0, 1, true>;  // the product kernel
     double *p2 = b.partial + 2 * 16384, *p3 = b.partial + 4 * 16384;
     hipStream_t s1, s2;
     CK(hipStreamCreateWithFlags(&s1, hipStreamNonBlocking));
