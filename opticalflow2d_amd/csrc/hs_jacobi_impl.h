@@ -851,7 +851,8 @@ __global__ __launch_bounds__(64 * WAVES, MINB) void jacobi3_kernel(
 // one u4 row out.  Register window: u0 rows j..j+3, u1 j..j+2, u2 j..j+1,
 // u3 j-1..j, gradient rows j..j+2 (+ one prefetched row of each).  Logger
 // partials of the four iterations: partial .. partial4.
-template <int ROWS, int WAVES, bool XCD = true, int MINB = 1, int UNR = 4, int PRIO = 0>
+template <int ROWS, int WAVES, bool XCD = true, int MINB = 1, int UNR = 4, int PRIO = 0,
+          bool ALT = false>
 __global__ __launch_bounds__(64 * WAVES, MINB) void jacobi4_kernel(
     const float2 *__restrict__ uo, float2 *__restrict__ un, const float2 *__restrict__ dI,
     const float *__restrict__ It, int P, int dimx, int nrows, int row0, int dimy, float alphasq,
@@ -912,29 +913,37 @@ __global__ __launch_bounds__(64 * WAVES, MINB) void jacobi4_kernel(
     auto ldg = [&](int j) { return fin(ldgr(j)); };
     // one row of one iteration (the arithmetic of jacobi3_kernel's stepr with
     // the divide-by-zero test left to hs_precheck_kernel)
+    // the row step of jacobi3_kernel<..., OPT = 1>
+    const bool xedge_w = __builtin_amdgcn_ballot_w64(x == 0 || x == dimx - 1 || x + 1 == 0 ||
+                                                     x + 1 == dimx - 1) != 0;
     auto stepr = [&](int j, const Row<2> &m, const Row<2> &c, const Row<2> &p, const G &g) {
-        float2 left, right;
-        left.x = dpp_from_left(c.v[1].x);
-        left.y = dpp_from_left(c.v[1].y);
-        right.x = dpp_from_right(c.v[0].x);
-        right.y = dpp_from_right(c.v[0].y);
+        float sx0 = dpp_from_left(c.v[1].x) + c.v[1].x;
+        float sy0 = dpp_from_left(c.v[1].y) + c.v[1].y;
+        float sx1 = dpp_from_right(c.v[0].x) + c.v[0].x;
+        float sy1 = dpp_from_right(c.v[0].y) + c.v[0].y;
+        asm("" : "+v"(sx0), "+v"(sy0), "+v"(sx1), "+v"(sy1));
         const int jg = row0 + j;
         const bool yb = (jg == 0) || (jg == dimy - 1);
-        float2 q[2];
+        v2f q[2];
+        q[0] = ((v2f{sx0, sy0} + v2f{m.v[0].x, m.v[0].y}) + v2f{p.v[0].x, p.v[0].y}) / 4.0f;
+        q[1] = ((v2f{sx1, sy1} + v2f{m.v[1].x, m.v[1].y}) + v2f{p.v[1].x, p.v[1].y}) / 4.0f;
+        if (yb || xedge_w) {
+#pragma unroll
+            for (int k = 0; k < 2; k++) {
+                const int xi = x + k;
+                const float2 z = zero_if(yb || xi == 0 || xi == dimx - 1, make_float2(q[k].x, q[k].y));
+                q[k] = v2f{z.x, z.y};
+            }
+        }
         float sc[2];
 #pragma unroll
         for (int k = 0; k < 2; k++) {
-            const float2 l = (k == 0) ? left : c.v[0];
-            const float2 r = (k == 1) ? right : c.v[1];
-            q[k].x = (((l.x + r.x) + m.v[k].x) + p.v[k].x) / 4.0f;
-            q[k].y = (((l.y + r.y) + m.v[k].y) + p.v[k].y) / 4.0f;
-            const int xi = x + k;
-            q[k] = zero_if(yb || xi == 0 || xi == dimx - 1, q[k]);
-            sc[k] = (g.t[k] + q[k].x * g.g.v[k].x) + q[k].y * g.g.v[k].y;
+            const v2f pr = q[k] * v2f{g.g.v[k].x, g.g.v[k].y};
+            sc[k] = (g.t[k] + pr.x) + pr.y;
         }
         Row<2> o;
-        if (grange &&
-            __builtin_amdgcn_ballot_w64(((int)exp_in<-49, 30>(sc[0]) & (int)exp_in<-49, 30>(sc[1])) == 0) == 0) {
+        const float mn = fminf(fabsf(sc[0]), fabsf(sc[1])), mx = fmaxf(fabsf(sc[0]), fabsf(sc[1]));
+        if (grange && __builtin_amdgcn_ballot_w64(!(mn >= 0x1p-50f && mx < 0x1p30f)) == 0) {
 #pragma unroll
             for (int k = 0; k < 2; k++) {
                 const float gx = g.g.v[k].x, gy = g.g.v[k].y;
@@ -961,68 +970,72 @@ __global__ __launch_bounds__(64 * WAVES, MINB) void jacobi4_kernel(
         sd += in1 ? d1 : 0.0f;
         sp += in1 ? p1 : 0.0f;
     };
-    if (jbeg < jend) {
+    // band march in direction D (ALT: odd waves upward, as jacobi3_kernel)
+    auto march = [&](auto dirc) __attribute__((always_inline)) {
+        constexpr int D = decltype(dirc)::value;
+        const int n = jend - jbeg;
+        auto J = [&](int sp) { return D > 0 ? jbeg + sp : jend - 1 - sp; };
+        auto S = [&](int sp, const Row<2> &bh, const Row<2> &c, const Row<2> &ah, const G &g) {
+            return D > 0 ? stepr(J(sp), bh, c, ah, g) : stepr(J(sp), ah, c, bh, g);
+        };
         // each iteration's Logger norms are taken where its row is produced
-        // (iteration 1 at row j+3, 2 at j+2, 3 at j+1, 4 at j), so the window
-        // holds only the rows the stencils still read
-        Row<2> uj2, uj3;  // u0 rows j+2 .. j+3
-        Row<2> vj1, vj2;  // u1 rows j+1 .. j+2
-        Row<2> wj, wj1;   // u2 rows j .. j+1
-        Row<2> xm1, xj;   // u3 rows j-1 .. j
-        G gj, gj1, gj2;   // gradient rows j .. j+2
+        // (iteration 1 at position sp+3, 2 at sp+2, 3 at sp+1, 4 at sp)
+        Row<2> uj2, uj3;  // u0 at positions sp+2 .. sp+3
+        Row<2> vj1, vj2;  // u1 at sp+1 .. sp+2
+        Row<2> wj, wj1;   // u2 at sp .. sp+1
+        Row<2> xm1, xj;   // u3 at sp-1 .. sp
+        G gj, gj1, gj2;   // gradients at sp .. sp+2
         {
-            const Row<2> a0 = ldu(jbeg - 4), a1 = ldu(jbeg - 3), a2 = ldu(jbeg - 2),
-                         a3 = ldu(jbeg - 1);
-            const Row<2> uj = ldu(jbeg), uj1 = ldu(jbeg + 1);
-            uj2 = ldu(jbeg + 2);
-            uj3 = ldu(jbeg + 3);
-            const G gm3 = ldg(jbeg - 3), gm2 = ldg(jbeg - 2), gm1 = ldg(jbeg - 1);
-            gj = ldg(jbeg);
-            gj1 = ldg(jbeg + 1);
-            gj2 = ldg(jbeg + 2);
-            // u1 rows jbeg-3 .. jbeg+2, u2 rows jbeg-2 .. jbeg+1, u3 rows jbeg-1 .. jbeg
-            const Row<2> pm3 = stepr(jbeg - 3, a0, a1, a2, gm3);
-            const Row<2> pm2 = stepr(jbeg - 2, a1, a2, a3, gm2);
-            const Row<2> pm1 = stepr(jbeg - 1, a2, a3, uj, gm1);
-            const Row<2> vj = stepr(jbeg, a3, uj, uj1, gj);
-            vj1 = stepr(jbeg + 1, uj, uj1, uj2, gj1);
-            vj2 = stepr(jbeg + 2, uj1, uj2, uj3, gj2);
-            const Row<2> qm2 = stepr(jbeg - 2, pm3, pm2, pm1, gm2);
-            const Row<2> qm1 = stepr(jbeg - 1, pm2, pm1, vj, gm1);
-            wj = stepr(jbeg, pm1, vj, vj1, gj);
-            wj1 = stepr(jbeg + 1, vj, vj1, vj2, gj1);
-            xm1 = stepr(jbeg - 1, qm2, qm1, wj, gm1);
-            xj = stepr(jbeg, qm1, wj, wj1, gj);
-            if (own) {  // iteration 1 rows jbeg .. jbeg+2, 2 rows jbeg .. jbeg+1, 3 row jbeg
+            const Row<2> a0 = ldu(J(-4)), a1 = ldu(J(-3)), a2 = ldu(J(-2)), a3 = ldu(J(-1));
+            const Row<2> uj = ldu(J(0)), uj1 = ldu(J(1));
+            uj2 = ldu(J(2));
+            uj3 = ldu(J(3));
+            const G gm3 = ldg(J(-3)), gm2 = ldg(J(-2)), gm1 = ldg(J(-1));
+            gj = ldg(J(0));
+            gj1 = ldg(J(1));
+            gj2 = ldg(J(2));
+            const Row<2> pm3 = S(-3, a0, a1, a2, gm3);
+            const Row<2> pm2 = S(-2, a1, a2, a3, gm2);
+            const Row<2> pm1 = S(-1, a2, a3, uj, gm1);
+            const Row<2> vj = S(0, a3, uj, uj1, gj);
+            vj1 = S(1, uj, uj1, uj2, gj1);
+            vj2 = S(2, uj1, uj2, uj3, gj2);
+            const Row<2> qm2 = S(-2, pm3, pm2, pm1, gm2);
+            const Row<2> qm1 = S(-1, pm2, pm1, vj, gm1);
+            wj = S(0, pm1, vj, vj1, gj);
+            wj1 = S(1, vj, vj1, vj2, gj1);
+            xm1 = S(-1, qm2, qm1, wj, gm1);
+            xj = S(0, qm1, wj, wj1, gj);
+            if (own) {
                 norms(vj, uj, s1d, s1p);
                 norms(wj, vj, s2d, s2p);
                 norms(xj, wj, s3d, s3p);
-                if (jbeg + 1 < jend) {
+                if (1 < n) {
                     norms(vj1, uj1, s1d, s1p);
                     norms(wj1, vj1, s2d, s2p);
                 }
-                if (jbeg + 2 < jend) norms(vj2, uj2, s1d, s1p);
+                if (2 < n) norms(vj2, uj2, s1d, s1p);
             }
         }
-        Row<2> nu = ldu(jbeg + 4);
-        GR ng = ldgr(jbeg + 3);
-        auto body = [&](int j, bool pref) __attribute__((always_inline)) {
-            const Row<2> a4 = nu;  // u0 row j+4
-            const G gj3 = fin(ng);  // gradients row j+3
+        Row<2> nu = ldu(J(4));
+        GR ng = ldgr(J(3));
+        auto body = [&](int sp, bool pref) __attribute__((always_inline)) {
+            const Row<2> a4 = nu;
+            const G gj3 = fin(ng);
             if (pref) {
-                nu = ldu(j + 5);
-                ng = ldgr(j + 4);
+                nu = ldu(J(sp + 5));
+                ng = ldgr(J(sp + 4));
             }
-            const Row<2> vj3 = stepr(j + 3, uj2, uj3, a4, gj3);  // u1 row j+3
-            const Row<2> wj2 = stepr(j + 2, vj1, vj2, vj3, gj2);  // u2 row j+2
-            const Row<2> xj1 = stepr(j + 1, wj, wj1, wj2, gj1);   // u3 row j+1
-            const Row<2> z = stepr(j, xm1, xj, xj1, gj);          // u4 row j
+            const Row<2> vj3 = S(sp + 3, uj2, uj3, a4, gj3);  // u1
+            const Row<2> wj2 = S(sp + 2, vj1, vj2, vj3, gj2);  // u2
+            const Row<2> xj1 = S(sp + 1, wj, wj1, wj2, gj1);   // u3
+            const Row<2> z = S(sp, xm1, xj, xj1, gj);          // u4
             if (own) {
-                if (j + 3 < jend) norms(vj3, uj3, s1d, s1p);
-                if (j + 2 < jend) norms(wj2, vj2, s2d, s2p);
-                if (j + 1 < jend) norms(xj1, wj1, s3d, s3p);
+                if (sp + 3 < n) norms(vj3, uj3, s1d, s1p);
+                if (sp + 2 < n) norms(wj2, vj2, s2d, s2p);
+                if (sp + 1 < n) norms(xj1, wj1, s3d, s3p);
                 norms(z, xj, s4d, s4p);
-                float2 *dst = un + (long)j * P + x;
+                float2 *dst = un + (long)J(sp) * P + x;
                 if (x + 2 <= dimx)
                     st4<true>(reinterpret_cast<float4 *>(dst),
                               make_float4(z.v[0].x, z.v[0].y, z.v[1].x, z.v[1].y));
@@ -1041,13 +1054,19 @@ __global__ __launch_bounds__(64 * WAVES, MINB) void jacobi4_kernel(
             gj1 = gj2;
             gj2 = gj3;
         };
-        int j = jbeg;
-        for (; j + UNR < jend; j += UNR) {
-            progress_prio<PRIO>(j - jbeg, jend - jbeg);
+        int sp = 0;
+        for (; sp + UNR < n; sp += UNR) {
+            progress_prio<PRIO>(sp, n);
 #pragma unroll
-            for (int k = 0; k < UNR; k++) body(j + k, true);
+            for (int k = 0; k < UNR; k++) body(sp + k, true);
         }
-        for (; j < jend; ++j) body(j, j + 1 < jend);
+        for (; sp < n; ++sp) body(sp, sp + 1 < n);
+    };
+    if (jbeg < jend) {
+        if (ALT && (wave & 1))
+            march(std::integral_constant<int, -1>{});
+        else
+            march(std::integral_constant<int, 1>{});
     }
     double d[8] = {s1d, s1p, s2d, s2p, s3d, s3p, s4d, s4p};
 #pragma unroll

@@ -238,7 +238,7 @@ int run3p(const Bufs &b, int iters, const char *name, double bytes) {
     const int r = hs3_rows(b.dimx, b.dimy);
     const int gy = (b.dimy + 4 * r - 1) / (4 * r);
     const int nl = iters / 3;
-    const float us = time_prio<1>(b, nl) / 3.0f;
+    const float us = time_prio<1, 0, 1, true>(b, nl) / 3.0f;
     printf("%-34s %4d blocks r=%-3d %8.2f us/iter (%6.2f us/launch)\n", name, 8 * ((gx * gy + 7) / 8),
            r, us, 3 * us);
     return 0;
@@ -246,12 +246,12 @@ int run3p(const Bufs &b, int iters, const char *name, double bytes) {
 
 // four iterations per launch (jacobi4_kernel), `r` j-lines per wave: timed per
 // ITERATION, checked against 8 single steps
-template <int WAVES, int MINB, int PRIO = 1, int UNR = 4>
+template <int WAVES, int MINB, int PRIO = 1, int UNR = 4, bool ALT = false>
 int run4(const Bufs &b, int iters, int r, const char *name, double bytes) {
     const int gx = (b.dimx + kHs3Out - 1) / kHs3Out;
     const int gy = (b.dimy + WAVES * r - 1) / (WAVES * r);
     const dim3 gl(8 * ((gx * gy + 7) / 8));
-    auto k = hs::jacobi4_kernel<0, WAVES, true, MINB, UNR, PRIO>;
+    auto k = hs::jacobi4_kernel<0, WAVES, true, MINB, UNR, PRIO, ALT>;
     auto k1 = hs::jacobi_kernel<32, 2, 4, true, true, false>;
     const dim3 g1 = hs::grid_for<32, 2, 4>(b.P, b.dimy);
     double *p2 = b.partial + 2 * 16384, *p3 = b.partial + 4 * 16384, *p4 = b.partial + 6 * 16384;
@@ -733,17 +733,12 @@ int main(int argc, char **argv) {
         for (int w = 0; w < 3; w++)  // past the clock transient of sustained load
             run3<36, 4, 4, 4, true>(b, iters, "(warm-up) three-step", bytes);
         for (int round = 0; round < 2; round++) {
-            b4 |= run3<36, 4, 4, 4, true>(b, iters, "three-step 36r 4w prio0", bytes);
-            b4 |= run3p(b, iters, "three-step (product, prio1)", bytes);
-            b4 |= run4<4, 4>(b, iters, 36, "four-step 4w minb4", bytes);
-            b4 |= run4<4, 4>(b, iters, 32, "four-step 4w minb4", bytes);
-            b4 |= run4<4, 4>(b, iters, 48, "four-step 4w minb4", bytes);
-            b4 |= run4<4, 3>(b, iters, 36, "four-step 4w minb3", bytes);
-            b4 |= run4<4, 3>(b, iters, 48, "four-step 4w minb3", bytes);
-            b4 |= run4<4, 3>(b, iters, 64, "four-step 4w minb3", bytes);
-            b4 |= run4<4, 4, 1, 2>(b, iters, 36, "four-step 4w minb4 unr2", bytes);
-            b4 |= run4<4, 4, 1, 1>(b, iters, 36, "four-step 4w minb4 unr1", bytes);
-            b4 |= run4<4, 3, 1, 2>(b, iters, 36, "four-step 4w minb3 unr2", bytes);
+            b4 |= run3p(b, iters, "three-step (product)", bytes);
+            b4 |= run4<4, 3, 1, 4, true>(b, iters, 36, "four-step minb3 alt", bytes);
+            b4 |= run4<4, 3, 1, 4, true>(b, iters, 64, "four-step minb3 alt", bytes);
+            b4 |= run4<4, 4, 1, 2, true>(b, iters, 36, "four-step minb4 unr2 alt", bytes);
+            b4 |= run4<4, 4, 1, 1, true>(b, iters, 36, "four-step minb4 unr1 alt", bytes);
+            b4 |= run4<4, 3, 1, 2, true>(b, iters, 36, "four-step minb3 unr2 alt", bytes);
         }
         return b4;
     }
