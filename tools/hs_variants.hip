@@ -230,7 +230,7 @@ int run3(const Bufs &b, int iters, const char *name, double bytes) {
 }
 
 template <int PRIO, int DIAG = 0, int OPT = 0, bool ALT = false>
-float time_prio(const Bufs &b, int nl);
+float time_prio(const Bufs &b, int nl, int rr = 0);
 
 // the product triple kernel (PRIO 1) timed per iteration
 int run3p(const Bufs &b, int iters, const char *name, double bytes) {
@@ -517,10 +517,10 @@ int run_stamps(const Bufs &b) {
 // Back-to-back launches of the product triple kernel with the progress
 // priority schemes, interleaved in rounds so clock drift hits all alike.
 template <int PRIO, int DIAG, int OPT, bool ALT>
-float time_prio(const Bufs &b, int nl) {
+float time_prio(const Bufs &b, int nl, int rr) {
     using namespace of2d::hs;
     const int gx = (b.dimx + kHs3Out - 1) / kHs3Out;
-    const int r = hs3_rows(b.dimx, b.dimy);
+    const int r = rr > 0 ? rr : hs3_rows(b.dimx, b.dimy);
     const int gy = (b.dimy + 4 * r - 1) / (4 * r);
     const int nblk = 8 * ((gx * gy + 7) / 8);
     auto k = jacobi3_kernel<0, 4, true, 4, 4, true, PRIO, DIAG, OPT, ALT>;
@@ -727,6 +727,18 @@ int main(int argc, char **argv) {
             printf("  median %.2f us/launch\n", t[v][t[v].size() / 2]);
         }
         return same ? 0 : 1;
+    }
+    if (argc > 3 && strcmp(argv[3], "rows") == 0) {  // product kernel, j-lines per wave swept
+        const int rs[] = {0, 36, 40, 50, 56, 64, 80, 100, 128};
+        for (int w = 0; w < 2; w++) time_prio<1, 0, 1, true>(b, 50);
+        for (int round = 0; round < 2; round++)
+            for (int r : rs) {
+                const int rr = r ? r : hs3_rows(b.dimx, b.dimy);
+                const int gx = (b.dimx + kHs3Out - 1) / kHs3Out, gy = (b.dimy + 4 * rr - 1) / (4 * rr);
+                printf("rows %3d%s: %6d blocks  %8.2f us/launch\n", rr, r ? "" : " (hs3_rows)",
+                       gx * gy, time_prio<1, 0, 1, true>(b, iters / 3, rr));
+            }
+        return 0;
     }
     if (argc > 3 && strcmp(argv[3], "quad") == 0) {  // four iterations per launch vs the triple
         int b4 = 0;
