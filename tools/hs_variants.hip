@@ -244,6 +244,34 @@ int run3p(const Bufs &b, int iters, const char *name, double bytes) {
     return 0;
 }
 
+// back-to-back launches of the four-step kernel (per launch, events)
+template <int MINB, bool ALT, int UNR = 4>
+float time_quad(const Bufs &b, int nl, int r) {
+    const int gx = (b.dimx + kHs3Out - 1) / kHs3Out;
+    const int gy = (b.dimy + 4 * r - 1) / (4 * r);
+    auto k = hs::jacobi4_kernel<0, 4, true, MINB, UNR, 1, ALT>;
+    double *p2 = b.partial + 2 * 16384, *p3 = b.partial + 4 * 16384, *p4 = b.partial + 6 * 16384;
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    auto go = [&](int it) {
+        hipLaunchKernelGGL(k, dim3(8 * ((gx * gy + 7) / 8)), dim3(256), 0, 0, (it & 1) ? b.u1 : b.u0,
+                           (it & 1) ? b.u0 : b.u1, b.dI, b.It, b.P, b.dimx, b.dimy, 0, b.dimy,
+                           0.01f, -1, b.dimy + 1, b.partial, p2, p3, p4, b.status, 0, gx, gy, r,
+                           b.rflag, -1, -1);
+    };
+    for (int it = 0; it < 4; it++) go(it);
+    CK(hipEventRecord(e0, 0));
+    for (int it = 0; it < nl; it++) go(it);
+    CK(hipEventRecord(e1, 0));
+    CK(hipEventSynchronize(e1));
+    float ms;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    CK(hipEventDestroy(e0));
+    CK(hipEventDestroy(e1));
+    return 1000.0f * ms / nl;
+}
+
 // four iterations per launch (jacobi4_kernel), `r` j-lines per wave: timed per
 // ITERATION, checked against 8 single steps
 template <int WAVES, int MINB, int PRIO = 1, int UNR = 4, bool ALT = false>
@@ -744,6 +772,17 @@ int main(int argc, char **argv) {
         int b4 = 0;
         for (int w = 0; w < 3; w++)  // past the clock transient of sustained load
             run3<36, 4, 4, 4, true>(b, iters, "(warm-up) three-step", bytes);
+        if (getenv("HV_WARM")) {  // sustained back-to-back timing (no host sync between)
+            time_prio<1, 0, 1, true>(b, 1500);
+            for (int round = 0; round < 3; round++) {
+                const float t3 = time_prio<1, 0, 1, true>(b, 600) / 3.0f;
+                const float t4 = time_quad<3, true>(b, 450, 36) / 4.0f;
+                const float t4b = time_quad<4, true, 1>(b, 450, 36) / 4.0f;
+                printf("warm round %d: triple %.2f us/iter, quad minb3 %.2f, quad minb4 unr1 %.2f\n",
+                       round, t3, t4, t4b);
+            }
+            return 0;
+        }
         for (int round = 0; round < 2; round++) {
             b4 |= run3p(b, iters, "three-step (product)", bytes);
             b4 |= run4<4, 3, 1, 4, true>(b, iters, 36, "four-step minb3 alt", bytes);
