@@ -222,7 +222,11 @@ int conv_nblocks(int dimx, int dimy);
 void launch_demons_update(const float *Iref, const float *Imov, const float2 *u, float2 *corr,
                           float2 *out, int dimx, int dimy, int P, float sigma_isq,
                           float sigma_xsq, const float *kf, const double *kd, int kw,
-                          double wfull, int mode, unsigned *status, hipStream_t st);
+                          double wfull, int mode, unsigned *status, hipStream_t st,
+                          hipStream_t side = nullptr, hipEvent_t ev_fork = nullptr,
+                          hipEvent_t ev_join = nullptr);
+// (with `side` and two events the edge columns run on `side` beside the fused
+// launch, and st waits for them before its next work)
 // tile columns of the fused update: returns the x-interior count, *nl / *nr
 // the edge columns on the left / right
 int demons_edge_tiles(int dimx, int kw, int *nl, int *nr);

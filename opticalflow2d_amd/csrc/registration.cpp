@@ -137,6 +137,9 @@ Registration::~Registration() {
     if (d_status_) (void)hipFree(d_status_);
     if (d_scalar_) (void)hipFree(d_scalar_);
     lv_.clear();
+    if (ev_fork_) (void)hipEventDestroy(ev_fork_);
+    if (ev_join_) (void)hipEventDestroy(ev_join_);
+    if (side_st_) (void)hipStreamDestroy(side_st_);
     if (st_) (void)hipStreamDestroy(st_);
 }
 
@@ -158,6 +161,9 @@ void Registration::ensure_device() {
     if (ready_) return;
     if (device_ >= 0) OF2D_HIP(hipSetDevice(device_));
     OF2D_HIP(hipStreamCreateWithFlags(&st_, hipStreamNonBlocking));
+    OF2D_HIP(hipStreamCreateWithFlags(&side_st_, hipStreamNonBlocking));
+    OF2D_HIP(hipEventCreateWithFlags(&ev_fork_, hipEventDisableTiming));
+    OF2D_HIP(hipEventCreateWithFlags(&ev_join_, hipEventDisableTiming));
     lv_.resize(nscales_ + 1);
     size_t maxnb = 1;
     for (int s = 0; s <= nscales_; s++) {
