@@ -1,22 +1,35 @@
 #!/usr/bin/env python3
 """Horn-Schunck Jacobi throughput on MI355X (BASELINE.json metric).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--size S]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--grid G] [--weak]
 
 One step = one Horn-Schunck iteration of the reference loop
 (ImageRegistrationOpticalFlow.cpp:123-135): OpticalFlowDiffusion::get_update +
-the Logger norms over the whole grid, the per-chunk norm reduction /
-convergence read-back, and — for N > 1 — the RCCL halo exchange.  Iterations
-run in threes fused into one pass over HBM (hs::jacobi3_kernel: 28 B/px per
-launch, three iterations per launch, bit-identical to three single steps;
-chunks of 33 iterations are eleven launches, and a single step or a pair fills
-the run's tail), with a three-j-line halo exchange per launch overlapped with
-the interior bands.  Early exit is disabled
-(fixed_iters) so that exactly K iterations run.
+the Logger norms over the whole grid, the per-chunk norm reduction, and — for
+N > 1 — the RCCL halo exchange.  Iterations run in threes fused into one pass
+over HBM (hs::jacobi3_kernel: 28 B/px per launch, three iterations per launch,
+bit-identical to three single steps; chunks of 33 iterations are eleven
+launches, and a single step or a pair fills the run's tail), with a three-j-line
+halo exchange per launch overlapped with the interior bands.  Early exit is
+disabled (fixed_iters) so that exactly K iterations run.
 
-Workload: N = 1 is BASELINE config 2 (Horn-Schunck 4096^2 fp32).  For N > 1
-every rank owns a 4096-row slab of a 4096 x (4096 N) grid (weak scaling, the
-row-slab decomposition of config 5 with a real halo exchange per iteration).
+Workloads (BASELINE.json configs):
+  N = 1 (default --grid 4096)   config 2: Horn-Schunck 4096^2 fp32 on one GPU
+  N > 1 (default --grid 16384)  config 5: Horn-Schunck 16384^2, row slabs of
+                                16384/N j-lines per GPU, RCCL halo over xGMI
+                                (strong scaling: the global grid is fixed)
+  --grid G at any N             G x G split into N row slabs (strong)
+  --weak                        every rank owns a G-row slab of a G x (G N)
+                                grid (weak scaling)
+
+Per-run setup stays outside the timed region, as in the reference's own loop:
+the gradients and the divide-by-zero test run in set_images (once per image
+pair), the Logger sums of the K-step run are reserved before the warm-up, and
+the zeroing of the next run's start buffer (motion_est->reset(),
+ImageRegistrationOpticalFlow.cpp:141) is enqueued at the end of the previous
+run.  The timed region is exactly K iterations plus the final read-back of
+their Logger sums.
+
 Inputs are a synthetic procedural texture pair generated per slab.  For N > 1
 launch with torch.distributed.run (one process per GPU); torch.distributed
 (gloo) bootstraps the RCCL communicator, barriers and takes the max time.
@@ -42,11 +55,66 @@ BYTES_PER_PX_LAUNCH = 28
 ITERS_PER_LAUNCH = 3
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s peak (spec)
 ALPHA = 0.1
+KERNEL = "of2d::hs::jacobi3_kernel<0,4,true,4,4,true,1,0,1,true>"
+TRAFFIC_PROFILE = os.path.join("profiles", "hs_traffic.json")
 
 
-def cpu_baseline(size: int, iters: int):
-    """The oracle (C restatement, 1 thread, reference loop order i-outer/j-inner)
-    timed on `iters` Horn-Schunck iterations of the same size-x-size workload."""
+def parse_args(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    # the default warm-up runs past the clock transient of the first ~40 ms of
+    # sustained load (profiles/r01_v14_bench_warmup.log: W=50 times the dip)
+    ap.add_argument("--steps", type=int, default=3000)
+    ap.add_argument("--warmup", type=int, default=1500)
+    ap.add_argument("--grid", type=int, default=0,
+                    help="global grid G x G (default: 4096 at N=1 = config 2, "
+                         "16384 at N>1 = config 5)")
+    ap.add_argument("--weak", action="store_true",
+                    help="weak scaling: each rank owns G rows of a G x (G N) grid")
+    ap.add_argument("--size", type=int, default=0, help=argparse.SUPPRESS)  # old name of --grid
+    ap.add_argument("--cpu-iters", type=int, default=20)
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="threads of the all-cores CPU baseline (default: OMP_NUM_THREADS, "
+                         "else every CPU)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--timing-launches", type=int, default=200)
+    ap.add_argument("--rccl", action="store_true",
+                    help="N = 1: run the Logger all-reduces through a one-rank RCCL communicator")
+    return ap.parse_args(argv)
+
+
+def workload(args, world: int) -> dict:
+    """Global grid and scaling mode of this run."""
+    g = args.grid or args.size or (4096 if world == 1 else 16384)
+    if args.weak:
+        dimx, dimy, scaling = g, g * world, "weak"
+    else:
+        dimx, dimy, scaling = g, g, "strong"
+    if dimx == 4096 and dimy == 4096:
+        name = "config 2: Horn-Schunck 4096^2 fp32, 1 MI355X"
+    elif dimx == 16384 and dimy == 16384:
+        name = (f"config 5: Horn-Schunck 16384^2 row-slab sharded over {world} MI355X, "
+                "RCCL halo over xGMI")
+    else:
+        name = f"Horn-Schunck {dimx}x{dimy} row slabs over {world} GPU(s)"
+    return {"dimx": dimx, "dimy": dimy, "scaling": scaling, "workload": name}
+
+
+def cpu_threads(args) -> int:
+    if args.cpu_threads > 0:
+        return args.cpu_threads
+    env = os.environ.get("OMP_NUM_THREADS", "")
+    if env.isdigit() and int(env) > 0:
+        return min(int(env), os.cpu_count() or 1)
+    return os.cpu_count() or 1
+
+
+def cpu_baseline(size: int, iters: int, threads: int) -> dict:
+    """The oracle (C restatement of the reference path) timed on `iters`
+    Horn-Schunck iterations of the same size x size workload: once on 1 thread
+    in the reference's loop order (i outer / j inner, what the single-threaded
+    MEX path does), once on `threads` OpenMP threads over j-lines (the Jacobi
+    update is order independent: same motion bit for bit, test_oracle.py)."""
     from oracle import oracle as O
     from opticalflow2d_amd import synthetic as S
     L = O.lib()
@@ -58,43 +126,114 @@ def cpu_baseline(size: int, iters: int):
     It = np.zeros(n, np.float32)
     L.oracle_spatial_derivative(I, size, size, dI)
     L.oracle_temporal_derivative(Ir, I, n, It)
-    u = np.zeros(2 * n, np.float32)
     errs = np.zeros(iters, np.float32)
+    u = np.zeros(2 * n, np.float32)
     L.oracle_set_reference_loop_order(1)
     t0 = time.perf_counter()
     L.oracle_hs_loop(u, dI, It, size, size, ALPHA, iters, 1, errs)
-    dt = time.perf_counter() - t0
+    dt1 = time.perf_counter() - t0
     L.oracle_set_reference_loop_order(0)
-    return {"value": n * iters / dt / 1e6, "unit": "Mpx-it/s", "cores": 1, "kind": "port",
+    mt_iters = iters * 4
+    u = np.zeros(2 * n, np.float32)
+    errs = np.zeros(mt_iters, np.float32)
+    L.oracle_hs_loop_mt(u, dI, It, size, size, ALPHA, 1, threads, errs)  # thread pool up
+    u[:] = 0
+    t0 = time.perf_counter()
+    L.oracle_hs_loop_mt(u, dI, It, size, size, ALPHA, mt_iters, threads, errs)
+    dtn = time.perf_counter() - t0
+    return {"value": round(n * iters / dt1 / 1e6, 2), "unit": "Mpx-it/s", "cores": 1,
+            "kind": "port",
             "sample": f"oracle HS loop (Jacobi + Logger), {size}x{size}, {iters} iterations, "
-                      f"reference loop order, {dt:.1f} s"}
+                      f"1 thread, reference loop order, {dt1:.1f} s",
+            "all_cores": {"value": round(n * mt_iters / dtn / 1e6, 2), "unit": "Mpx-it/s",
+                          "cores": threads, "nproc": os.cpu_count(),
+                          "sample": f"oracle HS loop, {size}x{size}, {mt_iters} iterations, "
+                                    f"{threads} OpenMP threads over j-lines, {dtn:.1f} s"}}
 
 
-def load_traffic():
-    p = os.path.join(ROOT, "profiles", "hs_traffic.json")
-    if os.path.exists(p):
-        try:
-            return json.load(open(p))
-        except Exception:
-            return None
-    return None
+def load_traffic(dimx: int, rows: int):
+    """PMC traffic per launch from the committed profile, only for the grid it
+    was measured on (it is not measured inside this run)."""
+    p = os.path.join(ROOT, TRAFFIC_PROFILE)
+    try:
+        t = json.load(open(p))
+    except Exception:
+        return None
+    if list(t.get("grid", [])) != [dimx, rows]:
+        return None
+    return t
+
+
+def make_record(*, world, wl, steps, warmup, elapsed, gpu_ms, avg_us, iso_us, px_rank, info,
+                traffic, cpu, rows_per_rank):
+    """The JSON line (bench.py contract + roofline + cpu_baseline)."""
+    dimx, dimy = wl["dimx"], wl["dimy"]
+    total_px = dimx * dimy
+    achieved = BYTES_PER_PX_LAUNCH * px_rank / (avg_us * 1e-6) / 1e9
+    return {
+        "metric": METRIC,
+        "value": round(total_px * steps / elapsed / 1e6, 1),
+        "unit": "Mpx-it/s",
+        "n_gpus": world,
+        "steps": steps,
+        "warmup": warmup,
+        "ms_per_step": round(1000 * elapsed / steps, 5),
+        "higher_is_better": True,
+        "scaling": wl["scaling"],
+        "vs_baseline": None,
+        "dtype": "fp32",
+        "data": "synthetic (procedural texture pair, shift (1.5,-0.75))",
+        "config": {
+            "workload": wl["workload"],
+            "grid": [dimx, dimy],
+            "alpha": ALPHA,
+            "iterations": steps,
+            "fixed_iters": True,
+            "parallelism": f"row-slab x{world}",
+            "rows_per_rank": rows_per_rank,
+            "rccl_ranks": info.get("rccl_ranks", 0),
+            "halo_lines_per_launch": info.get("halo_lines", 0),
+            "halo_bytes_per_exchange": (2 * info.get("halo_lines", 0) * dimx * 8
+                                        if world > 1 else 0),
+            "interior_edge_split": bool(info.get("split", 0)),
+            "gpu_ms_rank0": round(gpu_ms, 3),
+            "wall_over_gpu_rank0": round(elapsed * 1000.0 / gpu_ms, 4) if gpu_ms > 0 else None,
+            # the path's own algorithmic traffic (28 B/px per fused launch) per GPU
+            "hbm_GBps_from_step_time": round(BYTES_PER_PX_LAUNCH * total_px * steps
+                                             / ITERS_PER_LAUNCH / elapsed / 1e9 / world, 1),
+            # the reference algorithm's 28 B per pixel-iteration at this rate
+            "ref_bytes_GBps_equiv": round(BYTES_PER_PX_IT * total_px * steps
+                                          / elapsed / 1e9 / world, 1),
+        },
+        "roofline": {
+            "bound": "hbm",
+            "kernel": KERNEL,
+            "scope": "per GPU (rank 0's slab)",
+            "iterations_per_launch": ITERS_PER_LAUNCH,
+            "achieved": round(achieved, 1),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "avg_launch_us": round(avg_us, 3),
+            "avg_launch_source": "HIP events around the timed run on the solver's stream "
+                                 "(gpu ms x 3 / steps)",
+            "isolated_launch_us": round(iso_us, 3),
+            "bytes_per_launch": BYTES_PER_PX_LAUNCH * px_rank,
+            "traffic": (traffic or {}).get("bytes_per_launch"),
+            "traffic_source": (f"{TRAFFIC_PROFILE} (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, "
+                               "committed profile of this kernel at this grid; not measured "
+                               "in this run)" if traffic else None),
+            # the unfused reference algorithm's 28 B per pixel-iteration at the
+            # kernel's per-iteration rate, as a fraction of the HBM peak
+            "ref_equiv_frac": round(BYTES_PER_PX_IT * px_rank * ITERS_PER_LAUNCH
+                                    / (avg_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
+        },
+        "cpu_baseline": cpu,
+    }
 
 
 def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    # the default warm-up runs past the clock transient of the first ~40 ms of
-    # sustained load (profiles/r01_v14_bench_warmup.log: W=50 times the dip)
-    ap.add_argument("--steps", type=int, default=3000)
-    ap.add_argument("--warmup", type=int, default=1500)
-    ap.add_argument("--size", type=int, default=4096, help="dimx and rows per GPU")
-    ap.add_argument("--cpu-iters", type=int, default=20)
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--timing-launches", type=int, default=200)
-    ap.add_argument("--rccl", action="store_true",
-                    help="N = 1: run the Logger all-reduces through a one-rank RCCL communicator")
-    args = ap.parse_args()
-
+    args = parse_args()
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -126,11 +265,15 @@ def main():
         dist.broadcast_object_list(obj, src=0)
         uid = obj[0]
 
-    dimx, dimy = args.size, args.size * world
+    wl = workload(args, world)
+    dimx, dimy = wl["dimx"], wl["dimy"]
     solver = SlabSolver(dimx, dimy, ALPHA, rank, world, device=local, unique_id=uid)
     lo, hi = halo_rows(dimy, rank, world)
     ref, mov = S.procedural_pair(dimx, lo, hi)
     solver.set_images(ref, mov)
+    del ref, mov
+    solver.reserve(max(args.steps, args.warmup))
+    info = solver.info()
 
     def barrier():
         if dist is not None:
@@ -165,68 +308,20 @@ def main():
     avg_us = gpu_ms * 1000.0 * ITERS_PER_LAUNCH / args.steps
     # and back-to-back launches of the kernel alone, after the run
     iso_us = solver.time_kernel(args.timing_launches)
-    px_rank = dimx * (solver.row_end - solver.row_begin)
-    achieved = BYTES_PER_PX_LAUNCH * px_rank / (avg_us * 1e-6) / 1e9
-    traffic = load_traffic()
+    rows = solver.row_end - solver.row_begin
+    px_rank = dimx * rows
 
-    result = None
     if rank == 0:
-        total_px = dimx * dimy
-        value = total_px * args.steps / elapsed / 1e6
-        result = {
-            "metric": METRIC,
-            "value": round(value, 1),
-            "unit": "Mpx-it/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(1000 * elapsed / args.steps, 5),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "fp32",
-            "data": "synthetic (procedural texture pair, shift (1.5,-0.75))",
-            "config": {
-                "workload": "Horn-Schunck Jacobi (config 2: 4096^2 fp32 per GPU; N>1: "
-                            "row slabs of a 4096 x 4096N grid with RCCL halo)",
-                "grid": [dimx, dimy],
-                "alpha": ALPHA,
-                "iterations": args.steps,
-                "fixed_iters": True,
-                "parallelism": f"row-slab x{world}",
-                "gpu_ms_rank0": round(gpu_ms, 3),
-                # the path's own algorithmic traffic (28 B/px per fused launch) per GPU
-                "hbm_GBps_from_step_time": round(BYTES_PER_PX_LAUNCH * total_px * args.steps
-                                                 / ITERS_PER_LAUNCH / elapsed / 1e9 / world, 1),
-                # the reference algorithm's 28 B per pixel-iteration at this rate
-                "ref_bytes_GBps_equiv": round(BYTES_PER_PX_IT * total_px * args.steps
-                                              / elapsed / 1e9 / world, 1),
-            },
-            "roofline": {
-                "bound": "hbm",
-                "kernel": "of2d::hs::jacobi3_kernel<0,4,true,4,4,true,1,0,1,true>",
-                "iterations_per_launch": ITERS_PER_LAUNCH,
-                "achieved": round(achieved, 1),
-                "peak": HBM_PEAK_GBS,
-                "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "avg_launch_us": round(avg_us, 3),
-                "avg_launch_source": "HIP events around the timed run on the solver's stream "
-                                     "(gpu ms x 3 / steps)",
-                "isolated_launch_us": round(iso_us, 3),
-                "bytes_per_launch": BYTES_PER_PX_LAUNCH * px_rank,
-                "traffic": (traffic or {}).get("bytes_per_launch"),
-                # the unfused reference algorithm's 28 B per pixel-iteration at the
-                # kernel's per-iteration rate, as a fraction of the HBM peak
-                "ref_equiv_frac": round(BYTES_PER_PX_IT * px_rank * ITERS_PER_LAUNCH
-                                        / (avg_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
-                "traffic_source": (traffic or {}).get("source"),
-            },
-            "cpu_baseline": None,
-        }
+        cpu = None
         if world == 1 and not args.no_cpu_baseline:
-            result["cpu_baseline"] = cpu_baseline(args.size, args.cpu_iters)
-        print(json.dumps(result), flush=True)
+            # the same grid; iterations scaled to keep the sample at ~15-30 s
+            cpu_it = max(1, int(args.cpu_iters * (4096.0 / dimx) ** 2))
+            cpu = cpu_baseline(dimx, cpu_it, cpu_threads(args))
+        rec = make_record(world=world, wl=wl, steps=args.steps, warmup=args.warmup,
+                          elapsed=elapsed, gpu_ms=gpu_ms, avg_us=avg_us, iso_us=iso_us,
+                          px_rank=px_rank, info=info, traffic=load_traffic(dimx, rows),
+                          cpu=cpu, rows_per_rank=rows)
+        print(json.dumps(rec), flush=True)
     solver.close()
     if dist is not None:
         dist.barrier()

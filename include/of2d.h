@@ -126,15 +126,31 @@ int of2d_slab_create(of2d_slab **out, int dimx, int dimy, float alpha, int rank,
  * (three halo rows: iterations run fused in threes, whose first step also
  * covers two halo j-lines on each side) */
 int of2d_slab_set_images(of2d_slab *s, const double *Iref_rows, const double *Imov_rows);
-/* runs niter Jacobi iterations (HS, Logger, convergence unless fixed_iters);
- * *iters_done receives the iterations executed */
+/* The slab's per-run setup lives outside of2d_slab_run: set_images computes the
+ * gradients and the divide-by-zero / division-range test (dI is fixed per image
+ * pair), and every run ends by zeroing the buffer the next run starts from
+ * (motion_est->reset(), ImageRegistrationOpticalFlow.cpp:141), enqueued behind
+ * the run's end event.  of2d_slab_reserve sizes the per-iteration Logger sums
+ * of a fixed_iters run of niter iterations (3000 are reserved at create), so a
+ * run allocates nothing. */
+int of2d_slab_reserve(of2d_slab *s, int niter);
+/* runs niter Jacobi iterations (HS, Logger, convergence unless fixed_iters)
+ * from zero motion (ImageRegistrationOpticalFlow.cpp:123-135); *iters_done
+ * receives the iterations executed */
 int of2d_slab_run(of2d_slab *s, int niter, int fixed_iters, int *iters_done);
 /* owned rows of the motion, planar double [dimx*nrows*2] */
 int of2d_slab_get_motion(of2d_slab *s, double *out);
 /* average duration (microseconds) of one launch of the Jacobi kernel (the
- * fused kernel: THREE iterations per launch) over nlaunch launches, timed with
- * HIP events on the stream it is launched on */
+ * fused kernel: THREE iterations per launch, over the whole slab in one
+ * launch) over nlaunch launches, timed with HIP events on the stream it is
+ * launched on.  The launches read the zeroed start buffer and write scratch:
+ * the last run's motion (of2d_slab_get_motion) is left intact. */
 int of2d_slab_time_kernel(of2d_slab *s, int nlaunch, double *avg_us);
+/* slab facts for reports: info[0..8] = {nranks, ranks of the RCCL
+ * communicator (ncclCommCount; 0 without one), in-process group (0/1),
+ * row_begin, row_end, dimx, pitch (elements), halo j-lines exchanged per fused
+ * launch, interior/edge split (0/1)}; returns the number of entries written */
+int of2d_slab_info(const of2d_slab *s, int *info, int n);
 /* wall time (ms, HIP events) of the last of2d_slab_run on this rank */
 int of2d_slab_last_run_ms(const of2d_slab *s, double *ms);
 int of2d_slab_destroy(of2d_slab *s);

@@ -54,6 +54,8 @@ SIGNATURES = {
     "of2d_slab_create": (C.c_int, [C.POINTER(C.c_void_p), C.c_int, C.c_int, C.c_float, C.c_int,
                                    C.c_int, C.c_int, C.c_void_p, C.c_int]),
     "of2d_slab_set_images": (C.c_int, [C.c_void_p, _f64p, _f64p]),
+    "of2d_slab_reserve": (C.c_int, [C.c_void_p, C.c_int]),
+    "of2d_slab_info": (C.c_int, [C.c_void_p, C.POINTER(C.c_int), C.c_int]),
     "of2d_slab_run": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.POINTER(C.c_int)]),
     "of2d_slab_get_motion": (C.c_int, [C.c_void_p, _f64p]),
     "of2d_slab_time_kernel": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(C.c_double)]),

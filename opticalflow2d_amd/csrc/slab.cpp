@@ -66,7 +66,12 @@ struct of2d_slab {
     unsigned *d_status = nullptr;
     of2d::HostScratch hs;
     int chunk = 33;  // eleven fused triples per chunk
-    int fin = 0;  // buffer holding the final motion
+    int fin = 0;    // buffer holding the final motion
+    int start = 0;  // zeroed buffer the next run starts from (motion_est->reset())
+    // set_images' divide-by-zero test (dI is fixed per image pair): this rank's
+    // result, and whether the ranks have voted on it yet (first run after
+    // set_images; set_images itself need not be called by all ranks together)
+    bool divzero_local = false, divzero_voted = false, divzero = false;
     double last_ms = 0.0;
     std::vector<float> errs;
     std::string err;
@@ -240,6 +245,24 @@ struct SlabGeometry {
     int n3 = 0;          // block partials a triple writes
     int nb = 0;          // partial row length for every kernel of the slab
 };
+// the motion buffer holding neither the result nor the next run's zeroed start
+int scratch_buffer(const of2d_slab *s) {
+    for (int b = 0; b < 3; b++)
+        if (b != s->fin && b != s->start) return b;
+    return 0;
+}
+
+// room for the per-iteration sums of a fixed_iters run of niter iterations
+void reserve_sums(of2d_slab *s, int niter) {
+    if (s->all_cap >= 2 * (size_t)niter) return;
+    if (s->d_all) OF2D_HIP(hipFree(s->d_all));
+    s->d_all = nullptr;
+    s->all_cap = 0;
+    OF2D_HIP(hipMalloc(&s->d_all, sizeof(double) * 2 * (size_t)niter));
+    s->all_cap = 2 * (size_t)niter;
+    s->hs.ensure((niter + 1) / 2);  // 4 doubles per unit of capacity
+}
+
 SlabGeometry slab_geometry(const of2d_slab *s) {
     SlabGeometry g;
     const int gx = (s->dimx + of2d::kHs3Out - 1) / of2d::kHs3Out;
@@ -317,6 +340,7 @@ static int slab_create(of2d_slab **out, int dimx, int dimy, float alpha, int ran
         OF2D_HIP(hipDeviceSynchronize());  // null-stream memset vs the non-blocking stream
         OF2D_HIP(hipMalloc(&s->d_stage, sizeof(double) * 2 * (size_t)dimx * (s->nrows + 6)));
         s->hs.ensure(s->chunk);
+        reserve_sums(s, 3000);  // 48 KB: a fixed_iters run of 3000 iterations needs no allocation
         if (grp) {
             if (grp->n != nranks) throw std::invalid_argument("slab: group size != nranks");
             OF2D_HIP(hipEventCreateWithFlags(&s->ev_ready, hipEventDisableTiming));
@@ -399,8 +423,29 @@ int of2d_slab_set_images(of2d_slab *s, const double *Iref_rows, const double *Im
                                     s->st);
         for (auto &f : s->u) f.zero(s->st);
         s->fin = 0;
+        s->start = 0;
+        // the triple kernel's division range and the reference's divide-by-zero
+        // test (coord2d.h:95-100), once per image pair: dI is fixed for every
+        // iteration of every run on these images, so the test each iteration
+        // would make is known now; run() throws on all ranks together instead
+        // of one rank leaving the others in an exchange
+        unsigned *range_flag = s->d_status + of2d::kRangeFlagWord;
+        OF2D_HIP(hipMemsetAsync(s->d_status, 0, sizeof(unsigned), s->st));
+        of2d::launch_hs_precheck(s->dI.base, s->dI.count, s->P, 2, s->dimx, s->nrows,
+                                 s->alpha * s->alpha, range_flag, s->d_status, s->st);
+        OF2D_HIP(hipMemcpyAsync(s->hs.status, s->d_status, sizeof(unsigned),
+                                hipMemcpyDeviceToHost, s->st));
+        OF2D_HIP(hipStreamSynchronize(s->st));
+        s->divzero_local = (s->hs.status[0] & of2d::kStatusDivZero) != 0;
+        s->divzero_voted = false;
+        OF2D_HIP(hipMemsetAsync(s->d_status, 0, sizeof(unsigned), s->st));
         OF2D_HIP(hipStreamSynchronize(s->st));
     });
+}
+
+int of2d_slab_reserve(of2d_slab *s, int niter) {
+    if (!s || niter < 0) return OF2D_ERR_INVALID_ARGUMENT;
+    return sguard(s, [&] { reserve_sums(s, niter); });
 }
 
 int of2d_slab_run(of2d_slab *s, int niter, int fixed_iters, int *iters_done) {
@@ -475,31 +520,22 @@ int of2d_slab_run(of2d_slab *s, int niter, int fixed_iters, int *iters_done) {
         auto step = [&](int a, int t, double *partial) {
             single(src_of(a, t), dst_of(a, t), partial);
         };
-        if (fixed_iters && s->all_cap < 2 * (size_t)niter) {
-            if (s->d_all) OF2D_HIP(hipFree(s->d_all));
-            s->all_cap = 2 * (size_t)niter;
-            OF2D_HIP(hipMalloc(&s->d_all, sizeof(double) * s->all_cap));
-            s->hs.ensure((niter + 1) / 2);  // 4 doubles per unit of capacity
+        if (!s->P) throw std::invalid_argument("slab: set_images first");
+        if (!s->divzero_voted) {
+            s->divzero = any_rank(s, s->divzero_local);
+            s->divzero_voted = true;
         }
-        for (auto &f : s->u) f.zero(s->st);  // motion_est starts at zero
+        if (s->divzero) throw std::runtime_error("Divide by zero exception");
+        if (fixed_iters) reserve_sums(s, niter);  // no-op after of2d_slab_reserve
         OF2D_HIP(hipMemsetAsync(s->d_status, 0, sizeof(unsigned), s->st));
-        // the triple kernel's division range and the reference's divide-by-zero
-        // test (coord2d.h:95-100), once for the whole run: dI is fixed, so the
-        // test every iteration would make is known now, and all ranks throw
-        // together instead of one rank leaving the others in an exchange
-        of2d::launch_hs_precheck(s->dI.base, s->dI.count, s->P, 2, s->dimx, s->nrows, alphasq,
-                                 range_flag, s->d_status, s->st);
-        OF2D_HIP(hipMemcpyAsync(s->hs.status, s->d_status, sizeof(unsigned),
-                                hipMemcpyDeviceToHost, s->st));
-        OF2D_HIP(hipStreamSynchronize(s->st));
-        if (any_rank(s, (s->hs.status[0] & of2d::kStatusDivZero) != 0))
-            throw std::runtime_error("Divide by zero exception");
         s->errs.clear();
         OF2D_HIP(hipEventRecord(s->ev0, s->st));
         mark_st();  // comm_st starts after everything enqueued so far
         OF2D_HIP(hipStreamWaitEvent(s->comm_st, s->ev_int, 0));
         OF2D_HIP(hipEventRecord(s->ev_edge, s->comm_st));
-        int a = 0, k0 = 0, done = -1;
+        // motion_est starts at zero: buffer `start` was zeroed by set_images or
+        // at the end of the previous run (below)
+        int a = s->start, k0 = 0, done = -1;
         while (k0 < niter && done < 0) {
             const int C = std::min(s->chunk, niter - k0);
             auto part = [&](int t) { return s->d_partial + (size_t)t * nb * 2; };
@@ -584,6 +620,11 @@ int of2d_slab_run(of2d_slab *s, int niter, int fixed_iters, int *iters_done) {
                     of2d::logger_error(s->hs.sums[2 * t], s->hs.sums[2 * t + 1], npx));
         }
         OF2D_HIP(hipEventRecord(s->ev1, s->st));
+        // ImageRegistrationOpticalFlow.cpp:141 motion_est->reset() after the
+        // loop: zero a buffer other than the result for the next run; it runs
+        // behind ev1 and is not waited for here
+        s->start = (s->fin + 2) % 3;
+        s->u[s->start].zero(s->st);
         OF2D_HIP(hipEventSynchronize(s->ev1));
         float ms = 0.0f;
         OF2D_HIP(hipEventElapsedTime(&ms, s->ev0, s->ev1));
@@ -596,8 +637,9 @@ int of2d_slab_get_motion(of2d_slab *s, double *out) {
     if (!s || !out) return OF2D_ERR_INVALID_ARGUMENT;
     return sguard(s, [&] {
         // motion->accumulate(*motion_est) onto the zero initial motion, then planar
-        // output (Motion::copy_motion_to_input); the scratch buffer is one not holding fin
-        float2 *tmp = s->u[(s->fin + 1) % 3].p;
+        // output (Motion::copy_motion_to_input); the scratch buffer is the one
+        // holding neither fin nor the next run's zeroed start
+        float2 *tmp = s->u[scratch_buffer(s)].p;
         of2d::launch_compose_zero(s->u[s->fin].p, tmp, s->dimx, s->nrows, s->P, s->rb, s->dimy,
                                   s->st);
         of2d::launch_motion_to_planar(tmp, s->P, s->dimx, s->nrows, s->d_stage, s->st);
@@ -610,26 +652,43 @@ int of2d_slab_get_motion(of2d_slab *s, double *out) {
 int of2d_slab_time_kernel(of2d_slab *s, int nlaunch, double *avg_us) {
     if (!s || nlaunch <= 0 || !avg_us) return OF2D_ERR_INVALID_ARGUMENT;
     return sguard(s, [&] {
+        if (!s->P) throw std::invalid_argument("slab: set_images first");
         const float alphasq = s->alpha * s->alpha;
-        // the triple kernel (three iterations per launch): warm-up launch, then
-        // nlaunch back-to-back launches between two events
-        const int nb = of2d::hs_partial_blocks(s->P, s->dimx, s->nrows);
-        double *p2 = s->d_partial + (size_t)nb * 2, *p3 = s->d_partial + (size_t)nb * 4;
-        auto go = [&](int k) {
-            of2d::launch_hs_jacobi3(s->u[1 + (k & 1)].p, s->u[2 - (k & 1)].p, s->dI.p, s->It.p,
-                                    s->P, s->dimx, s->nrows, s->rb, s->dimy, alphasq, -3,
-                                    s->nrows + 3, s->d_partial, p2, p3, s->d_status,
-                                    s->d_status + of2d::kRangeFlagWord, s->st);
+        // the triple kernel (three iterations per launch) over the slab's whole
+        // geometry: a warm-up launch, then nlaunch back-to-back launches between
+        // two events.  Every launch reads the zeroed start buffer and writes the
+        // scratch buffer, so the last run's result (fin) and the next run's start
+        // survive; the partials go to the run's partial buffer, re-written by
+        // every run before it is read
+        const int nb = slab_geometry(s).nb;
+        double *p1 = s->d_partial, *p2 = p1 + (size_t)nb * 2, *p3 = p1 + (size_t)nb * 4;
+        const int in = s->start, out = scratch_buffer(s);
+        auto go = [&] {
+            of2d::launch_hs_jacobi3(s->u[in].p, s->u[out].p, s->dI.p, s->It.p, s->P, s->dimx,
+                                    s->nrows, s->rb, s->dimy, alphasq, -3, s->nrows + 3, p1, p2,
+                                    p3, s->d_status, s->d_status + of2d::kRangeFlagWord, s->st);
         };
-        go(0);
+        go();
         OF2D_HIP(hipEventRecord(s->ev0, s->st));
-        for (int k = 0; k < nlaunch; k++) go(k);
+        for (int k = 0; k < nlaunch; k++) go();
         OF2D_HIP(hipEventRecord(s->ev1, s->st));
         OF2D_HIP(hipEventSynchronize(s->ev1));
         float ms = 0.0f;
         OF2D_HIP(hipEventElapsedTime(&ms, s->ev0, s->ev1));
         *avg_us = 1000.0 * ms / nlaunch;
     });
+}
+
+int of2d_slab_info(const of2d_slab *s, int *info, int n) {
+    if (!s || !info || n < 1) return -OF2D_ERR_INVALID_ARGUMENT;
+    int rccl = 0;
+    if (s->comm && ncclCommCount(s->comm, &rccl) != ncclSuccess) return -OF2D_ERR_DEVICE;
+    const int halo_lines = s->nranks > 1 ? 3 : 0;
+    const int v[] = {s->nranks, rccl, s->grp ? 1 : 0, s->rb, s->re, s->dimx, s->P,
+                     halo_lines, slab_geometry(s).split ? 1 : 0};
+    const int k = std::min(n, (int)(sizeof v / sizeof v[0]));
+    for (int i = 0; i < k; i++) info[i] = v[i];
+    return k;
 }
 
 int of2d_slab_last_run_ms(const of2d_slab *s, double *ms) {

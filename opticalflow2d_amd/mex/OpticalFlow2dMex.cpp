@@ -5,8 +5,8 @@
 // same error strings.  All mode logic and the process-global singleton live in
 // the library (of2d_gateway); this adapter only converts mxArray <-> double*.
 // Build (needs a real MATLAB/Octave mex.h, not available in this image):
-//   mkoctfile --mex -o OpticalFlow2d.mex OpticalFlow2dMex.cpp \
-//       -I<repo>/include -L<repo>/opticalflow2d_amd -lof2d
+//   mkoctfile --mex -o OpticalFlow2d.mex OpticalFlow2dMex.cpp
+//     -I<repo>/include -L<repo>/opticalflow2d_amd -lof2d   (one command line)
 #include <mex.h>
 
 #include <vector>

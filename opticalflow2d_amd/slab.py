@@ -107,6 +107,22 @@ class SlabSolver:
             raise ValueError(f"expected {n} values (rows {lo}..{hi})")
         self._chk(_lib.lib().of2d_slab_set_images(self._h, r, m))
 
+    def reserve(self, niter: int) -> None:
+        """Size the per-iteration Logger sums of a fixed_iters run of `niter`
+        iterations now, so that run allocates nothing."""
+        self._chk(_lib.lib().of2d_slab_reserve(self._h, int(niter)))
+
+    def info(self) -> dict:
+        """nranks, the RCCL communicator's rank count (ncclCommCount; 0 without
+        one), rows, pitch, halo lines per fused launch, interior/edge split."""
+        buf = (C.c_int * 9)()
+        n = _lib.lib().of2d_slab_info(self._h, buf, 9)
+        if n < 0:
+            self._chk(-n)
+        keys = ["nranks", "rccl_ranks", "in_process_group", "row_begin", "row_end", "dimx",
+                "pitch", "halo_lines", "split"]
+        return {k: int(buf[i]) for i, k in enumerate(keys[:n])}
+
     def run(self, niter: int, fixed_iters: bool = False) -> int:
         done = C.c_int(0)
         self._chk(_lib.lib().of2d_slab_run(self._h, int(niter), int(bool(fixed_iters)),

@@ -596,6 +596,68 @@ int oracle_hs_loop(float *u, const float *dI, const float *It, int dimx, int dim
     return rc;
 }
 
+/* The HS loop of oracle_hs_loop (fixed iterations) on `nthreads` OpenMP
+ * threads, for bench.py's all-cores CPU baseline only.  The Jacobi update is
+ * order independent (q is computed from the old u over the whole grid before u
+ * is written, OpticalFlowDiffusion.cpp:43-55), so threads over j-lines give the
+ * same u bit for bit (tests/test_oracle.py).  The Logger norms are summed per
+ * thread in fp32 (the reference's sequential order within each thread's
+ * j-lines) and combined in thread order: the errors round differently from the
+ * single sequential sum, the motion does not depend on them. */
+int oracle_hs_loop_mt(float *uf, const float *dIf, const float *It, int dimx, int dimy,
+                      float alpha, int niter, int nthreads, float *errs) {
+    const unsigned dx = (unsigned)dimx, dy = (unsigned)dimy, n = dx * dy;
+    v2 *u = (v2 *)uf;
+    const v2 *dI = (const v2 *)dIf;
+    v2 *q = (v2 *)malloc(n * sizeof(v2)), *prev = (v2 *)calloc(n, sizeof(v2));
+    float *part = (float *)calloc(2 * (size_t)(nthreads > 0 ? nthreads : 1), sizeof(float));
+    if (!q || !prev || !part) return -1;
+    const float alphasq = alpha * alpha;
+    for (int it = 0; it < niter; it++) {
+#pragma omp parallel num_threads(nthreads)
+        {
+#pragma omp for schedule(static)
+            for (unsigned j = 0; j < dy; j++)
+                for (unsigned i = 0; i < dx; i++) {
+                    unsigned idx = i + j * dx;
+                    q[idx] = qlap_v(u, idx, i, j, dx, dy);
+                }
+            float sd = 0.0f, sp = 0.0f;
+#pragma omp for schedule(static)
+            for (unsigned j = 0; j < dy; j++)
+                for (unsigned i = 0; i < dx; i++) {
+                    unsigned idx = i + j * dx;
+                    v2 f = vmul(dI[idx], It[idx] + q[idx].x * dI[idx].x + q[idx].y * dI[idx].y);
+                    u[idx] = vsub(q[idx], vdiv(f, alphasq + dI[idx].x * dI[idx].x +
+                                                      dI[idx].y * dI[idx].y));
+                    v2 d = vsub(u[idx], prev[idx]);
+                    double px = prev[idx].x, py = prev[idx].y, ex = d.x, ey = d.y;
+                    sp = (float)((double)sp + sqrt(px * px + py * py));
+                    sd = (float)((double)sd + sqrt(ex * ex + ey * ey));
+                    prev[idx] = u[idx];
+                }
+#ifdef _OPENMP
+            extern int omp_get_thread_num(void);
+            const int t = omp_get_thread_num();
+#else
+            const int t = 0;
+#endif
+            part[2 * t] = sd;
+            part[2 * t + 1] = sp;
+        }
+        float sd = 0.0f, sp = 0.0f;
+        for (int t = 0; t < (nthreads > 0 ? nthreads : 1); t++) {
+            sd += part[2 * t];
+            sp += part[2 * t + 1];
+        }
+        if (errs) errs[it] = (sp == 0.0f) ? 0.0f : (sd / (float)n) / (sp / (float)n);
+    }
+    free(q);
+    free(prev);
+    free(part);
+    return niter;
+}
+
 /* src/regularization/Demons/Demons.cpp:34-63 */
 static void demons_force(v2 *c, const v2 *dI, const float *It, unsigned n, float sigma_i,
                          float sigma_x) {

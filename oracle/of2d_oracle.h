@@ -55,6 +55,8 @@ int oracle_hs_update(float *u, const float *dI, const float *It, int dimx, int d
  * returns iterations executed or -1 on error; errs[] receives Logger errors */
 int oracle_hs_loop(float *u, const float *dI, const float *It, int dimx, int dimy, float alpha,
                    int niter, int fixed, float *errs);
+int oracle_hs_loop_mt(float *u, const float *dI, const float *It, int dimx, int dimy,
+                      float alpha, int niter, int nthreads, float *errs);
 float oracle_motion_norm(const float *u, int n);
 float oracle_motion_maxabs(const float *u, int n);
 void oracle_warp2d(float *I, const float *u, int dimx, int dimy);

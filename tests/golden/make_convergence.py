@@ -1,0 +1,82 @@
+#!/usr/bin/env python3
+"""Golden fixtures for convergence-on (default semantics) Horn-Schunck at
+config scale: the oracle (the C restatement of the reference path, pinned by
+the reference's known answers, tests/golden/reference_known_answers.json) run
+init -> register -> get with niter = 1000 and the reference's break test
+`err < 0.001f && iter > 1` (ImageRegistrationOpticalFlow.cpp:131-134) on the
+Logger's sequential fp32 norm (Motion.cpp:42-49, Logger.cpp:32-51).
+
+Each fixture records the iterations executed, every iteration's Logger error,
+the fp64 relative error the same iterates have (to show how close the break is
+to the threshold) and a SHA-256 of the final motion's float32 bits, so a GPU
+test can compare a 4096^2 run without running the oracle again.
+
+    python tests/golden/make_convergence.py [name ...]
+"""
+import hashlib
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+
+from oracle import oracle as O  # noqa: E402
+from opticalflow2d_amd import synthetic as S  # noqa: E402
+
+CASES = {
+    # name: (generator, n, niter)
+    "hs_texture1024": ("texture_pair", 1024, 1000),
+    "hs_texture4096": ("texture_pair", 4096, 1000),
+    "hs_procedural4096": ("procedural_pair", 4096, 1000),
+}
+
+
+def inputs(gen, n):
+    if gen == "texture_pair":
+        return S.texture_pair(n)
+    return S.procedural_pair(n, 0, n)
+
+
+def motion_digest(m):
+    """SHA-256 of the motion as float32 planar [x-plane; y-plane] bits (the
+    double output is an exact widening of the float field)."""
+    f = np.asarray(m, np.float32)
+    planar = np.concatenate([f[:, :, 0].reshape(-1, order="F"), f[:, :, 1].reshape(-1, order="F")])
+    return hashlib.sha256(planar.tobytes()).hexdigest()
+
+
+def main(names):
+    for name in names or CASES:
+        gen, n, niter = CASES[name]
+        ref, mov = inputs(gen, n)
+        O.lib().oracle_capture_output(1)
+        t0 = time.time()
+        o = O.Registration((n, n), [niter], 0, 0, [0.1], 1, 0)
+        o.register(ref, mov)
+        m = o.motion()
+        it = o.iterations()
+        errs = o.last_errors()
+        o.close()
+        O.lib().oracle_clear_output()
+        rec = {
+            "_source": "oracle/of2d_oracle.c via tests/golden/make_convergence.py",
+            "generator": gen, "n": n, "niter": [niter], "alpha": 0.1, "reg": 0,
+            "iterations_executed": it,
+            "errors": [float(e) for e in errs],
+            "motion_sha256_f32_planar": motion_digest(m),
+            "sum_motion": float(m.sum()),
+            "max_abs_motion": float(np.abs(m).max()),
+            "oracle_seconds": round(time.time() - t0, 1),
+        }
+        with open(os.path.join(HERE, f"convergence_{name}.json"), "w") as f:
+            json.dump(rec, f, indent=1)
+        print(name, it, rec["oracle_seconds"], "s", flush=True)
+
+
+if __name__ == "__main__":
+    main(sys.argv[1:])

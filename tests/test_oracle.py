@@ -157,3 +157,25 @@ def test_curvature_dct_matches_r2r_definitions(oracle, shape):
         oracle.lib().oracle_dct2d(b, n0, n1, kind)
         want = scipy_fft.dct(scipy_fft.dct(a, type=dct_type, axis=1), type=dct_type, axis=0)
         np.testing.assert_allclose(b, want, rtol=1e-12, atol=1e-12 * np.abs(want).max())
+
+
+def test_hs_loop_mt_motion_equals_single_thread(oracle):
+    """bench.py's all-cores CPU baseline (oracle_hs_loop_mt, OpenMP over
+    j-lines) computes the same motion bit for bit as the sequential loop: the
+    Jacobi update reads only the previous iterate (OpticalFlowDiffusion.cpp:43-55)."""
+    from opticalflow2d_amd import synthetic as S
+    L = oracle.lib()
+    n = 192
+    ref, mov = S.procedural_pair(n, 0, n)
+    I = np.ascontiguousarray(mov.reshape(-1, order="F").astype(np.float32))
+    Ir = np.ascontiguousarray(ref.reshape(-1, order="F").astype(np.float32))
+    dI = np.zeros(2 * n * n, np.float32)
+    It = np.zeros(n * n, np.float32)
+    L.oracle_spatial_derivative(I, n, n, dI)
+    L.oracle_temporal_derivative(Ir, I, n * n, It)
+    u1, e1 = np.zeros(2 * n * n, np.float32), np.zeros(12, np.float32)
+    u2, e2 = np.zeros(2 * n * n, np.float32), np.zeros(12, np.float32)
+    L.oracle_hs_loop(u1, dI, It, n, n, 0.1, 12, 1, e1)
+    L.oracle_hs_loop_mt(u2, dI, It, n, n, 0.1, 12, 4, e2)
+    assert np.array_equal(u1.view(np.uint32), u2.view(np.uint32))
+    np.testing.assert_allclose(e2[1:], e1[1:], rtol=1e-4)
