@@ -51,10 +51,12 @@ def test_default_semantics_break_and_motion(gpu, name):
     assert it == fx["iterations_executed"]
     assert digest(m) == fx["motion_sha256_f32_planar"]
     # the GPU's Logger sums are fp64; the reference's are sequential fp32
-    # (Motion.cpp:42-49).  At 1024^2 they agree to 3e-5 relative, and the error
-    # falls by ~3 % per iteration around the threshold: the break cannot move.
+    # (Motion.cpp:42-49).  At 1024^2 they agree to 2e-4 relative (measured
+    # 1.7e-4 at iteration 1, <= 3e-5 from iteration 2 on), and around the
+    # threshold the error falls by ~3 % per iteration: the break cannot move.
     want = np.asarray(fx["errors"], np.float32)
-    np.testing.assert_allclose(errs[1:], want[1:], rtol=1e-4)
+    np.testing.assert_allclose(errs[1:], want[1:], rtol=5e-4)
+    np.testing.assert_allclose(errs[2:], want[2:], rtol=1e-4)
     k = it[0] - 1
     assert want[k] < 0.001 <= want[k - 1]
     assert abs(want[k] - 0.001) / 0.001 > 10 * 1e-4
