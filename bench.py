@@ -55,7 +55,7 @@ BYTES_PER_PX_LAUNCH = 28
 ITERS_PER_LAUNCH = 3
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s peak (spec)
 ALPHA = 0.1
-KERNEL = "of2d::hs::jacobi3_kernel<0,4,true,4,4,true,1,0,1,true>"
+KERNEL = "of2d::hs::jacobi3_kernel<0,4,true,4,4,1,true>"
 TRAFFIC_PROFILE = os.path.join("profiles", "hs_traffic.json")
 
 

@@ -59,10 +59,11 @@ void launch_hs_jacobi2(const float2 *u_old, float2 *u_new, const float2 *dI, con
 // 4 resident 4-wave blocks per CU (<= 128 VGPRs), loop unrolled 4x, unscaled
 // exact division where its range holds, issue priority by progress (the four
 // waves of a SIMD finish together: 89.8 -> 83.6 us per launch at 4096^2,
-// tools/hs_variants prio), fewer VALU per row step (OPT 1) and alternating
+// tools/hs_variants prio), fewer VALU per row step (border masks behind a
+// wave-uniform branch, DPP folded into adds) and alternating
 // march directions, so the waves on either side of a band boundary read its
 // halo j-lines together (83.8 -> 82.9 us, tools/hs_variants opt)
-static const auto kHsJacobi3 = &hs::jacobi3_kernel<0, kHs3Waves, true, 4, 4, true, 1, 0, 1, true>;
+static const auto kHsJacobi3 = &hs::jacobi3_kernel<0, kHs3Waves, true, 4, 4, 1, true>;
 
 void launch_hs_jacobi3(const float2 *u_old, float2 *u_new, const float2 *dI, const float *It,
                        int P, int dimx, int nrows, int row0, int dimy, float alphasq, int glo,

@@ -28,7 +28,7 @@ __device__ unsigned long long *g_stamps = nullptr;
         g_stamps[4 * w_ + 2] = __builtin_amdgcn_s_getreg((3 << 11) | 20);              \
         g_stamps[4 * w_ + 3] = __builtin_amdgcn_s_getreg((31 << 11) | 4);              \
     }
-#include "hs_jacobi_impl.h"
+#include "hs_variants_impl.h"  // the variant zoo (product kernels: csrc/hs_jacobi_impl.h)
 
 using namespace of2d;
 

@@ -1,8 +1,6 @@
-// hs_jacobi_impl.h — the fused Horn-Schunck Jacobi kernels the product
-// launches (hs_kernels.hip): one, two and three iterations per pass.  The
-// measured variants that are not launched (four iterations per pass, the
-// pre-OPT row step, diagnostic modes) live in tools/hs_variants_impl.h with
-// the tuning harness.
+// hs_jacobi_impl.h — the fused Horn-Schunck Jacobi step as a template, shared
+// by the product kernel (hs_kernels.hip) and the tuning harness
+// (tools/hs_variants.hip).
 //
 // Restates, fused into one pass over HBM, the three full-grid passes of
 // OpticalFlowDiffusion::get_update (src/regularization/OpticalFlow/
@@ -23,6 +21,12 @@
 #include "of2d_device.h"
 #include <type_traits>
 
+// Diagnostic hooks of the triple kernel (the tuning harness defines them to
+// stamp each wave's start / end; the product build leaves them empty)
+#ifndef OF2D_HS3_STAMP_BEGIN
+#define OF2D_HS3_STAMP_BEGIN
+#define OF2D_HS3_STAMP_END
+#endif
 
 namespace of2d {
 namespace hs {
@@ -548,12 +552,12 @@ __device__ __forceinline__ void progress_prio(int done, int total) {
     }
 }
 
-// Row step: border masks behind a wave-uniform branch (only strips and rows
-// that touch the image border apply them), the division range test on min /
-// max of |sc| (zeros take the IEEE path), the x-neighbour lane shifts folded
-// into the first add of each sum (v_add_f32 with DPP).  The division by the
-// denominator is the unscaled exact sequence (div2_unscaled) when the
-// gradient field passed hs_precheck_kernel's range test (range_flag == 0).
+// DIAG (tuning harness only): 1 skips the Logger magnitudes, to price them;
+// 2 loads the gradients non-temporally too (Infinity Cache residency probe)
+// OPT 1: border masks behind a wave-uniform branch (only strips and rows that
+// touch the image border apply them), the division range test on min / max of
+// |sc| (zeros take the IEEE path), the x-neighbour lane shifts folded into the
+// first add of each sum (v_add_f32 with DPP)
 // ALT: odd waves march their band upward (from its last j-line to its first),
 // even waves downward, so the two waves on either side of every band boundary
 // of a block read the shared halo j-lines at about the same time (both at the
@@ -561,8 +565,8 @@ __device__ __forceinline__ void progress_prio(int done, int total) {
 // with one direction the halo rows of a band boundary are read a whole band
 // apart, from HBM twice.  The stencil is symmetric in j and every output
 // depends only on input values: bit-identical either way.
-template <int ROWS, int WAVES, bool XCD = true, int MINB = 1, int UNR = 4, int PRIO = 0,
-          bool ALT = false>
+template <int ROWS, int WAVES, bool XCD = true, int MINB = 1, int UNR = 4, bool FD = true,
+          int PRIO = 0, int DIAG = 0, int OPT = 0, bool ALT = false>
 __global__ __launch_bounds__(64 * WAVES, MINB) void jacobi3_kernel(
     const float2 *__restrict__ uo, float2 *__restrict__ un, const float2 *__restrict__ dI,
     const float *__restrict__ It, int P, int dimx, int nrows, int row0, int dimy, float alphasq,
@@ -570,6 +574,7 @@ __global__ __launch_bounds__(64 * WAVES, MINB) void jacobi3_kernel(
     double *__restrict__ partial3, unsigned *__restrict__ status, int band0, int gx, int gy,
     int rows = ROWS, const unsigned *__restrict__ range_flag = nullptr, int jlo = -1,
     int jhi = -1) {
+    OF2D_HS3_STAMP_BEGIN
     int bx = (int)blockIdx.x, by = (int)blockIdx.y;
     if constexpr (XCD) {
         if (!xcd_block(gx, gy, bx, by)) return;
@@ -603,22 +608,22 @@ __global__ __launch_bounds__(64 * WAVES, MINB) void jacobi3_kernel(
         Row<2> g;
         float t[2], den[2], rcp[2];
     };
-    // the gradient field is in the unscaled-division range (hs_precheck_kernel)
-    const bool grange = range_flag && *range_flag == 0;
+    // FD: the gradient field is in the unscaled-division range (hs_precheck_kernel)
+    const bool grange = FD && range_flag && *range_flag == 0;
     auto ldg = [&](int j) {
         G r;
-        r.g = load_row<2, false>(dI + (long)cl(j) * P, xl);
-        const float2 tt = ld2<false>(reinterpret_cast<const float2 *>(It + (long)cl(j) * P + xl));
+        r.g = load_row<2, DIAG == 2>(dI + (long)cl(j) * P, xl);
+        const float2 tt = ld2<DIAG == 2>(reinterpret_cast<const float2 *>(It + (long)cl(j) * P + xl));
         r.t[0] = tt.x;
         r.t[1] = tt.y;
 #pragma unroll
         for (int k = 0; k < 2; k++) {
             r.den[k] = (alphasq + r.g.v[k].x * r.g.v[k].x) + r.g.v[k].y * r.g.v[k].y;
-            r.rcp[k] = recip_refined(r.den[k]);
+            if constexpr (FD) r.rcp[k] = recip_refined(r.den[k]);
         }
         return r;
     };
-    // any lane of this wave on an x-border pixel: wave-uniform
+    // any lane of this wave on an x-border pixel (OPT 1): wave-uniform
     const bool xedge_w = __builtin_amdgcn_ballot_w64(x == 0 || x == dimx - 1 || x + 1 == 0 ||
                                                      x + 1 == dimx - 1) != 0;
     auto stepr_opt = [&](int j, const Row<2> &m, const Row<2> &c, const Row<2> &p, const G &g) {
@@ -668,10 +673,51 @@ __global__ __launch_bounds__(64 * WAVES, MINB) void jacobi3_kernel(
         }
         return o;
     };
-    // the triple kernel needs no per-pixel zero test: hs_precheck_kernel made
-    // it once for the field (dI is fixed), so the flag word stays unused
     auto stepr = [&](int j, const Row<2> &m, const Row<2> &c, const Row<2> &p, const G &g,
-                     unsigned &) { return stepr_opt(j, m, c, p, g); };
+                     unsigned &b) {
+        if constexpr (OPT == 1) return stepr_opt(j, m, c, p, g);
+        float2 left, right;
+        left.x = dpp_from_left(c.v[1].x);
+        left.y = dpp_from_left(c.v[1].y);
+        right.x = dpp_from_right(c.v[0].x);
+        right.y = dpp_from_right(c.v[0].y);
+        const int jg = row0 + j;
+        const bool yb = (jg == 0) || (jg == dimy - 1);
+        float2 q[2];
+        float sc[2];
+#pragma unroll
+        for (int k = 0; k < 2; k++) {
+            const float2 l = (k == 0) ? left : c.v[0];
+            const float2 r = (k == 1) ? right : c.v[1];
+            q[k].x = (((l.x + r.x) + m.v[k].x) + p.v[k].x) / 4.0f;
+            q[k].y = (((l.y + r.y) + m.v[k].y) + p.v[k].y) / 4.0f;
+            const int xi = x + k;
+            q[k] = zero_if(yb || xi == 0 || xi == dimx - 1, q[k]);
+            sc[k] = (g.t[k] + q[k].x * g.g.v[k].x) + q[k].y * g.g.v[k].y;
+            // FD: the zero test is hs_precheck_kernel's, once per field
+            if constexpr (!FD) b |= (g.den[k] == 0.0f) ? 1u : 0u;
+        }
+        Row<2> o;
+        // sc in 0 or [2^-50, 2^30) puts the numerators gx*sc, gy*sc in the
+        // range where the unscaled division is exact (div2_unscaled)
+        if (FD && grange &&
+            __builtin_amdgcn_ballot_w64(((int)exp_in<-49, 30>(sc[0]) & (int)exp_in<-49, 30>(sc[1])) == 0) == 0) {
+#pragma unroll
+            for (int k = 0; k < 2; k++) {
+                const float gx = g.g.v[k].x, gy = g.g.v[k].y;
+                const float2 f = div2_unscaled(gx * sc[k], gy * sc[k], g.den[k], g.rcp[k]);
+                o.v[k] = make_float2(q[k].x - f.x, q[k].y - f.y);
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < 2; k++) {
+                const float gx = g.g.v[k].x, gy = g.g.v[k].y;
+                const float fx = gx * sc[k], fy = gy * sc[k];
+                o.v[k] = make_float2(q[k].x - fx / g.den[k], q[k].y - fy / g.den[k]);
+            }
+        }
+        return o;
+    };
     const bool in1 = x + 1 < dimx;
     auto mag = [](float a, float b) { return __builtin_amdgcn_sqrtf(a * a + b * b); };
     auto norms = [&](const Row<2> &nw, const Row<2> &od, float &sd, float &sp) {
@@ -721,9 +767,11 @@ __global__ __launch_bounds__(64 * WAVES, MINB) void jacobi3_kernel(
             const Row<2> wj1 = S(sp + 1, vj, vj1, vj2, gj1, b1);  // u2
             const Row<2> z = S(sp, wm1, wj, wj1, gj, b3);         // u3
             if (own) {
-                norms(vj, uj, s1d, s1p);
-                norms(wj, vj, s2d, s2p);
-                norms(z, wj, s3d, s3p);
+                if constexpr (DIAG != 1) {
+                    norms(vj, uj, s1d, s1p);
+                    norms(wj, vj, s2d, s2p);
+                    norms(z, wj, s3d, s3p);
+                }
                 bad |= b3;  // the denominator depends on dI only: one test per pixel
                 float2 *dst = un + (long)J(sp) * P + x;
                 if (x + 2 <= dimx)
@@ -756,6 +804,7 @@ __global__ __launch_bounds__(64 * WAVES, MINB) void jacobi3_kernel(
         else
             march(std::integral_constant<int, 1>{});
     }
+    OF2D_HS3_STAMP_END
     double d1d = s1d, d1p = s1p, d2d = s2d, d2p = s2p, d3d = s3d, d3p = s3p;
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) {
@@ -790,6 +839,261 @@ __global__ __launch_bounds__(64 * WAVES, MINB) void jacobi3_kernel(
         partial2[2 * blk + 1] = r[3];
         partial3[2 * blk] = r[4];
         partial3[2 * blk + 1] = r[5];
+    }
+}
+
+// FOUR Jacobi iterations per pass (K = 4), bit-identical to four single steps.
+// Same strip geometry as jacobi3_kernel: 128-px strips, 120 output columns;
+// the two halo lanes on each side (4 px) are exactly the halo four steps
+// consume (u1 is exact at lane 0 px 1 and lane 63 px 0, u2 at lane 1 px 0 /
+// lane 62 px 1, u3 at lane 1 px 1 / lane 62 px 0).  Per row step j: one u0
+// row (j+4) and one gradient row (j+3) in, u1(j+3), u2(j+2), u3(j+1), u4(j),
+// one u4 row out.  Register window: u0 rows j..j+3, u1 j..j+2, u2 j..j+1,
+// u3 j-1..j, gradient rows j..j+2 (+ one prefetched row of each).  Logger
+// partials of the four iterations: partial .. partial4.
+template <int ROWS, int WAVES, bool XCD = true, int MINB = 1, int UNR = 4, int PRIO = 0,
+          bool ALT = false>
+__global__ __launch_bounds__(64 * WAVES, MINB) void jacobi4_kernel(
+    const float2 *__restrict__ uo, float2 *__restrict__ un, const float2 *__restrict__ dI,
+    const float *__restrict__ It, int P, int dimx, int nrows, int row0, int dimy, float alphasq,
+    int glo, int ghi, double *__restrict__ partial, double *__restrict__ partial2,
+    double *__restrict__ partial3, double *__restrict__ partial4, unsigned *__restrict__ status,
+    int band0, int gx, int gy, int rows = ROWS, const unsigned *__restrict__ range_flag = nullptr,
+    int jlo = -1, int jhi = -1) {
+    int bx = (int)blockIdx.x, by = (int)blockIdx.y;
+    if constexpr (XCD) {
+        if (!xcd_block(gx, gy, bx, by)) return;
+    }
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int x = bx * kHs3Out - 4 + 2 * lane;
+    const bool own = lane >= 2 && lane <= 61 && x < dimx;
+    const bool xin = x >= 0 && x + 2 <= P;
+    const int band = band0 + by;
+    if (jlo < 0) jlo = band0 * WAVES * rows;
+    if (jhi < 0) jhi = nrows;
+    const int jbeg = jlo + (by * WAVES + wave) * rows;
+    const int jend = min(jbeg + rows, jhi);
+    float s1d = 0.0f, s1p = 0.0f, s2d = 0.0f, s2p = 0.0f, s3d = 0.0f, s3p = 0.0f, s4d = 0.0f,
+          s4p = 0.0f;
+    unsigned bad = 0;
+    auto cl = [&](int j) { return min(max(j, glo), ghi - 1); };
+    const int xl = xin ? x : (x < 0 ? 0 : P - 2);
+    auto ldu = [&](int j) { return load_row<2, true>(uo + (long)cl(j) * P, xl); };
+    struct G {
+        Row<2> g;
+        float t[2], den[2], rcp[2];
+    };
+    const bool grange = range_flag && *range_flag == 0;
+    // a gradient row is loaded raw (dI, It) and completed with the shared
+    // denominator and its reciprocal at first use, so the prefetched row holds
+    // 6 registers instead of 10
+    struct GR {
+        Row<2> g;
+        float2 t;
+    };
+    auto ldgr = [&](int j) {
+        GR r;
+        r.g = load_row<2, false>(dI + (long)cl(j) * P, xl);
+        r.t = ld2<false>(reinterpret_cast<const float2 *>(It + (long)cl(j) * P + xl));
+        return r;
+    };
+    auto fin = [&](const GR &a) {
+        G r;
+        r.g = a.g;
+        r.t[0] = a.t.x;
+        r.t[1] = a.t.y;
+#pragma unroll
+        for (int k = 0; k < 2; k++) {
+            r.den[k] = (alphasq + r.g.v[k].x * r.g.v[k].x) + r.g.v[k].y * r.g.v[k].y;
+            r.rcp[k] = recip_refined(r.den[k]);
+        }
+        return r;
+    };
+    auto ldg = [&](int j) { return fin(ldgr(j)); };
+    // one row of one iteration (the arithmetic of jacobi3_kernel's stepr with
+    // the divide-by-zero test left to hs_precheck_kernel)
+    // the row step of jacobi3_kernel<..., OPT = 1>
+    const bool xedge_w = __builtin_amdgcn_ballot_w64(x == 0 || x == dimx - 1 || x + 1 == 0 ||
+                                                     x + 1 == dimx - 1) != 0;
+    auto stepr = [&](int j, const Row<2> &m, const Row<2> &c, const Row<2> &p, const G &g) {
+        float sx0 = dpp_from_left(c.v[1].x) + c.v[1].x;
+        float sy0 = dpp_from_left(c.v[1].y) + c.v[1].y;
+        float sx1 = dpp_from_right(c.v[0].x) + c.v[0].x;
+        float sy1 = dpp_from_right(c.v[0].y) + c.v[0].y;
+        asm("" : "+v"(sx0), "+v"(sy0), "+v"(sx1), "+v"(sy1));
+        const int jg = row0 + j;
+        const bool yb = (jg == 0) || (jg == dimy - 1);
+        v2f q[2];
+        q[0] = ((v2f{sx0, sy0} + v2f{m.v[0].x, m.v[0].y}) + v2f{p.v[0].x, p.v[0].y}) / 4.0f;
+        q[1] = ((v2f{sx1, sy1} + v2f{m.v[1].x, m.v[1].y}) + v2f{p.v[1].x, p.v[1].y}) / 4.0f;
+        if (yb || xedge_w) {
+#pragma unroll
+            for (int k = 0; k < 2; k++) {
+                const int xi = x + k;
+                const float2 z = zero_if(yb || xi == 0 || xi == dimx - 1, make_float2(q[k].x, q[k].y));
+                q[k] = v2f{z.x, z.y};
+            }
+        }
+        float sc[2];
+#pragma unroll
+        for (int k = 0; k < 2; k++) {
+            const v2f pr = q[k] * v2f{g.g.v[k].x, g.g.v[k].y};
+            sc[k] = (g.t[k] + pr.x) + pr.y;
+        }
+        Row<2> o;
+        const float mn = fminf(fabsf(sc[0]), fabsf(sc[1])), mx = fmaxf(fabsf(sc[0]), fabsf(sc[1]));
+        if (grange && __builtin_amdgcn_ballot_w64(!(mn >= 0x1p-50f && mx < 0x1p30f)) == 0) {
+#pragma unroll
+            for (int k = 0; k < 2; k++) {
+                const float gx = g.g.v[k].x, gy = g.g.v[k].y;
+                const float2 f = div2_unscaled(gx * sc[k], gy * sc[k], g.den[k], g.rcp[k]);
+                o.v[k] = make_float2(q[k].x - f.x, q[k].y - f.y);
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < 2; k++) {
+                const float gx = g.g.v[k].x, gy = g.g.v[k].y;
+                const float fx = gx * sc[k], fy = gy * sc[k];
+                o.v[k] = make_float2(q[k].x - fx / g.den[k], q[k].y - fy / g.den[k]);
+            }
+        }
+        return o;
+    };
+    const bool in1 = x + 1 < dimx;
+    auto mag = [](float a, float b) { return __builtin_amdgcn_sqrtf(a * a + b * b); };
+    auto norms = [&](const Row<2> &nw, const Row<2> &od, float &sd, float &sp) {
+        sd += mag(nw.v[0].x - od.v[0].x, nw.v[0].y - od.v[0].y);
+        sp += mag(od.v[0].x, od.v[0].y);
+        const float d1 = mag(nw.v[1].x - od.v[1].x, nw.v[1].y - od.v[1].y);
+        const float p1 = mag(od.v[1].x, od.v[1].y);
+        sd += in1 ? d1 : 0.0f;
+        sp += in1 ? p1 : 0.0f;
+    };
+    // band march in direction D (ALT: odd waves upward, as jacobi3_kernel)
+    auto march = [&](auto dirc) __attribute__((always_inline)) {
+        constexpr int D = decltype(dirc)::value;
+        const int n = jend - jbeg;
+        auto J = [&](int sp) { return D > 0 ? jbeg + sp : jend - 1 - sp; };
+        auto S = [&](int sp, const Row<2> &bh, const Row<2> &c, const Row<2> &ah, const G &g) {
+            return D > 0 ? stepr(J(sp), bh, c, ah, g) : stepr(J(sp), ah, c, bh, g);
+        };
+        // each iteration's Logger norms are taken where its row is produced
+        // (iteration 1 at position sp+3, 2 at sp+2, 3 at sp+1, 4 at sp)
+        Row<2> uj2, uj3;  // u0 at positions sp+2 .. sp+3
+        Row<2> vj1, vj2;  // u1 at sp+1 .. sp+2
+        Row<2> wj, wj1;   // u2 at sp .. sp+1
+        Row<2> xm1, xj;   // u3 at sp-1 .. sp
+        G gj, gj1, gj2;   // gradients at sp .. sp+2
+        {
+            const Row<2> a0 = ldu(J(-4)), a1 = ldu(J(-3)), a2 = ldu(J(-2)), a3 = ldu(J(-1));
+            const Row<2> uj = ldu(J(0)), uj1 = ldu(J(1));
+            uj2 = ldu(J(2));
+            uj3 = ldu(J(3));
+            const G gm3 = ldg(J(-3)), gm2 = ldg(J(-2)), gm1 = ldg(J(-1));
+            gj = ldg(J(0));
+            gj1 = ldg(J(1));
+            gj2 = ldg(J(2));
+            const Row<2> pm3 = S(-3, a0, a1, a2, gm3);
+            const Row<2> pm2 = S(-2, a1, a2, a3, gm2);
+            const Row<2> pm1 = S(-1, a2, a3, uj, gm1);
+            const Row<2> vj = S(0, a3, uj, uj1, gj);
+            vj1 = S(1, uj, uj1, uj2, gj1);
+            vj2 = S(2, uj1, uj2, uj3, gj2);
+            const Row<2> qm2 = S(-2, pm3, pm2, pm1, gm2);
+            const Row<2> qm1 = S(-1, pm2, pm1, vj, gm1);
+            wj = S(0, pm1, vj, vj1, gj);
+            wj1 = S(1, vj, vj1, vj2, gj1);
+            xm1 = S(-1, qm2, qm1, wj, gm1);
+            xj = S(0, qm1, wj, wj1, gj);
+            if (own) {
+                norms(vj, uj, s1d, s1p);
+                norms(wj, vj, s2d, s2p);
+                norms(xj, wj, s3d, s3p);
+                if (1 < n) {
+                    norms(vj1, uj1, s1d, s1p);
+                    norms(wj1, vj1, s2d, s2p);
+                }
+                if (2 < n) norms(vj2, uj2, s1d, s1p);
+            }
+        }
+        Row<2> nu = ldu(J(4));
+        GR ng = ldgr(J(3));
+        auto body = [&](int sp, bool pref) __attribute__((always_inline)) {
+            const Row<2> a4 = nu;
+            const G gj3 = fin(ng);
+            if (pref) {
+                nu = ldu(J(sp + 5));
+                ng = ldgr(J(sp + 4));
+            }
+            const Row<2> vj3 = S(sp + 3, uj2, uj3, a4, gj3);  // u1
+            const Row<2> wj2 = S(sp + 2, vj1, vj2, vj3, gj2);  // u2
+            const Row<2> xj1 = S(sp + 1, wj, wj1, wj2, gj1);   // u3
+            const Row<2> z = S(sp, xm1, xj, xj1, gj);          // u4
+            if (own) {
+                if (sp + 3 < n) norms(vj3, uj3, s1d, s1p);
+                if (sp + 2 < n) norms(wj2, vj2, s2d, s2p);
+                if (sp + 1 < n) norms(xj1, wj1, s3d, s3p);
+                norms(z, xj, s4d, s4p);
+                float2 *dst = un + (long)J(sp) * P + x;
+                if (x + 2 <= dimx)
+                    st4<true>(reinterpret_cast<float4 *>(dst),
+                              make_float4(z.v[0].x, z.v[0].y, z.v[1].x, z.v[1].y));
+                else
+                    dst[0] = z.v[0];
+            }
+            uj2 = uj3;
+            uj3 = a4;
+            vj1 = vj2;
+            vj2 = vj3;
+            wj = wj1;
+            wj1 = wj2;
+            xm1 = xj;
+            xj = xj1;
+            gj = gj1;
+            gj1 = gj2;
+            gj2 = gj3;
+        };
+        int sp = 0;
+        for (; sp + UNR < n; sp += UNR) {
+            progress_prio<PRIO>(sp, n);
+#pragma unroll
+            for (int k = 0; k < UNR; k++) body(sp + k, true);
+        }
+        for (; sp < n; ++sp) body(sp, sp + 1 < n);
+    };
+    if (jbeg < jend) {
+        if (ALT && (wave & 1))
+            march(std::integral_constant<int, -1>{});
+        else
+            march(std::integral_constant<int, 1>{});
+    }
+    double d[8] = {s1d, s1p, s2d, s2p, s3d, s3p, s4d, s4p};
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1)
+#pragma unroll
+        for (int q = 0; q < 8; q++) d[q] += __shfl_down(d[q], off);
+    __shared__ double red[8][WAVES];
+    if (lane == 0)
+#pragma unroll
+        for (int q = 0; q < 8; q++) red[q][wave] = d[q];
+    if (__any(bad) && lane == 0) atomicOr(status, kStatusDivZero);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double r[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+        for (int w = 0; w < WAVES; ++w)
+#pragma unroll
+            for (int q = 0; q < 8; q++) r[q] += red[q][w];
+        const long blk = (long)band * gx + bx;
+        partial[2 * blk] = r[0];
+        partial[2 * blk + 1] = r[1];
+        partial2[2 * blk] = r[2];
+        partial2[2 * blk + 1] = r[3];
+        partial3[2 * blk] = r[4];
+        partial3[2 * blk + 1] = r[5];
+        partial4[2 * blk] = r[6];
+        partial4[2 * blk + 1] = r[7];
     }
 }
 
