@@ -3,15 +3,18 @@
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--grid G] [--weak]
 
-One step = one Horn-Schunck iteration of the reference loop
-(ImageRegistrationOpticalFlow.cpp:123-135): OpticalFlowDiffusion::get_update +
-the Logger norms over the whole grid, the per-chunk norm reduction, and — for
-N > 1 — the RCCL halo exchange.  Iterations run in threes fused into one pass
-over HBM (hs::jacobi3_kernel: 28 B/px per launch, three iterations per launch,
+One step = one pass of the hot path: the Horn-Schunck iteration loop of
+ImageRegistrationOpticalFlow::estimate_motion_at_current_resolution
+(ImageRegistrationOpticalFlow.cpp:123-135) over the whole grid with BASELINE
+config 2's 1000 Jacobi iterations (--iters-per-step), each iteration
+OpticalFlowDiffusion::get_update + the Logger norms, plus the per-chunk norm
+reductions, the read-back of the loop's Logger errors and motion_est->reset()
+(:141), and — for N > 1 — the RCCL halo exchanges.  Iterations run in threes
+fused into one pass over HBM (hs::jacobi3_kernel: 28 B/px per launch, three iterations per launch,
 bit-identical to three single steps; chunks of 33 iterations are eleven
 launches, and a single step or a pair fills the run's tail), with a three-j-line
 halo exchange per launch overlapped with the interior bands.  Early exit is
-disabled (fixed_iters) so that exactly K iterations run.
+disabled (fixed_iters) so that exactly K x 1000 iterations run.
 
 Workloads (BASELINE.json configs):
   N = 1 (default --grid 4096)   config 2: Horn-Schunck 4096^2 fp32 on one GPU
@@ -24,11 +27,12 @@ Workloads (BASELINE.json configs):
 
 Per-run setup stays outside the timed region, as in the reference's own loop:
 the gradients and the divide-by-zero test run in set_images (once per image
-pair), the Logger sums of the K-step run are reserved before the warm-up, and
+pair), the Logger sums of a loop are reserved before the warm-up, and
 the zeroing of the next run's start buffer (motion_est->reset(),
 ImageRegistrationOpticalFlow.cpp:141) is enqueued at the end of the previous
-run.  The timed region is exactly K iterations plus the final read-back of
-their Logger sums.
+run.  The timed region is exactly K loops of 1000 iterations, each followed
+by the read-back of its Logger sums (one host synchronisation per loop, as the
+reference returns to its caller after every loop).
 
 Inputs are a synthetic procedural texture pair generated per slab.  For N > 1
 launch with torch.distributed.run (one process per GPU); torch.distributed
@@ -50,22 +54,28 @@ sys.path.insert(0, ROOT)
 
 METRIC = "Mpixel-iterations/sec + achieved HBM GB/s, Horn-Schunck 4096^2 @ 1/2/4/8 GPU"
 BYTES_PER_PX_IT = 28  # read u 8 + dI 8 + It 4, write u 8
-# the fused kernel moves those 28 B/px once per launch and advances THREE iterations
-BYTES_PER_PX_LAUNCH = 28
+# the fused kernel reads u 8 + dI 8 + It 4 and writes u 8 B/px once per launch
+# and advances THREE iterations; once dI + It no longer fit in the MALL it
+# derives dI from Iaux in the kernel and reads Iaux 4 instead of dI 8
+BYTES_PER_PX_LAUNCH = {"image": 24, "field": 28}
 ITERS_PER_LAUNCH = 3
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s peak (spec)
 ALPHA = 0.1
-KERNEL = "of2d::hs::jacobi3_kernel<0,4,true,4,4,1,true>"
+KERNEL = {"image": "of2d::hs::jacobi3_kernel<0,4,true,4,4,1,true,true> (gradients from Iaux)",
+          "field": "of2d::hs::jacobi3_kernel<0,4,true,4,4,1,true,false> (gradients read from dI)"}
 TRAFFIC_PROFILE = os.path.join("profiles", "hs_traffic.json")
 
 
 def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    # the default warm-up runs past the clock transient of the first ~40 ms of
-    # sustained load (profiles/r01_v14_bench_warmup.log: W=50 times the dip)
-    ap.add_argument("--steps", type=int, default=3000)
-    ap.add_argument("--warmup", type=int, default=1500)
+    # a step is a 1000-iteration loop (28 ms at 4096^2): even the driver's W=5
+    # runs past the clock transient of the first ~40 ms of sustained load
+    # (profiles/r01_v14_bench_warmup.log)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--iters-per-step", type=int, default=1000,
+                    help="Jacobi iterations per step (config 2: 1000)")
     ap.add_argument("--grid", type=int, default=0,
                     help="global grid G x G (default: 4096 at N=1 = config 2, "
                          "16384 at N>1 = config 5)")
@@ -77,6 +87,10 @@ def parse_args(argv=None):
                     help="threads of the all-cores CPU baseline (default: OMP_NUM_THREADS, "
                          "else every CPU)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--gradients", choices=["auto", "image", "field"], default="auto",
+                    help="triple kernel: derive dI from Iaux in the kernel (image, 24 B/px "
+                         "per launch) or read the stored field dI (field, 28 B/px); auto "
+                         "(default): image once dI + It exceed the 256 MB MALL")
     ap.add_argument("--timing-launches", type=int, default=200)
     ap.add_argument("--rccl", action="store_true",
                     help="N = 1: run the Logger all-reduces through a one-rank RCCL communicator")
@@ -151,7 +165,7 @@ def cpu_baseline(size: int, iters: int, threads: int) -> dict:
                                     f"{threads} OpenMP threads over j-lines, {dtn:.1f} s"}}
 
 
-def load_traffic(dimx: int, rows: int):
+def load_traffic(dimx: int, rows: int, gradients: str = "field"):
     """PMC traffic per launch from the committed profile, only for the grid it
     was measured on (it is not measured inside this run)."""
     p = os.path.join(ROOT, TRAFFIC_PROFILE)
@@ -159,20 +173,23 @@ def load_traffic(dimx: int, rows: int):
         t = json.load(open(p))
     except Exception:
         return None
-    if list(t.get("grid", [])) != [dimx, rows]:
+    if list(t.get("grid", [])) != [dimx, rows] or t.get("gradients", "field") != gradients:
         return None
     return t
 
 
 def make_record(*, world, wl, steps, warmup, elapsed, gpu_ms, avg_us, iso_us, px_rank, info,
-                traffic, cpu, rows_per_rank):
+                loop_us=None, avg_n=0,
+                traffic, cpu, rows_per_rank, iters_per_step=1, gradients="image"):
     """The JSON line (bench.py contract + roofline + cpu_baseline)."""
     dimx, dimy = wl["dimx"], wl["dimy"]
     total_px = dimx * dimy
-    achieved = BYTES_PER_PX_LAUNCH * px_rank / (avg_us * 1e-6) / 1e9
+    bpl = BYTES_PER_PX_LAUNCH[gradients]
+    achieved = bpl * px_rank / (avg_us * 1e-6) / 1e9
+    iters = steps * iters_per_step
     return {
         "metric": METRIC,
-        "value": round(total_px * steps / elapsed / 1e6, 1),
+        "value": round(total_px * iters / elapsed / 1e6, 1),
         "unit": "Mpx-it/s",
         "n_gpus": world,
         "steps": steps,
@@ -187,7 +204,10 @@ def make_record(*, world, wl, steps, warmup, elapsed, gpu_ms, avg_us, iso_us, px
             "workload": wl["workload"],
             "grid": [dimx, dimy],
             "alpha": ALPHA,
-            "iterations": steps,
+            "step": (f"one HS iteration loop of {iters_per_step} fixed Jacobi iterations "
+                     "(ImageRegistrationOpticalFlow.cpp:123-135) + its Logger read-back"),
+            "iterations_per_step": iters_per_step,
+            "iterations": iters,
             "fixed_iters": True,
             "parallelism": f"row-slab x{world}",
             "rows_per_rank": rows_per_rank,
@@ -199,15 +219,15 @@ def make_record(*, world, wl, steps, warmup, elapsed, gpu_ms, avg_us, iso_us, px
             "gpu_ms_rank0": round(gpu_ms, 3),
             "wall_over_gpu_rank0": round(elapsed * 1000.0 / gpu_ms, 4) if gpu_ms > 0 else None,
             # the path's own algorithmic traffic (28 B/px per fused launch) per GPU
-            "hbm_GBps_from_step_time": round(BYTES_PER_PX_LAUNCH * total_px * steps
+            "hbm_GBps_from_step_time": round(bpl * total_px * iters
                                              / ITERS_PER_LAUNCH / elapsed / 1e9 / world, 1),
             # the reference algorithm's 28 B per pixel-iteration at this rate
-            "ref_bytes_GBps_equiv": round(BYTES_PER_PX_IT * total_px * steps
+            "ref_bytes_GBps_equiv": round(BYTES_PER_PX_IT * total_px * iters
                                           / elapsed / 1e9 / world, 1),
         },
         "roofline": {
             "bound": "hbm",
-            "kernel": KERNEL,
+            "kernel": KERNEL[gradients],
             "scope": "per GPU (rank 0's slab)",
             "iterations_per_launch": ITERS_PER_LAUNCH,
             "achieved": round(achieved, 1),
@@ -215,10 +235,13 @@ def make_record(*, world, wl, steps, warmup, elapsed, gpu_ms, avg_us, iso_us, px
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "avg_launch_us": round(avg_us, 3),
-            "avg_launch_source": "HIP events around the timed run on the solver's stream "
-                                 "(gpu ms x 3 / steps)",
+            "avg_launch_source": ("HIP events on the solver's stream around each chunk's "
+                                  "back-to-back triple launches inside the timed loops "
+                                  f"({avg_n} launches)"),
+            "loop_us_per_3_iterations": round(loop_us, 3) if loop_us else None,
             "isolated_launch_us": round(iso_us, 3),
-            "bytes_per_launch": BYTES_PER_PX_LAUNCH * px_rank,
+            "bytes_per_launch": bpl * px_rank,
+            "bytes_per_px_launch": bpl,
             "traffic": (traffic or {}).get("bytes_per_launch"),
             "traffic_source": (f"{TRAFFIC_PROFILE} (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, "
                                "committed profile of this kernel at this grid; not measured "
@@ -272,8 +295,12 @@ def main():
     ref, mov = S.procedural_pair(dimx, lo, hi)
     solver.set_images(ref, mov)
     del ref, mov
-    solver.reserve(max(args.steps, args.warmup))
+    solver.set_option("hs_gradients_from_image",
+                      {"auto": -1, "image": 1, "field": 0}[args.gradients])
+    ips = args.iters_per_step
+    solver.reserve(ips)
     info = solver.info()
+    gradients = "image" if info.get("gradients_from_image") else "field"
 
     def barrier():
         if dist is not None:
@@ -285,27 +312,36 @@ def main():
         except Exception:
             pass
 
-    if args.warmup > 0:
-        solver.run(args.warmup, fixed_iters=True)
+    for _ in range(args.warmup):
+        solver.run(ips, fixed_iters=True)
     barrier()
+    gpu_ms = 0.0
+    done = 0
+    tri_us, tri_n = 0.0, 0
     t0 = time.perf_counter()
-    done = solver.run(args.steps, fixed_iters=True)  # returns after the stream is drained
+    for _ in range(args.steps):
+        done += solver.run(ips, fixed_iters=True)  # returns after the stream is drained
+        gpu_ms += solver.last_run_ms()
+        us, n = solver.last_run_kernel_us()
+        tri_us += us * n
+        tri_n += n
     t1 = time.perf_counter()
     barrier()
     elapsed = t1 - t0
-    gpu_ms = solver.last_run_ms()
     if dist is not None:
         import torch
         t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    assert done == args.steps
+    assert done == args.steps * ips
 
-    # dominant kernel: average duration per launch over the timed region, from
-    # the HIP events the solver records around the run on its own stream (the
-    # run is triple launches except a pair / single step per run tail; the
-    # per-chunk partial reductions between them are included)
-    avg_us = gpu_ms * 1000.0 * ITERS_PER_LAUNCH / args.steps
+    # dominant kernel: its own average duration per launch inside the timed
+    # loops, from the HIP events the solver records on its stream around each
+    # chunk's back-to-back triple launches (the per-chunk partial reductions
+    # and the loop's single-step tail are outside them)
+    avg_us = tri_us / tri_n if tri_n else gpu_ms * 1000.0 * ITERS_PER_LAUNCH / (args.steps * ips)
+    # per iteration over the whole loop (reductions and tail included)
+    loop_us = gpu_ms * 1000.0 * ITERS_PER_LAUNCH / (args.steps * ips)
     # and back-to-back launches of the kernel alone, after the run
     iso_us = solver.time_kernel(args.timing_launches)
     rows = solver.row_end - solver.row_begin
@@ -319,8 +355,10 @@ def main():
             cpu = cpu_baseline(dimx, cpu_it, cpu_threads(args))
         rec = make_record(world=world, wl=wl, steps=args.steps, warmup=args.warmup,
                           elapsed=elapsed, gpu_ms=gpu_ms, avg_us=avg_us, iso_us=iso_us,
-                          px_rank=px_rank, info=info, traffic=load_traffic(dimx, rows),
-                          cpu=cpu, rows_per_rank=rows)
+                          loop_us=loop_us, avg_n=tri_n,
+                          px_rank=px_rank, info=info, traffic=load_traffic(dimx, rows, gradients),
+                          cpu=cpu, rows_per_rank=rows, iters_per_step=ips,
+                          gradients=gradients)
         print(json.dumps(rec), flush=True)
     solver.close()
     if dist is not None:

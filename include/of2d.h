@@ -146,13 +146,24 @@ int of2d_slab_get_motion(of2d_slab *s, double *out);
  * launched on.  The launches read the zeroed start buffer and write scratch:
  * the last run's motion (of2d_slab_get_motion) is left intact. */
 int of2d_slab_time_kernel(of2d_slab *s, int nlaunch, double *avg_us);
-/* slab facts for reports: info[0..8] = {nranks, ranks of the RCCL
+/* slab facts for reports: info[0..9] = {nranks, ranks of the RCCL
  * communicator (ncclCommCount; 0 without one), in-process group (0/1),
  * row_begin, row_end, dimx, pitch (elements), halo j-lines exchanged per fused
- * launch, interior/edge split (0/1)}; returns the number of entries written */
+ * launch, interior/edge split (0/1), triple kernel derives dI from Iaux (0/1)};
+ * returns the number of entries written */
 int of2d_slab_info(const of2d_slab *s, int *info, int n);
 /* wall time (ms, HIP events) of the last of2d_slab_run on this rank */
 int of2d_slab_last_run_ms(const of2d_slab *s, double *ms);
+/* the triple kernel's own average launch time (us) inside the last run,
+ * from HIP events bracketing the back-to-back triple launches of each of its
+ * first 64 chunks on the solver's stream (halo exchange included for N > 1),
+ * and the number of launches that average covers */
+int of2d_slab_last_run_kernel_us(const of2d_slab *s, double *avg_us, int *nlaunch);
+/* tuning switches (no reference counterpart; results are bit-identical either way):
+ *   "hs_gradients_from_image" (-1 auto = default, 0, 1): the triple kernel
+ *   derives dI from Iaux in the kernel (24 B/px per launch) instead of reading
+ *   dI (28); auto does so when dI + It (12 B/px) exceed the 256 MB MALL */
+int of2d_slab_set_option(of2d_slab *s, const char *key, double value);
 int of2d_slab_destroy(of2d_slab *s);
 const char *of2d_slab_last_error(const of2d_slab *s);
 /* In-process slab group: the nranks slabs of one grid in ONE process, driven by

@@ -561,15 +561,25 @@ __device__ __forceinline__ void progress_prio(int done, int total) {
 // with one direction the halo rows of a band boundary are read a whole band
 // apart, from HBM twice.  The stencil is symmetric in j and every output
 // depends only on input values: bit-identical either way.
+// GI: the gradients are not read from dI but derived in the kernel from the
+// image they were taken of, Iaux (IterativeSolver::spatial_derivative,
+// IterativeSolver.cpp:22-56, gradients.h:9-32: the same float operations, so
+// the same bits as dI): per row step one Iaux row (4 B/px) replaces one dI row
+// (8 B/px), 24 instead of 28 B per pixel and launch.  The x-neighbours of a
+// lane's two Iaux px come by DPP from the adjacent lanes like those of u; the
+// j-neighbours are the Iaux rows before and after in the march.  Iaux needs
+// the same ghost j-lines as u (rows glo .. ghi-1 readable).  Worth it when dI
+// and It do not stay resident in the 256 MB MALL between launches (the
+// launchers' callers decide, of2d_device.h hs3_gradients_from_image).
 template <int ROWS, int WAVES, bool XCD = true, int MINB = 1, int UNR = 4, int PRIO = 0,
-          bool ALT = false>
+          bool ALT = false, bool GI = false>
 __global__ __launch_bounds__(64 * WAVES, MINB) void jacobi3_kernel(
     const float2 *__restrict__ uo, float2 *__restrict__ un, const float2 *__restrict__ dI,
     const float *__restrict__ It, int P, int dimx, int nrows, int row0, int dimy, float alphasq,
     int glo, int ghi, double *__restrict__ partial, double *__restrict__ partial2,
     double *__restrict__ partial3, unsigned *__restrict__ status, int band0, int gx, int gy,
     int rows = ROWS, const unsigned *__restrict__ range_flag = nullptr, int jlo = -1,
-    int jhi = -1) {
+    int jhi = -1, const float *__restrict__ Ia = nullptr) {
     int bx = (int)blockIdx.x, by = (int)blockIdx.y;
     if constexpr (XCD) {
         if (!xcd_block(gx, gy, bx, by)) return;
@@ -605,6 +615,13 @@ __global__ __launch_bounds__(64 * WAVES, MINB) void jacobi3_kernel(
     };
     // the gradient field is in the unscaled-division range (hs_precheck_kernel)
     const bool grange = range_flag && *range_flag == 0;
+    // GI: raw rows of Iaux and It
+    auto ldia = [&](int j) {
+        return ld2<false>(reinterpret_cast<const float2 *>(Ia + (long)cl(j) * P + xl));
+    };
+    auto ldit = [&](int j) {
+        return ld2<false>(reinterpret_cast<const float2 *>(It + (long)cl(j) * P + xl));
+    };
     auto ldg = [&](int j) {
         G r;
         r.g = load_row<2, false>(dI + (long)cl(j) * P, xl);
@@ -621,6 +638,46 @@ __global__ __launch_bounds__(64 * WAVES, MINB) void jacobi3_kernel(
     // any lane of this wave on an x-border pixel: wave-uniform
     const bool xedge_w = __builtin_amdgcn_ballot_w64(x == 0 || x == dimx - 1 || x + 1 == 0 ||
                                                      x + 1 == dimx - 1) != 0;
+    // GI: the gradient row of j-line j from the Iaux rows j-1 (im), j (ic),
+    // j+1 (ip) and the It row (t); the border rule of gradients.h:9-32 with
+    // the global j
+    auto mkg = [&](int j, float2 im, float2 ic, float2 ip, float2 t) {
+        G r;
+        const float lft = dpp_from_left(ic.y);   // Iaux[x - 1]
+        const float rgt = dpp_from_right(ic.x);  // Iaux[x + 2]
+        // partial_x: (f[i+1] - f[i-1]) / 2.0f, one-sided at i = 0 / dimx - 1
+        float gx0 = (ic.y - lft) / 2.0f, gx1 = (rgt - ic.x) / 2.0f;
+        if (xedge_w) {
+            if (x == 0)
+                gx0 = ic.y - ic.x;
+            else if (x == dimx - 1)
+                gx0 = ic.x - lft;
+            if (x + 1 == dimx - 1) gx1 = ic.y - ic.x;
+        }
+        // partial_y with the global j-line (wave-uniform)
+        const int jg = row0 + j;
+        float gy0, gy1;
+        if (jg == 0) {
+            gy0 = ip.x - ic.x;
+            gy1 = ip.y - ic.y;
+        } else if (jg == dimy - 1) {
+            gy0 = ic.x - im.x;
+            gy1 = ic.y - im.y;
+        } else {
+            gy0 = (ip.x - im.x) / 2.0f;
+            gy1 = (ip.y - im.y) / 2.0f;
+        }
+        r.g.v[0] = make_float2(gx0, gy0);
+        r.g.v[1] = make_float2(gx1, gy1);
+        r.t[0] = t.x;
+        r.t[1] = t.y;
+#pragma unroll
+        for (int k = 0; k < 2; k++) {
+            r.den[k] = (alphasq + r.g.v[k].x * r.g.v[k].x) + r.g.v[k].y * r.g.v[k].y;
+            r.rcp[k] = recip_refined(r.den[k]);
+        }
+        return r;
+    };
     auto stepr_opt = [&](int j, const Row<2> &m, const Row<2> &c, const Row<2> &p, const G &g) {
         // (l + r) per component with the lane shift folded into the add
         // (the empty asm keeps the SLP vectorizer from pairing x and y into a
@@ -696,8 +753,28 @@ __global__ __launch_bounds__(64 * WAVES, MINB) void jacobi3_kernel(
         unsigned bx_ = 0;  // halo rows: flagged by the waves that own them
         const Row<2> a0 = ldu(J(-3)), a1 = ldu(J(-2)), a2 = ldu(J(-1));
         Row<2> uj = ldu(J(0)), uj1 = ldu(J(1)), uj2 = ldu(J(2));
-        const G gm2 = ldg(J(-2)), gm1 = ldg(J(-1));
-        G gj = ldg(J(0)), gj1 = ldg(J(1));
+        // GI: the gradient row at position sp from the Iaux rows at positions
+        // sp-1 (behind), sp, sp+1 (ahead), in j order by direction
+        auto MG = [&](int sp, float2 bh, float2 c, float2 ah, float2 t) {
+            return D > 0 ? mkg(J(sp), bh, c, ah, t) : mkg(J(sp), ah, c, bh, t);
+        };
+        G gm2, gm1, gj, gj1;
+        float2 i1, i2, i3, nt;  // GI: Iaux at positions sp+1, sp+2, sp+3; It at sp+2
+        if constexpr (GI) {
+            const float2 im3 = ldia(J(-3)), im2 = ldia(J(-2)), im1 = ldia(J(-1)),
+                         i0 = ldia(J(0));
+            i1 = ldia(J(1));
+            i2 = ldia(J(2));
+            gm2 = MG(-2, im3, im2, im1, ldit(J(-2)));
+            gm1 = MG(-1, im2, im1, i0, ldit(J(-1)));
+            gj = MG(0, im1, i0, i1, ldit(J(0)));
+            gj1 = MG(1, i0, i1, i2, ldit(J(1)));
+        } else {
+            gm2 = ldg(J(-2));
+            gm1 = ldg(J(-1));
+            gj = ldg(J(0));
+            gj1 = ldg(J(1));
+        }
         // u1 at positions -2 .. 1, u2 at -1, 0
         const Row<2> p0 = S(-2, a0, a1, a2, gm2, bx_);
         const Row<2> p1 = S(-1, a1, a2, uj, gm1, bx_);
@@ -706,15 +783,33 @@ __global__ __launch_bounds__(64 * WAVES, MINB) void jacobi3_kernel(
         Row<2> wm1 = S(-1, p0, p1, vj, gm1, bx_);
         Row<2> wj = S(0, p1, vj, vj1, gj, bx_);
         Row<2> nu = ldu(J(3));
-        G ng = ldg(J(2));
+        G ng;
+        if constexpr (GI) {
+            i3 = ldia(J(3));
+            nt = ldit(J(2));
+        } else {
+            ng = ldg(J(2));
+        }
         // one output row; the window shifts by renaming, which the unrolled
         // copies below turn into register renames instead of moves
         auto body = [&](int sp, bool pref) __attribute__((always_inline)) {
             const Row<2> a3 = nu;  // u at position sp+3
-            const G gj2 = ng;      // gradients at position sp+2
+            G gj2;                 // gradients at position sp+2
+            if constexpr (GI) {
+                gj2 = MG(sp + 2, i1, i2, i3, nt);
+                i1 = i2;
+                i2 = i3;
+            } else {
+                gj2 = ng;
+            }
             if (pref) {
                 nu = ldu(J(sp + 4));
-                ng = ldg(J(sp + 3));
+                if constexpr (GI) {
+                    i3 = ldia(J(sp + 4));
+                    nt = ldit(J(sp + 3));
+                } else {
+                    ng = ldg(J(sp + 3));
+                }
             }
             unsigned b1 = 0, b3 = 0;
             const Row<2> vj2 = S(sp + 2, uj1, uj2, a3, gj2, b1);  // u1

@@ -64,12 +64,14 @@ void launch_hs_jacobi2(const float2 *u_old, float2 *u_new, const float2 *dI, con
 // march directions, so the waves on either side of a band boundary read its
 // halo j-lines together (83.8 -> 82.9 us, tools/hs_variants opt)
 static const auto kHsJacobi3 = &hs::jacobi3_kernel<0, kHs3Waves, true, 4, 4, 1, true>;
+// the same with the gradients derived from Iaux in the kernel (GI: 24 B/px)
+static const auto kHsJacobi3I = &hs::jacobi3_kernel<0, kHs3Waves, true, 4, 4, 1, true, true>;
 
 void launch_hs_jacobi3(const float2 *u_old, float2 *u_new, const float2 *dI, const float *It,
                        int P, int dimx, int nrows, int row0, int dimy, float alphasq, int glo,
                        int ghi, double *partial, double *partial2, double *partial3,
                        unsigned *status, const unsigned *range_flag, hipStream_t st,
-                       int band_lo, int band_hi) {
+                       int band_lo, int band_hi, const float *Ia) {
     if (P % kHsStrip != 0 || nrows <= 0 || dimx > P || dimx < 2 || glo > -1 || ghi < nrows + 1)
         throw std::invalid_argument("launch_hs_jacobi3: bad geometry");
     if (!range_flag) throw std::invalid_argument("launch_hs_jacobi3: no range flag");
@@ -81,10 +83,10 @@ void launch_hs_jacobi3(const float2 *u_old, float2 *u_new, const float2 *dI, con
     dim3 g = hs3_grid(dimx, nrows);
     g.y = band_hi - band_lo;
     const dim3 gl(8 * ((g.x * g.y + 7) / 8));
-    hipLaunchKernelGGL(kHsJacobi3, gl, dim3(64 * kHs3Waves), 0, st, u_old, u_new, dI, It, P,
-                       dimx, nrows, row0, dimy, alphasq, glo, ghi, partial, partial2, partial3,
-                       status, band_lo, (int)g.x, (int)g.y, hs3_rows(dimx, nrows), range_flag, -1,
-                       -1);
+    hipLaunchKernelGGL(Ia ? kHsJacobi3I : kHsJacobi3, gl, dim3(64 * kHs3Waves), 0, st, u_old,
+                       u_new, dI, It, P, dimx, nrows, row0, dimy, alphasq, glo, ghi, partial,
+                       partial2, partial3, status, band_lo, (int)g.x, (int)g.y,
+                       hs3_rows(dimx, nrows), range_flag, -1, -1, Ia);
     OF2D_HIP(hipGetLastError());
 }
 
@@ -93,7 +95,7 @@ int launch_hs_jacobi3_window(const float2 *u_old, float2 *u_new, const float2 *d
                              float alphasq, int glo, int ghi, int jlo, int jhi,
                              int rows_per_wave, int slot_band0, double *partial,
                              double *partial2, double *partial3, unsigned *status,
-                             const unsigned *range_flag, hipStream_t st) {
+                             const unsigned *range_flag, hipStream_t st, const float *Ia) {
     if (P % kHsStrip != 0 || nrows <= 0 || dimx > P || dimx < 2 || glo > -1 || ghi < nrows + 1 ||
         jlo < 0 || jhi > nrows || jlo >= jhi || rows_per_wave < 1 || slot_band0 < 0)
         throw std::invalid_argument("launch_hs_jacobi3_window: bad geometry");
@@ -102,9 +104,10 @@ int launch_hs_jacobi3_window(const float2 *u_old, float2 *u_new, const float2 *d
     const int per_band = kHs3Waves * rows_per_wave;
     const int gy = (jhi - jlo + per_band - 1) / per_band;
     const dim3 gl(8 * ((gx * gy + 7) / 8));
-    hipLaunchKernelGGL(kHsJacobi3, gl, dim3(64 * kHs3Waves), 0, st, u_old, u_new, dI, It, P,
-                       dimx, nrows, row0, dimy, alphasq, glo, ghi, partial, partial2, partial3,
-                       status, slot_band0, gx, gy, rows_per_wave, range_flag, jlo, jhi);
+    hipLaunchKernelGGL(Ia ? kHsJacobi3I : kHsJacobi3, gl, dim3(64 * kHs3Waves), 0, st, u_old,
+                       u_new, dI, It, P, dimx, nrows, row0, dimy, alphasq, glo, ghi, partial,
+                       partial2, partial3, status, slot_band0, gx, gy, rows_per_wave, range_flag,
+                       jlo, jhi, Ia);
     OF2D_HIP(hipGetLastError());
     return gy;
 }

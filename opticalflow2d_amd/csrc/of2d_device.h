@@ -132,11 +132,24 @@ inline int hs3_nblocks(int dimx, int nrows) {
 }
 // range_flag: the word launch_hs_precheck wrote for this dI (required: the
 // kernel leaves the divide-by-zero test to it)
+// The triple kernel reads dI + It (12 B/px) at every launch.  While both fit
+// in the 256 MB MALL (Infinity Cache) they stay resident between launches
+// and reading them costs no HBM bandwidth; past that the launch is HBM-bound
+// and deriving dI from Iaux in the kernel (GI, 4 B/px instead of 8) saves a
+// seventh of its bytes.  Measured per launch (profiles/r02_d_gi_pf_ab*.log):
+// 4096^2 81.4 (dI) vs 81.1 us (GI), 16384^2 1553 vs 1335 us.
+constexpr double kMallBytes = 256.0 * 1024 * 1024;
+inline bool hs3_gradients_from_image(int dimx, int nrows) {
+    return 12.0 * dimx * nrows > kMallBytes;
+}
+// Ia (Iaux, the image dI was taken of) non-null: the kernel derives the
+// gradients from it (24 instead of 28 B/px per launch, same bits); null: it
+// reads dI
 void launch_hs_jacobi3(const float2 *u_old, float2 *u_new, const float2 *dI, const float *It,
                        int P, int dimx, int nrows, int row0, int dimy, float alphasq, int glo,
                        int ghi, double *partial, double *partial2, double *partial3,
                        unsigned *status, const unsigned *range_flag, hipStream_t st,
-                       int band_lo = -1, int band_hi = -1);
+                       int band_lo = -1, int band_hi = -1, const float *Ia = nullptr);
 // Once per gradient field, before the triple kernel runs on it
 // (hs_jacobi_impl.h hs_precheck_kernel): zeroes *range_flag, then sets it if
 // any gradient / denominator of the allocation [base, base + count) lies
@@ -151,7 +164,8 @@ int launch_hs_jacobi3_window(const float2 *u_old, float2 *u_new, const float2 *d
                              float alphasq, int glo, int ghi, int jlo, int jhi,
                              int rows_per_wave, int slot_band0, double *partial,
                              double *partial2, double *partial3, unsigned *status,
-                             const unsigned *range_flag, hipStream_t st);
+                             const unsigned *range_flag, hipStream_t st,
+                             const float *Ia = nullptr);
 void launch_hs_precheck(const float2 *base, size_t count, int P, int ghost, int dimx, int dimy,
                         float alphasq, unsigned *range_flag, unsigned *status, hipStream_t st);
 constexpr int kRangeFlagWord = 32;  // word of the 64-word status buffers holding range_flag

@@ -396,8 +396,11 @@ int Registration::loop_hs(Level &L, int niter, float alpha, int &final_buf) {
         })
               : StepFn2(),
         pairs ? StepFn3([&](const float2 *src, float2 *dst, double *p1, double *p2, double *p3) {
+            // past the MALL the gradients are derived from Iaux in the kernel
+            // (dI was taken of it; hs3_gradients_from_image)
             launch_hs_jacobi3(src, dst, L.dI.p, L.It.p, L.P, L.dx, L.dy, 0, L.dy, alphasq, -1,
-                              L.dy + 1, p1, p2, p3, d_status_, range_flag, st_);
+                              L.dy + 1, p1, p2, p3, d_status_, range_flag, st_, -1, -1,
+                              hs3_gradients_from_image(L.dx, L.dy) ? L.Iaux.p : nullptr);
         })
               : StepFn3(),
         nblk);

@@ -68,6 +68,9 @@ struct of2d_slab {
     int chunk = 33;  // eleven fused triples per chunk
     int fin = 0;    // buffer holding the final motion
     int start = 0;  // zeroed buffer the next run starts from (motion_est->reset())
+    // the triple kernel takes the gradients from Iaux (= Imov) instead of dI:
+    // -1 by slab size (of2d::hs3_gradients_from_image), 0 / 1 forced
+    int gi = -1;
     // set_images' divide-by-zero test (dI is fixed per image pair): this rank's
     // result, and whether the ranks have voted on it yet (first run after
     // set_images; set_images itself need not be called by all ranks together)
@@ -76,6 +79,14 @@ struct of2d_slab {
     std::vector<float> errs;
     std::string err;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    // the triple launches of the first kTriTimed chunks of a run, bracketed by
+    // event pairs on st (after the edge launches have joined it): the dominant
+    // kernel's own launch time inside the run, for the roofline report
+    static constexpr int kTriTimed = 64;
+    hipEvent_t ev_tri[2 * kTriTimed] = {};
+    int tri_pairs = 0, tri_launches = 0;
+    double tri_us = 0.0;  // average per triple launch of the last run
+    int tri_n = 0;        // triple launches that average covers
 };
 
 // The ranks of one grid inside ONE process, one host thread per rank: halos
@@ -245,6 +256,9 @@ struct SlabGeometry {
     int n3 = 0;          // block partials a triple writes
     int nb = 0;          // partial row length for every kernel of the slab
 };
+bool use_gi(const of2d_slab *s) {
+    return s->gi < 0 ? of2d::hs3_gradients_from_image(s->dimx, s->nrows) : s->gi != 0;
+}
 // the motion buffer holding neither the result nor the next run's zeroed start
 int scratch_buffer(const of2d_slab *s) {
     for (int b = 0; b < 3; b++)
@@ -324,6 +338,7 @@ static int slab_create(of2d_slab **out, int dimx, int dimy, float alpha, int ran
         OF2D_HIP(hipStreamCreateWithFlags(&s->st, hipStreamNonBlocking));
         OF2D_HIP(hipEventCreate(&s->ev0));
         OF2D_HIP(hipEventCreate(&s->ev1));
+        for (auto &e : s->ev_tri) OF2D_HIP(hipEventCreate(&e));
         OF2D_HIP(hipStreamCreateWithFlags(&s->comm_st, hipStreamNonBlocking));
         OF2D_HIP(hipEventCreateWithFlags(&s->ev_int, hipEventDisableTiming));
         OF2D_HIP(hipEventCreateWithFlags(&s->ev_edge, hipEventDisableTiming));
@@ -460,6 +475,9 @@ int of2d_slab_run(of2d_slab *s, int niter, int fixed_iters, int *iters_done) {
                   n3 = G.n3;
         const double npx = (double)s->dimx * s->dimy;
         unsigned *range_flag = s->d_status + of2d::kRangeFlagWord;
+        // Iaux == Imov (zero initial motion); its three ghost j-lines hold the
+        // neighbours' image rows, as the gradients of the halo rows need
+        const float *ia = use_gi(s) ? s->Imov.p : nullptr;
         auto src_of = [](int a, int t) { return t == 0 ? a : (t % 2 == 1 ? (a + 1) % 3 : (a + 2) % 3); };
         auto dst_of = [](int a, int t) { return t % 2 == 0 ? (a + 1) % 3 : (a + 2) % 3; };
         // st runs after the latest edge launches / comm_st after the latest st work
@@ -470,7 +488,7 @@ int of2d_slab_run(of2d_slab *s, int niter, int fixed_iters, int *iters_done) {
             of2d::launch_hs_jacobi3_window(s->u[in].p, s->u[out].p, s->dI.p, s->It.p, s->P,
                                            s->dimx, s->nrows, s->rb, s->dimy, alphasq, -3,
                                            s->nrows + 3, jlo, jhi, rpw, slot, p1, p2, p3,
-                                           s->d_status, range_flag, st);
+                                           s->d_status, range_flag, st, ia);
         };
         // K (2 or 3) iterations in one pass from buffer `in` to buffer `out`.
         // One rank: one launch.  With neighbours, triples are split: the
@@ -501,7 +519,7 @@ int of2d_slab_run(of2d_slab *s, int niter, int fixed_iters, int *iters_done) {
             if (K == 3)
                 of2d::launch_hs_jacobi3(uin, s->u[out].p, s->dI.p, s->It.p, s->P, s->dimx,
                                         s->nrows, s->rb, s->dimy, alphasq, -3, s->nrows + 3, p1,
-                                        p2, p3, s->d_status, range_flag, s->st);
+                                        p2, p3, s->d_status, range_flag, s->st, -1, -1, ia);
             else
                 of2d::launch_hs_jacobi2(uin, s->u[out].p, s->dI.p, s->It.p, s->P, s->dimx,
                                         s->nrows, s->rb, s->dimy, alphasq, -3, s->nrows + 3, p1,
@@ -529,6 +547,8 @@ int of2d_slab_run(of2d_slab *s, int niter, int fixed_iters, int *iters_done) {
         if (fixed_iters) reserve_sums(s, niter);  // no-op after of2d_slab_reserve
         OF2D_HIP(hipMemsetAsync(s->d_status, 0, sizeof(unsigned), s->st));
         s->errs.clear();
+        s->tri_pairs = 0;
+        s->tri_launches = 0;
         OF2D_HIP(hipEventRecord(s->ev0, s->st));
         mark_st();  // comm_st starts after everything enqueued so far
         OF2D_HIP(hipStreamWaitEvent(s->comm_st, s->ev_int, 0));
@@ -545,12 +565,24 @@ int of2d_slab_run(of2d_slab *s, int niter, int fixed_iters, int *iters_done) {
             of2d::PartialRuns runs;
             auto other = [&](int b) { return b == (a + 1) % 3 ? (a + 2) % 3 : (a + 1) % 3; };
             int cur = a, tp = 0;
+            // time this chunk's triples (the first kTriTimed chunks of the run)
+            const bool timed = C >= 3 && s->tri_pairs < of2d_slab::kTriTimed;
+            if (timed) {
+                join_st();
+                OF2D_HIP(hipEventRecord(s->ev_tri[2 * s->tri_pairs], s->st));
+            }
             while (tp < C) {
                 const int nxt = other(cur);
                 if (C - tp >= 3) {
                     fused(3, cur, nxt, part(tp), part(tp + 1), part(tp + 2));
                     runs.add(tp, 3, n3);
                     tp += 3;
+                    if (timed && C - tp < 3) {  // the chunk's last triple
+                        join_st();
+                        OF2D_HIP(hipEventRecord(s->ev_tri[2 * s->tri_pairs + 1], s->st));
+                        s->tri_pairs++;
+                        s->tri_launches += C / 3;
+                    }
                 } else if (C - tp == 2) {
                     fused(2, cur, nxt, part(tp), part(tp + 1), nullptr);
                     runs.add(tp, 2, n2);
@@ -629,6 +661,14 @@ int of2d_slab_run(of2d_slab *s, int niter, int fixed_iters, int *iters_done) {
         float ms = 0.0f;
         OF2D_HIP(hipEventElapsedTime(&ms, s->ev0, s->ev1));
         s->last_ms = ms;
+        double tri_ms = 0.0;
+        for (int p = 0; p < s->tri_pairs; p++) {
+            float m = 0.0f;
+            OF2D_HIP(hipEventElapsedTime(&m, s->ev_tri[2 * p], s->ev_tri[2 * p + 1]));
+            tri_ms += m;
+        }
+        s->tri_n = s->tri_launches;
+        s->tri_us = s->tri_launches ? 1000.0 * tri_ms / s->tri_launches : 0.0;
         if (iters_done) *iters_done = done;
     });
 }
@@ -666,7 +706,8 @@ int of2d_slab_time_kernel(of2d_slab *s, int nlaunch, double *avg_us) {
         auto go = [&] {
             of2d::launch_hs_jacobi3(s->u[in].p, s->u[out].p, s->dI.p, s->It.p, s->P, s->dimx,
                                     s->nrows, s->rb, s->dimy, alphasq, -3, s->nrows + 3, p1, p2,
-                                    p3, s->d_status, s->d_status + of2d::kRangeFlagWord, s->st);
+                                    p3, s->d_status, s->d_status + of2d::kRangeFlagWord, s->st,
+                                    -1, -1, use_gi(s) ? s->Imov.p : nullptr);
         };
         go();
         OF2D_HIP(hipEventRecord(s->ev0, s->st));
@@ -685,10 +726,27 @@ int of2d_slab_info(const of2d_slab *s, int *info, int n) {
     if (s->comm && ncclCommCount(s->comm, &rccl) != ncclSuccess) return -OF2D_ERR_DEVICE;
     const int halo_lines = s->nranks > 1 ? 3 : 0;
     const int v[] = {s->nranks, rccl, s->grp ? 1 : 0, s->rb, s->re, s->dimx, s->P,
-                     halo_lines, slab_geometry(s).split ? 1 : 0};
+                     halo_lines, slab_geometry(s).split ? 1 : 0, use_gi(s) ? 1 : 0};
     const int k = std::min(n, (int)(sizeof v / sizeof v[0]));
     for (int i = 0; i < k; i++) info[i] = v[i];
     return k;
+}
+
+int of2d_slab_set_option(of2d_slab *s, const char *key, double value) {
+    if (!s || !key) return OF2D_ERR_INVALID_ARGUMENT;
+    if (std::strcmp(key, "hs_gradients_from_image") == 0) {
+        s->gi = value < 0.0 ? -1 : (value != 0.0 ? 1 : 0);
+        return OF2D_OK;
+    }
+    s->err = std::string("slab: unknown option ") + key;
+    return OF2D_ERR_INVALID_ARGUMENT;
+}
+
+int of2d_slab_last_run_kernel_us(const of2d_slab *s, double *avg_us, int *nlaunch) {
+    if (!s || !avg_us || !nlaunch) return OF2D_ERR_INVALID_ARGUMENT;
+    *avg_us = s->tri_us;
+    *nlaunch = s->tri_n;
+    return OF2D_OK;
 }
 
 int of2d_slab_last_run_ms(const of2d_slab *s, double *ms) {
@@ -716,6 +774,8 @@ int of2d_slab_destroy(of2d_slab *s) {
     if (s->d_stage) (void)hipFree(s->d_stage);
     if (s->ev0) (void)hipEventDestroy(s->ev0);
     if (s->ev1) (void)hipEventDestroy(s->ev1);
+    for (auto &e : s->ev_tri)
+        if (e) (void)hipEventDestroy(e);
     if (s->ev_int) (void)hipEventDestroy(s->ev_int);
     if (s->ev_edge) (void)hipEventDestroy(s->ev_edge);
     for (auto &f : s->u) f.release();

@@ -114,14 +114,20 @@ class SlabSolver:
 
     def info(self) -> dict:
         """nranks, the RCCL communicator's rank count (ncclCommCount; 0 without
-        one), rows, pitch, halo lines per fused launch, interior/edge split."""
-        buf = (C.c_int * 9)()
-        n = _lib.lib().of2d_slab_info(self._h, buf, 9)
+        one), rows, pitch, halo lines per fused launch, interior/edge split,
+        whether the triple kernel derives dI from Iaux."""
+        buf = (C.c_int * 10)()
+        n = _lib.lib().of2d_slab_info(self._h, buf, 10)
         if n < 0:
             self._chk(-n)
         keys = ["nranks", "rccl_ranks", "in_process_group", "row_begin", "row_end", "dimx",
-                "pitch", "halo_lines", "split"]
+                "pitch", "halo_lines", "split", "gradients_from_image"]
         return {k: int(buf[i]) for i, k in enumerate(keys[:n])}
+
+    def set_option(self, key: str, value: float) -> None:
+        """Tuning switch (include/of2d.h of2d_slab_set_option), e.g.
+        "hs_gradients_from_image" 0/1; results are bit-identical either way."""
+        self._chk(_lib.lib().of2d_slab_set_option(self._h, key.encode(), float(value)))
 
     def run(self, niter: int, fixed_iters: bool = False) -> int:
         done = C.c_int(0)
@@ -139,6 +145,13 @@ class SlabSolver:
         us = C.c_double(0.0)
         self._chk(_lib.lib().of2d_slab_time_kernel(self._h, int(nlaunch), C.byref(us)))
         return us.value
+
+    def last_run_kernel_us(self) -> tuple:
+        """(average us per triple launch, launches averaged) inside the last run."""
+        us = C.c_double(0.0)
+        n = C.c_int(0)
+        self._chk(_lib.lib().of2d_slab_last_run_kernel_us(self._h, C.byref(us), C.byref(n)))
+        return us.value, n.value
 
     def last_run_ms(self) -> float:
         ms = C.c_double(0.0)

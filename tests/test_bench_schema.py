@@ -14,6 +14,7 @@ CONTRACT = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step
 
 def test_default_workloads():
     a = bench.parse_args([])
+    assert a.iters_per_step == 1000  # BASELINE config 2: 1000 Jacobi iterations
     w1 = bench.workload(a, 1)
     assert (w1["dimx"], w1["dimy"], w1["scaling"]) == (4096, 4096, "strong")
     assert w1["workload"].startswith("config 2")
@@ -31,9 +32,11 @@ def _record(world, dimx, dimy, rows):
     wl = bench.workload(bench.parse_args(["--grid", str(dimx)]), world)
     info = {"nranks": world, "rccl_ranks": world if world > 1 else 0, "halo_lines": 3 if world > 1 else 0,
             "split": 1 if world > 1 else 0}
-    return bench.make_record(world=world, wl=wl, steps=300, warmup=50, elapsed=0.03,
-                             gpu_ms=29.0, avg_us=87.0, iso_us=85.0, px_rank=dimx * rows,
-                             info=info, traffic=None, cpu=None, rows_per_rank=rows)
+    # config 2's slab keeps dI + It in the MALL (field), config 5's do not (image)
+    return bench.make_record(world=world, wl=wl, steps=20, warmup=5, elapsed=0.6,
+                             gpu_ms=580.0, avg_us=87.0, iso_us=85.0, px_rank=dimx * rows,
+                             info=info, traffic=None, cpu=None, rows_per_rank=rows,
+                             iters_per_step=1000, gradients="field" if world == 1 else "image")
 
 
 @pytest.mark.parametrize("world", [1, 2, 4, 8])
@@ -43,25 +46,34 @@ def test_record_schema(world):
     r = _record(world, dimx, dimx, rows)
     assert CONTRACT <= set(r)
     json.loads(json.dumps(r))  # serialisable
-    assert r["n_gpus"] == world and r["steps"] == 300 and r["warmup"] == 50
+    assert r["n_gpus"] == world and r["steps"] == 20 and r["warmup"] == 5
     assert r["higher_is_better"] is True and r["vs_baseline"] is None
     assert r["unit"] == "Mpx-it/s" and r["dtype"] == "fp32"
+    # a step is one 1000-iteration HS loop (config 2's niter);
     # value = whole-job pixel-iterations / max-over-ranks time
-    assert r["value"] == pytest.approx(dimx * dimx * 300 / 0.03 / 1e6, rel=1e-6)
-    assert r["ms_per_step"] == pytest.approx(0.1, rel=1e-6)
+    assert r["value"] == pytest.approx(dimx * dimx * 20000 / 0.6 / 1e6, rel=1e-6)
+    assert r["ms_per_step"] == pytest.approx(30.0, rel=1e-6)
     c = r["config"]
+    assert c["iterations_per_step"] == 1000 and c["iterations"] == 20000
     assert c["grid"] == [dimx, dimx] and c["rows_per_rank"] == rows
     assert c["rccl_ranks"] == (world if world > 1 else 0)
     assert c["halo_bytes_per_exchange"] == (2 * 3 * dimx * 8 if world > 1 else 0)
     rf = r["roofline"]
     assert {"bound", "achieved", "peak", "unit", "frac", "traffic"} <= set(rf)
     assert rf["bound"] == "hbm" and rf["unit"] == "GB/s" and rf["peak"] == 8000.0
-    # per GPU: 28 B per px of the rank's slab per launch over the launch time
-    assert rf["achieved"] == pytest.approx(28 * dimx * rows / 87e-6 / 1e9, rel=1e-3)
+    # per GPU: the kernel's bytes per px of the rank's slab per launch (28:
+    # u 8 + dI 8 + It 4 in, u 8 out; 24 with dI derived from Iaux 4) over the
+    # launch time
+    b = 28 if world == 1 else 24
+    assert rf["bytes_per_px_launch"] == b
+    assert rf["achieved"] == pytest.approx(b * dimx * rows / 87e-6 / 1e9, rel=1e-3)
     assert rf["frac"] == pytest.approx(rf["achieved"] / 8000.0, rel=1e-3)
     assert rf["traffic"] is None and rf["traffic_source"] is None
+    assert rf["kernel"].startswith("of2d::hs::jacobi3_kernel")
 
 
-def test_traffic_only_for_its_grid():
-    assert bench.load_traffic(4096, 4096) is not None
-    assert bench.load_traffic(16384, 8192) is None
+def test_traffic_only_for_its_grid_and_kernel():
+    t = bench.load_traffic(4096, 4096, "field")
+    assert t is not None and t["grid"] == [4096, 4096]
+    assert bench.load_traffic(4096, 4096, "image") is None
+    assert bench.load_traffic(16384, 8192, "field") is None
