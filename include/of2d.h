@@ -90,7 +90,9 @@ int of2d_last_errors(const of2d_ctx *ctx, float *out, int cap);
 /* Options that the reference does not have (bench / deployment only):
  *   "fixed_iters" (0/1): run every iteration, no convergence break
  *   "chunk" (>=1): iterations enqueued between host convergence checks
- *   "device" (>=0): HIP device ordinal, must be set before of2d_set_images */
+ *   "device" (>=0): HIP device ordinal, must be set before of2d_set_images
+ *   "hs_gradients_from_image" (-1 auto = default, 0, 1): as for the slab
+ *   solver (of2d_slab_set_option); bit-identical results either way */
 int of2d_set_option(of2d_ctx *ctx, const char *key, double value);
 
 /* ---- gateway: the process-global singleton of WrapperOpticalFlow2d.cpp:13.

@@ -171,6 +171,7 @@ class Registration {
     std::vector<Level> lv_;
     bool fixed_ = false;
     int chunk_ = 33;  // eleven fused triples per chunk
+    int gi_ = -1;     // triple kernel: dI from Iaux (1), from dI (0), by size (-1)
     int device_ = -1;
     bool ready_ = false;
     hipStream_t st_ = nullptr;

@@ -150,6 +150,8 @@ void Registration::set_option(const std::string &key, double v) {
         if (ready_) throw std::invalid_argument("option 'chunk' must be set before first use");
         chunk_ = std::max(1, (int)v);
     }
+    else if (key == "hs_gradients_from_image")
+        gi_ = v < 0 ? -1 : (v != 0 ? 1 : 0);
     else if (key == "device") {
         if (ready_) throw std::invalid_argument("option 'device' must be set before first use");
         device_ = (int)v;
@@ -400,7 +402,9 @@ int Registration::loop_hs(Level &L, int niter, float alpha, int &final_buf) {
             // (dI was taken of it; hs3_gradients_from_image)
             launch_hs_jacobi3(src, dst, L.dI.p, L.It.p, L.P, L.dx, L.dy, 0, L.dy, alphasq, -1,
                               L.dy + 1, p1, p2, p3, d_status_, range_flag, st_, -1, -1,
-                              hs3_gradients_from_image(L.dx, L.dy) ? L.Iaux.p : nullptr);
+                              (gi_ < 0 ? hs3_gradients_from_image(L.dx, L.dy) : gi_ != 0)
+                                  ? L.Iaux.p
+                                  : nullptr);
         })
               : StepFn3(),
         nblk);

@@ -133,7 +133,8 @@ class ImageRegistration:
     Parameters mirror the init call: ``dims=(dimx, dimy)``, ``niter`` (nscales+1
     values, finest level first), ``nscales``, ``reg``, ``params`` (nparams
     floats), ``nrefine``, ``verbose``.  Extra keyword options map to
-    ``of2d_set_option`` (``fixed_iters``, ``chunk``, ``device``).
+    ``of2d_set_option`` (``fixed_iters``, ``chunk``, ``device``,
+    ``hs_gradients_from_image``).
     """
 
     def __init__(self, dims: Sequence[int], niter: Sequence[int], nscales: int, reg: int,

@@ -149,8 +149,26 @@ static inline v2 qlap_v(const v2 *f, unsigned idx, unsigned i, unsigned j, unsig
 }
 
 /* ------------------------------------------------------------------ Field ops */
+/* Logger norm precision knob (test infrastructure).  0: the reference's
+ * Motion::norm, a sequential FLOAT running sum (below).  1: the same
+ * magnitudes summed in double and divided as the GPU path does (registration.cpp
+ * logger_error: (float)sum / (float)n), i.e. the Logger error the reference
+ * would compute without fp32 running-sum rounding; the GPU's fp64 tree sums
+ * of fp32 per-lane partials agree with it to ~1e-7 relative.  Only the
+ * convergence fixtures (tests/golden/make_convergence.py) use 1. */
+static int g_logger_fp64 = 0;
+void oracle_set_logger_fp64(int on) { g_logger_fp64 = on; }
+
 /* src/Motion.cpp:42-49: float accumulation of a double magnitude */
 static float motion_norm(const v2 *u, unsigned n) {
+    if (g_logger_fp64) {
+        double s = 0.0;
+        for (unsigned i = 0; i < n; i++) {
+            double px = (double)u[i].x, py = (double)u[i].y;
+            s += sqrt(px * px + py * py);
+        }
+        return (float)s / (float)n;
+    }
     float norm = 0.0f;
     for (unsigned i = 0; i < n; i++) {
         double px = (double)u[i].x, py = (double)u[i].y;

@@ -83,6 +83,7 @@ void oracle_fluid_increment(const float *u, const float *v, int dimx, int dimy, 
 /* thread/loop-order knob for the CPU baseline: 1 = reference loop order
  * (i outer, j inner, strided), 0 = row order (same results, faster) */
 void oracle_set_reference_loop_order(int on);
+void oracle_set_logger_fp64(int on);
 
 #ifdef __cplusplus
 }

@@ -85,6 +85,7 @@ def lib():
             "oracle_dct2d": (None, [_f64p, i, i, i]),
             "oracle_fluid_increment": (None, [_f32p, _f32p, i, i, _f32p]),
             "oracle_set_reference_loop_order": (None, [i]),
+            "oracle_set_logger_fp64": (None, [i]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(L, name)

@@ -6,12 +6,16 @@ init -> register -> get with niter = 1000 and the reference's break test
 `err < 0.001f && iter > 1` (ImageRegistrationOpticalFlow.cpp:131-134) on the
 Logger's sequential fp32 norm (Motion.cpp:42-49, Logger.cpp:32-51).
 
-Each fixture records the iterations executed, every iteration's Logger error,
-the fp64 relative error the same iterates have (to show how close the break is
-to the threshold) and a SHA-256 of the final motion's float32 bits, so a GPU
-test can compare a 4096^2 run without running the oracle again.
+Each fixture records the iterations executed, every iteration's Logger error
+and a SHA-256 of the final motion's float32 bits, so a GPU test can compare a
+4096^2 run without running the oracle again.  "exact_norms" holds the same
+for the oracle with the Logger's norms summed in double (oracle_set_logger_fp64):
+at 4096^2 the reference's sequential FLOAT running sum (Motion.cpp:42-49)
+rounds each of its 16.7 M additions at ~1 ulp of the sum, so its error can
+cross 0.001 an iteration away from where the exactly summed error does; the
+GPU sums in fp64 and follows the exact-norm break.
 
-    python tests/golden/make_convergence.py [name ...]
+    python tests/golden/make_convergence.py [--exact-only] [name ...]
 """
 import hashlib
 import json
@@ -50,7 +54,43 @@ def motion_digest(m):
     return hashlib.sha256(planar.tobytes()).hexdigest()
 
 
+def run(gen, n, niter, fp64):
+    ref, mov = inputs(gen, n)
+    O.lib().oracle_capture_output(1)
+    O.lib().oracle_set_logger_fp64(1 if fp64 else 0)
+    t0 = time.time()
+    try:
+        o = O.Registration((n, n), [niter], 0, 0, [0.1], 1, 0)
+        o.register(ref, mov)
+        m, it, errs = o.motion(), o.iterations(), o.last_errors()
+        o.close()
+    finally:
+        O.lib().oracle_set_logger_fp64(0)
+        O.lib().oracle_clear_output()
+    return m, it, errs, time.time() - t0
+
+
+def add_exact(name):
+    gen, n, niter = CASES[name]
+    path = os.path.join(HERE, f"convergence_{name}.json")
+    rec = json.load(open(path))
+    m, it, errs, dt = run(gen, n, niter, True)
+    rec["exact_norms"] = {
+        "iterations_executed": it,
+        "errors": [float(e) for e in errs],
+        "motion_sha256_f32_planar": motion_digest(m),
+        "oracle_seconds": round(dt, 1),
+    }
+    with open(path, "w") as f:
+        json.dump(rec, f, indent=1)
+    print(name, "exact norms:", it, "reference norms:", rec["iterations_executed"], flush=True)
+
+
 def main(names):
+    if names and names[0] == "--exact-only":
+        for name in names[1:] or CASES:
+            add_exact(name)
+        return
     for name in names or CASES:
         gen, n, niter = CASES[name]
         ref, mov = inputs(gen, n)
@@ -76,6 +116,7 @@ def main(names):
         with open(os.path.join(HERE, f"convergence_{name}.json"), "w") as f:
             json.dump(rec, f, indent=1)
         print(name, it, rec["oracle_seconds"], "s", flush=True)
+        add_exact(name)
 
 
 if __name__ == "__main__":

@@ -79,13 +79,21 @@ def test_chunked_speculation_is_exact(gpu, oracle, chunk):
     assert np.array_equal(m, o["motion"])
 
 
+# hs_gradients_from_image: the triple kernel reads the stored gradient field
+# dI (0) or derives it from Iaux in the kernel (1; the product does so once dI
+# + It exceed the MALL, of2d_device.h hs3_gradients_from_image) — the same bits
+GI = [0, 1]
+
+
+@pytest.mark.parametrize("gi", GI)
 @pytest.mark.parametrize("dims", [(37, 23), (129, 65), (255, 130), (64, 300), (3, 3)])
-def test_ragged_sizes(gpu, oracle, dims):
+def test_ragged_sizes(gpu, oracle, dims, gi):
     nx, ny = dims
     rng = np.random.default_rng(nx * 1000 + ny)
     ref = rng.random((nx, ny))
     mov = np.roll(ref, 1, axis=0) * 0.9 + 0.05
-    with ImageRegistration(dims, [25], 0, 0, [0.3], fixed_iters=1) as r:
+    with ImageRegistration(dims, [25], 0, 0, [0.3], fixed_iters=1,
+                           hs_gradients_from_image=gi) as r:
         r.register(ref, mov)
         m = r.motion()
         w = r.warp(mov)
@@ -98,8 +106,9 @@ def _bits(a):
     return np.asarray(a, dtype=np.float32).view(np.uint32)
 
 
+@pytest.mark.parametrize("gi", GI)
 @pytest.mark.parametrize("case", ["blob", "tiny", "static"])
-def test_division_paths_bitwise(gpu, oracle, case):
+def test_division_paths_bitwise(gpu, oracle, case, gi):
     """The triple Jacobi kernel divides without div_scale where that is exact
     (hs_jacobi_impl.h div2_unscaled: gradients in 0 or [2^-30, 2^20), the
     denominator in [2^-40, 2^40), sc in 0 or [2^-50, 2^30)) and takes the
@@ -119,7 +128,8 @@ def test_division_paths_bitwise(gpu, oracle, case):
         ref, mov = ref * 1e-12, mov * 1e-12
     else:
         mov = ref.copy()
-    with ImageRegistration((n, n), [61], 0, 0, [0.3], fixed_iters=1) as r:
+    with ImageRegistration((n, n), [61], 0, 0, [0.3], fixed_iters=1,
+                           hs_gradients_from_image=gi) as r:
         r.register(ref, mov)
         m = r.motion()
     o = oracle_run(oracle, (n, n), [61], 0, 0, [0.3], 1, ref, mov, fixed=True)
@@ -140,10 +150,13 @@ def test_pyramid_and_refine_fixture(gpu):
             assert np.array_equal(r.warp(g[f"{name}/mov"]), g[f"{name}/warped"]), name
 
 
-def test_texture_three_levels_two_refines(gpu, oracle):
+@pytest.mark.parametrize("gi", GI)
+def test_texture_three_levels_two_refines(gpu, oracle, gi):
+    """Pyramid and refines: Iaux is the warped moving image on every refine
+    after the first, so the in-kernel gradients are taken of a warped image."""
     ref, mov = S.texture_pair(200, seed=11, ny=136)
     args = ((200, 136), [30, 25, 20], 2, 0, [0.15], 2)
-    with ImageRegistration(*args) as r:
+    with ImageRegistration(*args, hs_gradients_from_image=gi) as r:
         r.register(ref, mov)
         m, it = r.motion(), r.iterations()
     o = oracle_run(oracle, *args, ref, mov)

@@ -29,12 +29,13 @@ def _bits(a):
     return np.asarray(a, dtype=np.float32).view(np.uint32)
 
 
-def run_group(ref, mov, alpha, nranks, niter, fixed):
+def run_group(ref, mov, alpha, nranks, niter, fixed, gi=-1):
     dimx, dimy = ref.shape
     g = SlabGroup(nranks)
     slabs = [SlabSolver(dimx, dimy, alpha, r, nranks, group=g) for r in range(nranks)]
     try:
         for s in slabs:
+            s.set_option("hs_gradients_from_image", gi)
             lo, hi = halo_rows(dimy, s.rank, nranks)
             s.set_images(ref[:, lo:hi], mov[:, lo:hi])
         done, errs = [None] * nranks, [None] * nranks
@@ -79,10 +80,13 @@ def run_single(ref, mov, alpha, niter, fixed):
     (256, 512, 8, 50),    # eight ranks
     (64, 12, 4, 20),      # three j-lines per slab, the minimum
 ])
-def test_slab_group_fixed_iterations_bitwise(gpu, dimx, dimy, nranks, niter):
+@pytest.mark.parametrize("gi", [0, 1])
+def test_slab_group_fixed_iterations_bitwise(gpu, dimx, dimy, nranks, niter, gi):
+    """gi = 1: the triple kernel derives the gradients of the halo rows from the
+    image halo rows the slab took at set_images (three j-lines each side)."""
     ref, mov = S.texture_pair(dimx, seed=5, ny=dimy)
     m1, it1 = run_single(ref, mov, 0.1, niter, True)
-    mN, itN = run_group(ref, mov, 0.1, nranks, niter, True)
+    mN, itN = run_group(ref, mov, 0.1, nranks, niter, True, gi)
     assert it1 == niter and itN == [niter] * nranks
     assert np.abs(m1).max() > 0.01  # the motion has crossed the slab seams
     assert np.array_equal(_bits(mN), _bits(m1))

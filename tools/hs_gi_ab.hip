@@ -30,6 +30,30 @@ using namespace of2d;
         }                                                                            \
     } while (0)
 
+// streaming probes with the two kernels' access mixes and no stencil (2 px
+// per thread): u float4 + dI float4 + It float2 in, float4 out (28 B/px), and
+// u float4 + Iaux float2 + It float2 in, float4 out (24 B/px).  Their known
+// byte counts calibrate FETCH_SIZE / WRITE_SIZE for each mix, and their time
+// is the achievable ceiling for that mix at this grid.
+__global__ void probe_field_kernel(const float4 *__restrict__ u, const float4 *__restrict__ g,
+                                   const float2 *__restrict__ t, float4 *__restrict__ o, long n2) {
+    for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n2;
+         i += (long)gridDim.x * blockDim.x) {
+        const float4 a = u[i], b = g[i];
+        const float2 c = t[i];
+        o[i] = make_float4(a.x + b.x * c.x, a.y + b.y, a.z + b.z * c.y, a.w + b.w);
+    }
+}
+__global__ void probe_image_kernel(const float4 *__restrict__ u, const float2 *__restrict__ ia,
+                                   const float2 *__restrict__ t, float4 *__restrict__ o, long n2) {
+    for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n2;
+         i += (long)gridDim.x * blockDim.x) {
+        const float4 a = u[i];
+        const float2 b = ia[i], c = t[i];
+        o[i] = make_float4(a.x + b.x * c.x, a.y + b.y, a.z + b.x * c.y, a.w + b.y);
+    }
+}
+
 typedef void (*K3)(const float2 *, float2 *, const float2 *, const float *, int, int, int, int,
                    int, float, int, int, double *, double *, double *, unsigned *, int, int, int,
                    int, const unsigned *, int, int, const float *);
@@ -112,6 +136,22 @@ int main(int argc, char **argv) {
                            n, ny, 0, ny, alphasq, -1, ny + 1, part, part + 2 * nb, part + 4 * nb,
                            status, 0, gx, gy, rows, rflag, -1, -1, v.gi ? pIa : nullptr);
     };
+    // probes over the pitched rows (P * ny px, 2 px per thread)
+    const long n2 = (long)P * ny / 2;
+    auto probes = [&](int reps) {
+        for (int k = 0; k < reps; k++) {
+            hipLaunchKernelGGL(probe_field_kernel, dim3(8192), dim3(256), 0, st, (const float4 *)pu0,
+                               (const float4 *)pdI, (const float2 *)pIt, (float4 *)pu1, n2);
+            hipLaunchKernelGGL(probe_image_kernel, dim3(8192), dim3(256), 0, st, (const float4 *)pu1,
+                               (const float2 *)pIa, (const float2 *)pIt, (float4 *)pu0, n2);
+        }
+    };
+    if (argc > 4 && atoi(argv[4]) == -2) {  // PMC mode: the probes only
+        probes(launches);
+        CK(hipDeviceSynchronize());
+        printf("probes: %d launches each, %ld px\n", launches, 2 * n2);
+        return 0;
+    }
     if (argc > 4 && atoi(argv[4]) >= 0) {  // PMC mode: `launches` launches of variant argv[4] only
         const int v = atoi(argv[4]);
         for (int w = 0; w < launches; w++) launch(vs[v], (w & 1) ? pu1 : pu0, (w & 1) ? pu0 : pu1);
@@ -163,6 +203,30 @@ int main(int argc, char **argv) {
             CK(hipEventElapsedTime(&ms, e0, e1));
             t[v].push_back(1000.0f * ms / launches);
         }
+    {
+        probes(20);
+        float ms;
+        for (int which = 0; which < 2; which++) {
+            CK(hipEventRecord(e0, st));
+            for (int k = 0; k < launches; k++) {
+                if (which == 0)
+                    hipLaunchKernelGGL(probe_field_kernel, dim3(8192), dim3(256), 0, st,
+                                       (const float4 *)pu0, (const float4 *)pdI,
+                                       (const float2 *)pIt, (float4 *)pu1, n2);
+                else
+                    hipLaunchKernelGGL(probe_image_kernel, dim3(8192), dim3(256), 0, st,
+                                       (const float4 *)pu0, (const float2 *)pIa,
+                                       (const float2 *)pIt, (float4 *)pu1, n2);
+            }
+            CK(hipEventRecord(e1, st));
+            CK(hipEventSynchronize(e1));
+            CK(hipEventElapsedTime(&ms, e0, e1));
+            const double us = 1000.0 * ms / launches, b = (which ? 24.0 : 28.0) * P * ny;
+            printf("probe %-22s: %.2f us/launch, %.0f GB/s (%d B/px, no stencil)\n",
+                   which ? "u+Iaux+It (image mix)" : "u+dI+It (field mix)", us, b / us / 1e3,
+                   which ? 24 : 28);
+        }
+    }
     for (int v = 0; v < nv; v++) {
         printf("%-28s:", vs[v].name);
         for (float x : t[v]) printf(" %.2f", x);
