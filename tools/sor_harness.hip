@@ -1,12 +1,13 @@
-// SOR wavefront timeline harness: runs sor_strip_kernel on a synthetic
+// SOR wavefront timeline harness: runs the SOR sweep (sor_block_kernel) on a synthetic
 // {v, b} field and prints per-strip start/end times and polled batches.
 //   hipcc -O3 -ffp-contract=off --offload-arch=gfx950 -I opticalflow2d_amd/csrc \
 //         tools/sor_harness.hip -o tools/sor_harness
-//   tools/sor_harness DIMX DIMY [REPS]
+//   tools/sor_harness DIMX DIMY [REPS] [WAVES]
 #include "../opticalflow2d_amd/csrc/fluid_kernels.hip"
 
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <vector>
 
 using namespace of2d;
@@ -14,6 +15,7 @@ using namespace of2d;
 int main(int argc, char **argv) {
     const int dimx = argc > 1 ? atoi(argv[1]) : 8192, dimy = argc > 2 ? atoi(argv[2]) : 8192;
     const int reps = argc > 3 ? atoi(argv[3]) : 5;
+    const int waves = argc > 4 ? atoi(argv[4]) : 4;
     const int P = pitch_for(dimx), ns = sor_nstrips(dimx);
     const size_t rows = (size_t)sor_rows(dimx, dimy) + 1;
     std::vector<float4> h((size_t)rows * P);
@@ -36,7 +38,6 @@ int main(int argc, char **argv) {
     OF2D_HIP(hipMemset(status, 0, 4));
     OF2D_HIP(hipMalloc(&trace, 24 * (size_t)ns));
     float4 *vb0 = vb;
-    const float A = 1.0f - 0.66f, B = 0.66f / (-6 * 0.25f), M = 0.25f, ML = 0.25f;
     hipEvent_t e0, e1;
     hipEventCreate(&e0);
     hipEventCreate(&e1);
@@ -44,13 +45,11 @@ int main(int argc, char **argv) {
     for (int r = 0; r < reps; r++) {
         const unsigned epoch = r + 1;
         // column-0 granules for strip 0 (what sor_pack writes)
-        hipLaunchKernelGGL(sor_pack_kernel, dim3((dimx + 63) / 64, (dimy + 3) / 4), dim3(64, 4), 0,
-                           0, vb0, (const float2 *)vb0, (const float2 *)vb0, (const float *)vb0,
-                           (const float2 *)nullptr, dimx, dimy, P, (v4u *)H, epoch);
+        launch_sor_pack(vb0, (const float2 *)vb0, (const float2 *)vb0, (const float *)vb0, nullptr,
+                        dimx, dimy, P, H, epoch, 0);
         hipEventRecord(e0, 0);
-        hipLaunchKernelGGL(sor_strip_kernel, dim3(ns), dim3(64), 0, 0, vb0, dimx, dimy, P, A, B,
-                           M, ML, (v4u *)H, sor_granule_stride(dimy), epoch, ticket, ns, status,
-                           trace);
+        launch_sor_traced(vb0, dimx, dimy, P, 0.25f, 0.0f, 0.66f, H, epoch, ticket, status, trace, 0,
+                          waves);
         hipEventRecord(e1, 0);
         OF2D_HIP(hipDeviceSynchronize());
         float ms;
@@ -69,9 +68,9 @@ int main(int argc, char **argv) {
         double dur = 0;
         for (int i = 0; i < ns; i++) dur += (tr[3 * i + 1] - tr[3 * i]) * 0.01;
         dur /= ns;
-        printf("%dx%d strips %d: %.3f ms (timeline %.3f ms)  start lag %.2f us/strip  strip %.1f us"
+        printf("waves %d %dx%d strips %d: %.3f ms (timeline %.3f ms)  start lag %.2f us/strip  strip %.1f us"
                " = %.1f ns/step  polled batches %llu  status %u\n",
-               dimx, dimy, ns, ms, (t1 - t0) * 1e-5, lag, dur, dur * 1e3 / steps, polls, st);
+               waves, dimx, dimy, ns, ms, (t1 - t0) * 1e-5, lag, dur, dur * 1e3 / steps, polls, st);
         if (r == reps - 1 && ns > 1) {
             printf("  strip: start_us end_us polls\n");
             for (int i = 0; i < ns; i += std::max(1, ns / 12))
@@ -79,5 +78,15 @@ int main(int argc, char **argv) {
                        (tr[3 * i + 1] - t0) * 0.01, tr[3 * i + 2]);
         }
     }
+    // final field after `reps` sweeps from the seeded start: identical for
+    // every WAVES value when the sweeps are exact
+    OF2D_HIP(hipMemcpy(h.data(), vb, h.size() * sizeof(float4), hipMemcpyDeviceToHost));
+    unsigned long long hsh = 1469598103934665603ull;
+    for (const auto &q : h) {
+        unsigned u[4];
+        memcpy(u, &q, 16);
+        for (int k = 0; k < 4; k++) hsh = (hsh ^ u[k]) * 1099511628211ull;
+    }
+    printf("waves %d %dx%d reps %d: field hash %016llx\n", waves, dimx, dimy, reps, hsh);
     return 0;
 }
