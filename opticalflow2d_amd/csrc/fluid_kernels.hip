@@ -154,54 +154,37 @@ __device__ __forceinline__ float wide_min(float m) {
 //
 // Lane l (0..62) owns column c0 + l and at step s works on row s + 1 - 2l;
 // lane 63 is a ghost of the next strip's first column (OLD values only).
-// A block runs kSorWaves consecutive strips, one wave per SIMD.  Per step and
-// wave:
+// Per step and wave:
 //   * two DPP wave_shr:1 move the left neighbours' newest outputs one lane to
 //     the right; lane 0, which has no left lane, takes the DPP `old` operand,
 //     i.e. the ghost column's value (the previous strip's last column, or the
-//     image column 0 for strip 0), read from an LDS ring by every lane of the
-//     wave (one broadcast read per row) — the hand-off costs no select;
+//     image column 0 for strip 0) — the hand-off costs no select;
 //   * two DPP wave_shl:1 bring the right neighbour's newest OLD row; older
 //     neighbour values slide through registers (L <- LU, R <- RU ...);
 //   * the update itself runs on packed fp32 (v_pk_add/v_pk_mul, no
 //     contraction: the reference's float operation order, OpticalFlowFluid.cpp:27-35);
-//   * one 8-B store of the new value (lanes that own no interior column are
-//     dropped by the buffer range check: voffset past num_records, not
-//     masked) and one 8-B LDS write: lane 62 into the next strip's ring,
-//     the other lanes into a per-wave sink (no exec-mask change).
-// Hand-off between the waves of a block: LDS rings of kRing rows.  A producer
-// bumps the ring's row count (prog) after every batch of 8 rows; a consumer
-// reads prog and then the next batch's 8 ghost rows kLead steps before the
-// batch (LDS executes one CU's operations in order, so rows read after a prog
-// value are at least as new as that value) and validates prog at the batch;
-// it publishes how far it has read (cons), which the producer checks once per
-// group before reusing ring slots.  Between blocks: the last wave stages its
-// ring rows of the previous batch into tagged 16-B granules {epoch, x, y,
-// epoch} (lanes 0..7, one sc1 buffer_store_dwordx4 per batch); the first wave
-// of the next block prefetches those granule vectors two batches ahead,
-// tag-checks them once per batch and copies them into its own ring.
-// Loads run one group (4 batches of 8 rows) ahead.  Groups whose rows are
-// interior for every lane skip the boundary-row select.
+//   * one 8-B store of the new value, one 16-B granule store by lane 62; the
+//     stores of lanes that own no interior column are dropped by the buffer
+//     range check (voffset past num_records), not masked.
+// Loads run one group (4 batches of 8 rows) ahead; granules (lane k of a
+// vector = ghost row q + k, {epoch, x, y, epoch}: both 8-B halves carry the
+// tag) two batches ahead, are tag-checked once per batch and rotated one lane
+// per step by DPP.  Groups whose rows are interior for every lane skip the
+// boundary-row select.
 namespace {
 constexpr int kSorCols = 63;  // real columns per strip (lanes 0..62)
 constexpr int kSorB = 8;      // rows per batch
 constexpr int kSorNB = 4;     // batches per group
 constexpr int kSorG = kSorB * kSorNB;
+#ifdef OF2D_SOR_GLEAD  // tools/sor_harness.hip A/B builds only
+constexpr int kSorGLead = OF2D_SOR_GLEAD;
+#else
 constexpr int kSorGLead = 2;  // granule vectors are loaded this many batches ahead
-constexpr int kSorWaves = 4;  // strips per block, one wave per SIMD
-constexpr int kRing = 256;    // rows per LDS hand-off ring (power of two)
-// slot(row) = (row + kRingBias) & (kRing - 1): the 8 rows a producer's lane 62
-// publishes in one batch (rows sb - 123 .. sb - 116, sb = 5 mod 8) fill 8
-// aligned slots; a consumer's batch (rows sb + 2 .. sb + 9) spans slots
-// a, a+1, a+2 (a = 5 mod 8) and an aligned run of 5
-constexpr int kRingBias = 6;
-constexpr int kLead = 3;             // steps between reading a batch's ghost rows and the batch
-constexpr int kSink = 64 + kSorB;    // sink slots per wave
-constexpr int kLdsSlots = (kSorWaves + 1) * kRing + kSorWaves * kSink;
+#endif
+static_assert(kSorGLead >= 1 && kSorGLead <= kSorNB, "granule vectors rotate through GV[kSorNB]");
 constexpr unsigned kOob = 0x40000000u;   // voffset beyond num_records: the access is dropped
 constexpr int kNumRecords = 0x20000000;  // bytes addressable from a moving rsrc base
 constexpr int kRsrcFlags = 0x00020000;
-static_assert(((5 - 123 + kRingBias) & 7) == 0, "producer batches fill aligned ring slots");
 
 typedef float v2f __attribute__((ext_vector_type(2)));
 typedef unsigned v2u __attribute__((ext_vector_type(2)));
@@ -221,21 +204,19 @@ __device__ __forceinline__ v2f mid2(v4u q) { return v2f{__uint_as_float(q.y), __
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_at(const void *p) {
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), 0, kNumRecords, kRsrcFlags);
 }
-__device__ __forceinline__ void compiler_fence() { __asm__ volatile("" ::: "memory"); }
 
 // lanes 0..7 of a granule vector: tagged with this sweep's epoch, or a ghost
 // row outside the image (never published, never used for an interior pixel)
 __device__ __forceinline__ bool granules_ready(v4u g, int row0, int dimy, unsigned epoch) {
-    const int lane = threadIdx.x & 63;
+    const int lane = threadIdx.x;
     const bool ok = lane >= kSorB || (g.x == epoch && g.w == epoch) ||
                     (unsigned)(row0 + lane) >= (unsigned)dimy;
     return __builtin_amdgcn_ballot_w64(ok) == ~0ull;
 }
 
-// Slow path of the block-to-block hand-off: some granule of the batch was not
-// yet published when it was prefetched; poll the batch until it is.  Out of
-// line, so the fast path's counted vmcnt is not turned into a drain at a loop
-// preheader.
+// Slow path of the hand-off: some granule of the batch was not yet published
+// when it was prefetched; poll the batch until it is.  Out of line, so the
+// fast path's counted vmcnt is not turned into a drain at a loop preheader.
 __device__ __attribute__((noinline)) v4u granule_poll(__amdgpu_buffer_rsrc_t rs, unsigned voff,
                                                       int soff, int row0, int dimy,
                                                       unsigned epoch, unsigned *status) {
@@ -249,51 +230,24 @@ __device__ __attribute__((noinline)) v4u granule_poll(__amdgpu_buffer_rsrc_t rs,
     return g;
 }
 
-// LDS of the SOR block: the hand-off rings and sinks, and per ring the rows
-// published (prog) and read (cons); ring w holds the ghost column of wave w,
-// ring kSorWaves the last wave's output
-__shared__ __attribute__((aligned(16))) float2 s_sor_lds[kLdsSlots];
-__shared__ int s_sor_prog[kSorWaves + 1], s_sor_cons[kSorWaves + 1];
-// relaxed LDS accesses of the counters; their order against the ring reads and
-// writes is kept by compiler_fence() and the in-order LDS
-__device__ __forceinline__ int lds_ld(const int *p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-__device__ __forceinline__ void lds_st(int *p, int v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-
-// Slow path of an in-block hand-off: wait until counter k of prog (cons when
-// of_cons) reaches `need` (bounded; a timeout is reported through the status
-// word)
-__device__ __attribute__((noinline)) void lds_wait(int k, bool of_cons, int need,
-                                                   unsigned *status) {
-    int *const ctr = of_cons ? s_sor_cons + k : s_sor_prog + k;
-    for (unsigned spins = 0; spins < kSpinLimit; spins++) {
-        if (__builtin_amdgcn_readfirstlane(lds_ld(ctr)) >= need) return;
-        __builtin_amdgcn_s_sleep(1);
-    }
-    atomicOr(status, kStatusSpinTimeout);
-}
-
 template <bool B>
 struct Flag {
     static constexpr bool value = B;
 };
+}  // namespace
 
-// One strip (wave) of a block.  kGIn: ghost column from the granules of the
-// previous block (first wave) instead of the LDS ring filled by the previous
-// wave; kGOut: the output column goes to granules for the next block (last
-// wave) instead of the next wave's ring.  has_next: a strip consumes this
-// strip's ring (back-pressure applies).
-template <bool kGIn, bool kGOut>
-__device__ __forceinline__ void sor_strip(int w, int I,
-                                          bool has_next, float4 *__restrict__ vb, int dimx,
-                                          int dimy, int P, float A, float B, float M, float ML,
-                                          v4u *__restrict__ H, long Hstride, unsigned epoch,
-                                          unsigned *__restrict__ status,
-                                          unsigned long long *__restrict__ trace) {
-    const int lane = threadIdx.x & 63;
+__global__ __launch_bounds__(64) void sor_strip_kernel(float4 *__restrict__ vb, int dimx, int dimy,
+                                                       int P, float A, float B, float M, float ML,
+                                                       v4u *__restrict__ H, long Hstride,
+                                                       unsigned epoch,
+                                                       unsigned *__restrict__ ticket, int nstrips,
+                                                       unsigned *__restrict__ status,
+                                                       unsigned long long *__restrict__ trace) {
+    const int lane = threadIdx.x;
+    __shared__ int s_strip;
+    if (lane == 0) s_strip = (int)(atomicAdd(ticket, 1u) % (unsigned)nstrips);
+    __syncthreads();
+    const int I = __builtin_amdgcn_readfirstlane(s_strip);
     // optional timeline (tools/sor_harness.hip): start, end, polled batches
     const unsigned long long t_start = trace ? __builtin_amdgcn_s_memrealtime() : 0;
     unsigned npoll = 0;
@@ -309,12 +263,8 @@ __device__ __forceinline__ void sor_strip(int w, int I,
     // granules: region I (ghost column of this strip), region I+1 (published)
     const char *gin = reinterpret_cast<const char *>(H + (long)I * Hstride + kSorPadRows);
     const char *gout = reinterpret_cast<const char *>(H + (long)(I + 1) * Hstride + kSorPadRows);
-    const unsigned voff_g8 = lane < kSorB ? (unsigned)lane * 16u : kOob;
-    // LDS: ring w (this strip's ghost rows), ring w + 1 (its output rows)
-    const int ring_in = w * kRing, ring_out = (w + 1) * kRing;
-    const int sink = (kSorWaves + 1) * kRing + w * kSink + lane;
-    float2 *const lds = s_sor_lds;
-    auto slot = [](int row) { return (row + kRingBias) & (kRing - 1); };
+    const unsigned voff_gin = lane < kSorB ? (unsigned)lane * 16u : kOob;
+    const unsigned voff_pub = lane == kSorCols - 1 ? 0u : kOob;
 
     const int s0 = -3;
     const int s1 = dimy + 122;  // lane 62 publishes ghost row dimy - 1 at this step
@@ -338,73 +288,26 @@ __device__ __forceinline__ void sor_strip(int w, int I,
             for (int j = 0; j < kSorB; j++)
                 X[b][j] = __builtin_amdgcn_raw_buffer_load_b128(rs, voff_ld,
                                                                 (4 + kSorB * b + j) * (int)P16, 0);
-        if constexpr (kGIn) {
-            const auto gr = grs(s0);
+        const auto gr = grs(s0);
 #pragma unroll
-            for (int b = 0; b < kSorGLead; b++)
-                GV[b] = __builtin_amdgcn_raw_buffer_load_b128(gr, voff_g8, kSorB * b * 16, 16);
-        }
+        for (int b = 0; b < kSorGLead; b++)
+            GV[b] = __builtin_amdgcn_raw_buffer_load_b128(gr, voff_gin, kSorB * b * 16, 16);
     }
     v2f RD = v2f{dpp_shl(__uint_as_float(W1.x)), dpp_shl(__uint_as_float(W1.y))};
     v2f R = v2f{dpp_shl(__uint_as_float(W2.x)), dpp_shl(__uint_as_float(W2.y))};
     v2f RU = v2f{dpp_shl(__uint_as_float(W3.x)), dpp_shl(__uint_as_float(W3.y))};
     v2f LU = v2f{0.0f, 0.0f}, L = LU, D = lo2(W0);
+    v2f G = LU;  // lane k: ghost row (step + 2 + k) of the current batch
 
-    // ghost rows sb + 2 .. sb + 9 of the batch at step sb, all lanes
-    v2f Gn[kSorB];
-    int pn = 0;  // prog_in as read before them (LDS input)
-    auto read_ghost = [&](int sb) {
-        const int a = ring_in + slot(sb + 2), b = ring_in + slot(sb + 5);
-#pragma unroll
-        for (int j = 0; j < 3; j++) Gn[j] = *reinterpret_cast<const v2f *>(lds + a + j);
-#pragma unroll
-        for (int j = 3; j < kSorB; j++) Gn[j] = *reinterpret_cast<const v2f *>(lds + b + j - 3);
-    };
-    // gb: the group's batch index of the batch at sb (0..kSorNB, kSorNB = the
-    // next group's first); g: the current group's first step
-    auto prepare = [&](int sb, int g, int gb) {
-        if constexpr (kGIn) {
-            v4u gv = GV[gb % kSorNB];
-            if (!granules_ready(gv, sb + 2, dimy, epoch)) {
-                gv = granule_poll(grs(g), voff_g8, kSorB * gb * 16, sb + 2, dimy, epoch, status);
-                npoll++;
-            }
-            {
-                const int bl = gb + kSorGLead;  // batch index counted from group g
-                GV[bl % kSorNB] = __builtin_amdgcn_raw_buffer_load_b128(grs(g), voff_g8,
-                                                                        kSorB * bl * 16, 16);
-            }
-            const int dst = lane < kSorB ? ring_in + slot(sb + 2 + lane) : sink;
-            *reinterpret_cast<v2f *>(lds + dst) = mid2(gv);
-            compiler_fence();
-            read_ghost(sb);
-        } else {
-            pn = lds_ld(s_sor_prog + w);
-            compiler_fence();
-            read_ghost(sb);
-            compiler_fence();
-            lds_st(s_sor_cons + w, sb + kSorB + 2);
-        }
-    };
-    auto check = [&](int sb) {  // the batch at sb may use Gn
-        if constexpr (!kGIn) {
-            const int need = min(sb + kSorB + 2, dimy);
-            if (__builtin_amdgcn_readfirstlane(pn) < need) {
-                lds_wait(w, false, need, status);
-                npoll++;
-                compiler_fence();
-                read_ghost(sb);
-            }
-        }
-    };
-
-    auto step = [&](auto chk, int s, int j, __amdgpu_buffer_rsrc_t rs, v2f Gj, int pub,
-                    v4u xin) {
+    auto step = [&](auto chk, int s, int j, __amdgpu_buffer_rsrc_t rs,
+                    __amdgpu_buffer_rsrc_t ps, v4u xin) {
         const v2f C = lo2(W0), b = hi2(W0), U = lo2(W1);
         // left neighbours' NEW values at rows r+1, r, r-1 (ghost column in lane 0)
         const v2f LD = L;
         L = LU;
-        LU = v2f{dpp_shr_old(Gj.x, D.x), dpp_shr_old(Gj.y, D.y)};
+        const v2f Gn = v2f{dpp_shl(G.x), dpp_shl(G.y)};  // next step's ghost row in lane 0
+        LU = v2f{dpp_shr_old(G.x, D.x), dpp_shr_old(G.y, D.y)};
+        G = Gn;
         // OpticalFlowFluid.cpp:27-35, same association, no contraction
         const v2f RL = R + L;
         const v2f s1v = (RL + U) + D;
@@ -418,7 +321,9 @@ __device__ __forceinline__ void sor_strip(int w, int I,
         }
         __builtin_amdgcn_raw_buffer_store_b64(
             v2u{__float_as_uint(out.x), __float_as_uint(out.y)}, rs, voff_st, j * (int)P16, 0);
-        *reinterpret_cast<v2f *>(lds + pub + j) = out;  // lane 62: ring slot, others: sink
+        __builtin_amdgcn_raw_buffer_store_b128(
+            v4u{epoch, __float_as_uint(out.x), __float_as_uint(out.y), epoch}, ps,
+            voff_pub + (unsigned)j * 16u, 0, 16 /* sc1 */);
         D = out;
         W0 = W1;
         W1 = W2;
@@ -429,52 +334,26 @@ __device__ __forceinline__ void sor_strip(int w, int I,
         RU = v2f{dpp_shl(__uint_as_float(W3.x)), dpp_shl(__uint_as_float(W3.y))};
     };
 
-    v4u stage = v4u{0u, 0u, 0u, 0u};  // last wave: output rows of the previous batch
     auto group = [&](auto chk, int g) {
-        if constexpr (!kGOut) {
-            // back-pressure: the group's last batch reuses the slots of rows
-            // up to (g + 24 - 123) + 8 - kRing
-            if (has_next) {
-                const int need = g + kSorG - 123 - kRing;
-                if (__builtin_amdgcn_readfirstlane(lds_ld(s_sor_cons + w + 1)) < need) {
-                    lds_wait(w + 1, true, need, status);
-                    npoll++;
-                }
-                compiler_fence();
-            }
-        }
 #pragma unroll
         for (int b = 0; b < kSorNB; b++) {
             const int sb = g + kSorB * b;
-            const int row0 = sb - 123;  // rows lane 62 publishes in this batch
-            check(sb);
-            v2f Gc[kSorB];
-#pragma unroll
-            for (int j = 0; j < kSorB; j++) Gc[j] = Gn[j];
-            if constexpr (kGOut) {
-                // the previous batch's rows, lanes 0..7 (after its ring writes)
-                compiler_fence();
-                const int src = ring_out + slot(row0 - kSorB) + (lane & (kSorB - 1));
-                const v2f o = *reinterpret_cast<const v2f *>(lds + src);
-                stage = v4u{epoch, __float_as_uint(o.x), __float_as_uint(o.y), epoch};
+            // ghost rows sb+2 .. sb+9: check the tags, start the lead batch's load
+            v4u gv = GV[b];
+            if (!granules_ready(gv, sb + 2, dimy, epoch)) {
+                gv = granule_poll(grs(g), voff_gin, kSorB * b * 16, sb + 2, dimy, epoch, status);
+                npoll++;
             }
-            const int pub = lane == kSorCols - 1 ? ring_out + slot(row0) : sink;
+            G = mid2(gv);
+            {
+                const int bl = b + kSorGLead;  // batch index counted from this group
+                GV[bl % kSorNB] = __builtin_amdgcn_raw_buffer_load_b128(grs(g), voff_gin,
+                                                                        kSorB * bl * 16, 16);
+            }
             const auto rs = vrs(g, b);
+            const auto ps = rsrc_at(gout + (long)(sb - 123) * 16);
 #pragma unroll
-            for (int j = 0; j < kSorB; j++) {
-                if (j == kSorB - kLead) prepare(sb + kSorB, g, b + 1);
-                step(chk, sb + j, j, rs, Gc[j], pub, X[b][j]);
-                if constexpr (kGOut) {
-                    if (j == 1)
-                        __builtin_amdgcn_raw_buffer_store_b128(
-                            stage, rsrc_at(gout + (long)(row0 - kSorB) * 16), voff_g8, 0,
-                            16 /* sc1 */);
-                }
-            }
-            if constexpr (!kGOut) {
-                compiler_fence();
-                lds_st(s_sor_prog + w + 1, row0 + kSorB);
-            }
+            for (int j = 0; j < kSorB; j++) step(chk, sb + j, j, rs, ps, X[b][j]);
             // batch b of the next group: rows 32 further down
 #pragma unroll
             for (int j = 0; j < kSorB; j++)
@@ -483,79 +362,16 @@ __device__ __forceinline__ void sor_strip(int w, int I,
         }
     };
 
-    // the first batch's ghost rows
-    if constexpr (kGIn) {
-        // granule vectors of batches 0, 1 are in flight; batch 0 is prepared
-        // here, so the lead load of prepare() targets batch 2
-        v4u gv = GV[0];
-        if (!granules_ready(gv, s0 + 2, dimy, epoch)) {
-            gv = granule_poll(grs(s0), voff_g8, 0, s0 + 2, dimy, epoch, status);
-            npoll++;
-        }
-        GV[kSorGLead % kSorNB] =
-            __builtin_amdgcn_raw_buffer_load_b128(grs(s0), voff_g8, kSorB * kSorGLead * 16, 16);
-        const int dst = lane < kSorB ? ring_in + slot(s0 + 2 + lane) : sink;
-        *reinterpret_cast<v2f *>(lds + dst) = mid2(gv);
-        compiler_fence();
-        read_ghost(s0);
-    } else {
-        prepare(s0, s0, 0);
-    }
-    int g = s0;
-    for (; g <= s1; g += kSorG) {
+    for (int g = s0; g <= s1; g += kSorG) {
         if (g >= 124 && g + kSorG - 1 <= dimy - 3)
             group(Flag<false>{}, g);
         else
             group(Flag<true>{}, g);
     }
-    if constexpr (kGOut) {
-        // the last batch's rows
-        compiler_fence();
-        const int row0 = g - kSorB - 123;
-        const int src = ring_out + slot(row0) + (lane & (kSorB - 1));
-        const v2f o = *reinterpret_cast<const v2f *>(lds + src);
-        __builtin_amdgcn_raw_buffer_store_b128(
-            v4u{epoch, __float_as_uint(o.x), __float_as_uint(o.y), epoch},
-            rsrc_at(gout + (long)row0 * 16), voff_g8, 0, 16 /* sc1 */);
-    }
     if (trace && lane == 0) {
         trace[3 * I] = t_start;
         trace[3 * I + 1] = __builtin_amdgcn_s_memrealtime();
         trace[3 * I + 2] = npoll;
-    }
-}
-}  // namespace
-
-// A block of kW strips (kW <= kSorWaves waves); the LDS holds kSorWaves + 1 rings
-template <int kW>
-__global__ __launch_bounds__(64 * kW) void sor_block_kernel(
-    float4 *__restrict__ vb, int dimx, int dimy, int P, float A, float B, float M, float ML,
-    v4u *__restrict__ H, long Hstride, unsigned epoch, unsigned *__restrict__ ticket, int nstrips,
-    unsigned *__restrict__ status, unsigned long long *__restrict__ trace) {
-    __shared__ int s_block;
-    if (threadIdx.x == 0) s_block = (int)(atomicAdd(ticket, 1u) % gridDim.x);
-    if (threadIdx.x <= kSorWaves) {
-        s_sor_prog[threadIdx.x] = -(1 << 30);
-        s_sor_cons[threadIdx.x] = -(1 << 30);
-    }
-    __syncthreads();
-    const int w = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
-    const int I = __builtin_amdgcn_readfirstlane(s_block * kW + w);
-    if (I >= nstrips) return;
-    const bool has_next = I + 1 < nstrips;
-    if constexpr (kW == 1) {
-        sor_strip<true, true>(w, I, has_next, vb, dimx, dimy, P, A, B, M, ML, H, Hstride, epoch,
-                              status, trace);
-    } else {
-        if (w == 0)
-            sor_strip<true, false>(w, I, has_next, vb, dimx, dimy, P, A, B, M, ML, H, Hstride,
-                                   epoch, status, trace);
-        else if (w == kW - 1)
-            sor_strip<false, true>(w, I, has_next, vb, dimx, dimy, P, A, B, M, ML, H, Hstride,
-                                   epoch, status, trace);
-        else
-            sor_strip<false, false>(w, I, has_next, vb, dimx, dimy, P, A, B, M, ML, H, Hstride,
-                                    epoch, status, trace);
     }
 }
 
@@ -564,28 +380,18 @@ long sor_granule_stride(int dimy) { return (long)dimy + 2L * kSorPadRows; }
 size_t sor_granule_bytes(int dimx, int dimy) {
     return (size_t)(sor_nstrips(dimx) + 1) * (size_t)sor_granule_stride(dimy) * 16u;
 }
-int sor_nblocks(int dimx, int waves) { return (sor_nstrips(dimx) + waves - 1) / waves; }
 
-// waves: strips per block (1, 2 or kSorWaves)
 void launch_sor_traced(float4 *vb, int dimx, int dimy, int P, float mu, float lambda, float omega,
                        void *H, unsigned epoch, unsigned *ticket, unsigned *status,
-                       unsigned long long *trace, hipStream_t st, int waves = kSorWaves) {
+                       unsigned long long *trace, hipStream_t st) {
     if (dimx < 3 || dimy < 3) return;  // no interior (OpticalFlowFluid.cpp:23-24)
     const int ns = sor_nstrips(dimx);
     // per-pixel constants of OpticalFlowFluid.cpp:27 evaluated once, same float ops
     const float A = 1.0f - omega;
     const float B = omega / (-6 * mu - 2 * lambda);
     const float ML = mu + lambda;
-    auto go = [&](auto kern) {
-        hipLaunchKernelGGL(kern, dim3(sor_nblocks(dimx, waves)), dim3(64 * waves), 0, st, vb, dimx,
-                           dimy, P, A, B, mu, ML, (v4u *)H, sor_granule_stride(dimy), epoch,
-                           ticket, ns, status, trace);
-    };
-    switch (waves) {
-        case 1: go(sor_block_kernel<1>); break;
-        case 2: go(sor_block_kernel<2>); break;
-        default: go(sor_block_kernel<kSorWaves>); break;
-    }
+    hipLaunchKernelGGL(sor_strip_kernel, dim3(ns), dim3(64), 0, st, vb, dimx, dimy, P, A, B, mu,
+                       ML, (v4u *)H, sor_granule_stride(dimy), epoch, ticket, ns, status, trace);
     OF2D_HIP(hipGetLastError());
 }
 void launch_sor(float4 *vb, int dimx, int dimy, int P, float mu, float lambda, float omega,
@@ -746,41 +552,128 @@ void launch_increment(const float2 *u, const float4 *vel, float2 *R, int dimx, i
     OF2D_HIP(hipGetLastError());
 }
 
-// ------------------------------------------------------------ integrate + Logger
-// if dt < 65: u += R*dt (OpticalFlowFluid.cpp:115, skipped per :135-137); then
-// Logger::update_error against `prev` (Logger.cpp:34-42): partial sums of
-// ||u - prev|| and ||prev||, prev <- u.
-__global__ __launch_bounds__(256) void integrate_logger_kernel(float2 *__restrict__ u,
-                                                               const float2 *__restrict__ R,
-                                                               float2 *__restrict__ prev,
-                                                               const float *__restrict__ scal,
-                                                               int dimx, int dimy, int P,
-                                                               double *__restrict__ partial) {
-    const int i = blockIdx.x * 64 + threadIdx.x;
+// ------------------------------------------------------------ fused iteration step
+// The end of a fluid iteration and the start of the next in one pass over a
+// 64 x 32 tile (ImageRegistrationFluid.cpp:96-108, OpticalFlowFluid.cpp:97-139):
+//   un = u + R dt when dt < 65, else u (OpticalFlowFluid.cpp:115),
+//   written to another buffer (the halo of a neighbouring tile reads u);
+//   Logger partials against prev (Logger.cpp:34-42) where prev is the Logger's
+//   previous motion: the u this pass read (every iteration that follows an
+//   iteration without regridding) or, kPrev, a separate field;
+//   per-block min of the Jacobian of the new u (Image.cpp:189-218, Image::min
+//   at Image.cpp:96-104; the neighbours' new u from an LDS tile with a
+//   one-pixel halo);
+//   the next iteration's force f = dI ((It + u.x dI.x) + u.y dI.y) into vb.zw
+//   and the region-0 granules tagged with the next sweep's epoch (sor_pack's
+//   force-only mode).  When the iteration regrids, the host discards the packed
+//   force and packs again.  One pass instead of three (integrate + Logger,
+//   Jacobian, pack: 69 instead of 101 B/px), and no prev read or write in the
+//   common case.
+__global__ __launch_bounds__(1024) void min_final_kernel(const float *__restrict__ part, int n,
+                                                         float *__restrict__ out);
+template <bool kPrev>
+__global__ __launch_bounds__(256) void fluid_step_kernel(
+    const float2 *__restrict__ u, const float2 *__restrict__ R, float2 *__restrict__ uo,
+    const float2 *__restrict__ prev,
+    const float *__restrict__ scal, const float2 *__restrict__ dI, const float *__restrict__ It,
+    float4 *__restrict__ vb, int dimx, int dimy, int P, v4u *__restrict__ H, unsigned epoch,
+    double *__restrict__ lpart, float *__restrict__ jpart) {
+    constexpr int TW = kSkI + 2, TH = kSkJ + 2;
+    __shared__ float2 un[TH][TW];       // new u at (i0 - 1 + c, j0 - 1 + r)
+    __shared__ float2 fo[kSkJ][kSkI];   // the next iteration's force
+    const int i0 = blockIdx.x * kSkI, j0 = blockIdx.y * kSkJ;
     const float dt = scal[1];
-    double sd = 0.0, sp = 0.0;
-    for (int k = 0; k < kFieldRows / 4; k++) {
-        const int j = blockIdx.y * kFieldRows + 4 * k + threadIdx.y;
-        if (i >= dimx || j >= dimy) break;
+    const bool integ = dt < 65.0f;  // OpticalFlowFluid.cpp:135-137
+    const int tid = threadIdx.y * 64 + threadIdx.x;
+    // 1. new u over the tile and its one-pixel cross halo (corners unused)
+    for (int s = tid; s < TW * TH; s += 256) {
+        const int r = s / TW, c = s - r * TW;
+        const int i = i0 - 1 + c, j = j0 - 1 + r;
+        const bool corner = (r == 0 || r == TH - 1) && (c == 0 || c == TW - 1);
+        if (corner || (unsigned)i >= (unsigned)dimx || (unsigned)j >= (unsigned)dimy) continue;
         const long idx = (long)j * P + i;
         float2 m = u[idx];
-        if (dt < 65.0f) {
-            const float2 r = R[idx];
-            m = make_float2(m.x + r.x * dt, m.y + r.y * dt);
-            u[idx] = m;
+        if (integ) {
+            const float2 q = R[idx];
+            m = make_float2(m.x + q.x * dt, m.y + q.y * dt);
         }
-        const float2 pv = prev[idx];
+        un[r][c] = m;
+    }
+    __syncthreads();
+    // 2. per pixel; thread (x, y) sums the Logger terms of rows y, y + 4, ... in order
+    const int i = i0 + threadIdx.x;
+    double sd = 0.0, sp = 0.0;
+    float jm = __builtin_inff();
+    for (int k = 0; k < kSkJ / 4; k++) {
+        const int rr = 4 * k + threadIdx.y;
+        const int j = j0 + rr;
+        if (i >= dimx || j >= dimy) break;
+        const long idx = (long)j * P + i;
+        const int r = rr + 1, c = threadIdx.x + 1;
+        const float2 m = un[r][c];
+        const float2 pv = kPrev ? prev[idx] : u[idx];
+        uo[idx] = m;
         const float ex = m.x - pv.x, ey = m.y - pv.y;
         sd += (double)__builtin_sqrtf(ex * ex + ey * ey);
         sp += (double)__builtin_sqrtf(pv.x * pv.x + pv.y * pv.y);
-        prev[idx] = m;
+        // motion_gradients of the new u (gradients.h:9-32)
+        float2 dx, dy;
+        if (i == 0) {
+            const float2 a = un[r][c + 1], b = m;
+            dx = make_float2(a.x - b.x, a.y - b.y);
+        } else if (i == dimx - 1) {
+            const float2 a = m, b = un[r][c - 1];
+            dx = make_float2(a.x - b.x, a.y - b.y);
+        } else {
+            const float2 a = un[r][c + 1], b = un[r][c - 1];
+            dx = make_float2((a.x - b.x) / 2.0f, (a.y - b.y) / 2.0f);
+        }
+        if (j == 0) {
+            const float2 a = un[r + 1][c], b = m;
+            dy = make_float2(a.x - b.x, a.y - b.y);
+        } else if (j == dimy - 1) {
+            const float2 a = m, b = un[r - 1][c];
+            dy = make_float2(a.x - b.x, a.y - b.y);
+        } else {
+            const float2 a = un[r + 1][c], b = un[r - 1][c];
+            dy = make_float2((a.x - b.x) / 2.0f, (a.y - b.y) / 2.0f);
+        }
+        const float q = (1.0f + dx.x) * (1.0f + dy.y) - dx.y * dy.x;  // Image.cpp:189-218
+        jm = (q < jm) ? q : jm;
+        // OpticalFlow::get_force (OpticalFlow.cpp:15-39) of the new u
+        const float2 g = dI[idx];
+        const float sc = (It[idx] + m.x * g.x) + m.y * g.y;
+        fo[rr][threadIdx.x] = make_float2(g.x * sc, g.y * sc);
+        if (i == 0 && H) {  // ghost column of strip 0 for the next sweep
+            const float2 x = reinterpret_cast<const float2 *>(vb + sor_index(0, j, P))[0];
+            H[kSorPadRows + j] = v4u{epoch, __float_as_uint(x.x), __float_as_uint(x.y), epoch};
+        }
     }
-    block_sum2(sd, sp, partial);
+    block_sum2(sd, sp, lpart);
+    jm = block_min(jm);
+    if (threadIdx.x == 0 && threadIdx.y == 0) jpart[(long)blockIdx.y * gridDim.x + blockIdx.x] = jm;
+    // 3. vb.zw <- force along the skewed rows (whole 16-B granules, as sor_pack)
+    skew_tile_for_each(i0, j0, dimx, dimy, [&](int ii, int jj) {
+        const float2 f = fo[jj][ii];
+        float4 *dst = vb + sor_index(i0 + ii, j0 + jj, P);
+        const float4 o = *dst;
+        *dst = make_float4(o.x, o.y, f.x, f.y);
+    });
 }
 
-void launch_integrate_logger(float2 *u, const float2 *R, float2 *prev, const float *scal,
-                             int dimx, int dimy, int P, double *partial, hipStream_t st) {
-    hipLaunchKernelGGL(integrate_logger_kernel, field_grid(dimx, dimy), dim3(64, 4), 0, st, u, R, prev, scal, dimx, dimy, P, partial);
+void launch_fluid_step(const float2 *u, const float2 *R, float2 *uo, const float2 *prev,
+                       const float *scal,
+                       const float2 *dI, const float *It, float4 *vb, int dimx, int dimy, int P,
+                       void *H, unsigned epoch, double *lpart, float *jpart, float *jmin,
+                       hipStream_t st) {
+    const dim3 g = field_grid(dimx, dimy);
+    if (prev)
+        hipLaunchKernelGGL(fluid_step_kernel<true>, g, dim3(64, 4), 0, st, u, R, uo, prev, scal,
+                           dI, It, vb, dimx, dimy, P, (v4u *)H, epoch, lpart, jpart);
+    else
+        hipLaunchKernelGGL(fluid_step_kernel<false>, g, dim3(64, 4), 0, st, u, R, uo, prev, scal,
+                           dI, It, vb, dimx, dimy, P, (v4u *)H, epoch, lpart, jpart);
+    hipLaunchKernelGGL(min_final_kernel, dim3(1), dim3(1024), 0, st, jpart, (int)(g.x * g.y), jmin);
     OF2D_HIP(hipGetLastError());
 }
 
@@ -819,25 +712,7 @@ void launch_logger(const float4 *vb, float2 *u, float2 *prev, int dimx, int dimy
     OF2D_HIP(hipGetLastError());
 }
 
-// ------------------------------------------------------------ jacobian min
-// Image::jacobian (Image.cpp:189-218): (1 + dudx.x)(1 + dudy.y) - dudx.y dudy.x,
-// then Image::min (Image.cpp:96-104): per-block min, final min in scal[2]
-__global__ __launch_bounds__(256) void jacobian_min_kernel(const float2 *__restrict__ u,
-                                                           int dimx, int dimy, int P,
-                                                           float *__restrict__ part) {
-    const int i = blockIdx.x * 64 + threadIdx.x;
-    float m = __builtin_inff();
-    for (int k = 0; k < kFieldRows / 4; k++) {
-        const int j = blockIdx.y * kFieldRows + 4 * k + threadIdx.y;
-        if (i >= dimx || j >= dimy) break;
-        const long idx = (long)j * P + i;
-        const Grad2 d = motion_gradients(u, idx, i, j, dimx, dimy, P);
-        const float q = (1.0f + d.dx.x) * (1.0f + d.dy.y) - d.dx.y * d.dy.x;
-        m = (q < m) ? q : m;
-    }
-    m = block_min(m);
-    if (threadIdx.x == 0 && threadIdx.y == 0) part[(long)blockIdx.y * gridDim.x + blockIdx.x] = m;
-}
+// ------------------------------------------------------------ min of per-block minima
 __global__ __launch_bounds__(1024) void min_final_kernel(const float *__restrict__ part, int n,
                                                          float *__restrict__ out) {
     float m = __builtin_inff();
@@ -845,12 +720,4 @@ __global__ __launch_bounds__(1024) void min_final_kernel(const float *__restrict
     m = wide_min(m);
     if (threadIdx.x == 0) *out = m;
 }
-void launch_jacobian_min(const float2 *u, int dimx, int dimy, int P, float *part, float *out,
-                         hipStream_t st) {
-    const dim3 g = field_grid(dimx, dimy);
-    hipLaunchKernelGGL(jacobian_min_kernel, g, dim3(64, 4), 0, st, u, dimx, dimy, P, part);
-    hipLaunchKernelGGL(min_final_kernel, dim3(1), dim3(1024), 0, st, part, (int)(g.x * g.y), out);
-    OF2D_HIP(hipGetLastError());
-}
-
 }  // namespace of2d

@@ -301,11 +301,15 @@ int increment_nblocks(int dimx, int dimy);
 // R and scal[0] = maxabs(R), scal[1] = 0.65f / maxabs
 void launch_increment(const float2 *u, const float4 *vel, float2 *R, int dimx, int dimy, int P,
                       float *part, float *scal, hipStream_t st);
-void launch_integrate_logger(float2 *u, const float2 *R, float2 *prev, const float *scal,
-                             int dimx, int dimy, int P, double *partial, hipStream_t st);
+// uo <- u + R dt (dt < 65) or u; Logger partials of uo against prev (against u
+// when prev is null); per-block Jacobian minima of uo into jpart and their min
+// into *jmin; vb.zw <- force(uo) and granule region 0 tagged with `epoch` for
+// the next sweep (fluid_kernels.hip fluid_step_kernel)
+void launch_fluid_step(const float2 *u, const float2 *R, float2 *uo, const float2 *prev,
+                       const float *scal, const float2 *dI, const float *It, float4 *vb, int dimx,
+                       int dimy, int P, void *H, unsigned epoch, double *lpart, float *jpart,
+                       float *jmin, hipStream_t st);
 void launch_logger(const float4 *vb, float2 *u, float2 *prev, int dimx, int dimy, int P,
                    double *partial, hipStream_t st);
-void launch_jacobian_min(const float2 *u, int dimx, int dimy, int P, float *part, float *out,
-                         hipStream_t st);
 
 }  // namespace of2d

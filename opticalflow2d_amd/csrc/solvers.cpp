@@ -155,24 +155,37 @@ int Registration::loop_demons(Level &L, int niter, int &final_buf) {
 int Registration::loop_fluid(Level &L, int niter) {
     const float mu = params_[0], lambda = params_[1];
     const float omega = params_.size() == 3 ? params_[2] : (float)0.66;  // OpticalFlowFluid.h:10
-    float2 *est = L.est[0].p;
     float2 *prev = L.tmp.p;
     L.tmp.zero(st_);  // Logger::prev starts at zero (Logger.cpp:13, new per refine)
     float *scal = d_scalar_ + 8;  // [0] maxabs, [1] dt, [2] min jacobian
     const int nb = increment_nblocks(L.dx, L.dy);
     const double npx = (double)L.dx * L.dy;
+    // L.est[0] is the estimate; L.force receives the next one and the two swap
+    // every iteration.  prev_separate: the Logger's previous motion is L.tmp,
+    // not the iteration's input estimate (first iteration, after a regrid);
+    // packed: vb.zw already holds the force of the estimate, tagged with the
+    // next epoch (fluid_step of the previous iteration).
+    bool prev_separate = true, packed = false;
     last_err_.clear();
     int iter;
     for (iter = 0; iter < niter; iter++) {
+        float2 *est = L.est[0].p;
         // get_force(force, motion) into vb.zw, then the SOR sweep of the velocity vb.xy
         const unsigned ep = ++epoch_;
-        launch_sor_pack(L.vb.p, est, L.dI.p, L.It.p, nullptr, L.dx, L.dy, L.P, L.sorH.p, ep, st_);
+        if (!packed)
+            launch_sor_pack(L.vb.p, est, L.dI.p, L.It.p, nullptr, L.dx, L.dy, L.P, L.sorH.p, ep,
+                            st_);
         launch_sor(L.vb.p, L.dx, L.dy, L.P, mu, lambda, omega, L.sorH.p, ep, L.sorTicket.p,
                    d_status_, st_);
         launch_increment(est, L.vb.p, L.increment.p, L.dx, L.dy, L.P, L.part.p, scal, st_);
-        launch_integrate_logger(est, L.increment.p, prev, scal, L.dx, L.dy, L.P, d_partial_, st_);
+        // integrate, Logger, Jacobian and the next iteration's force in one pass
+        launch_fluid_step(est, L.increment.p, L.force.p, prev_separate ? prev : nullptr, scal,
+                          L.dI.p, L.It.p, L.vb.p, L.dx, L.dy, L.P, L.sorH.p, ep + 1, d_partial_,
+                          L.part.p, scal + 2, st_);
+        std::swap(L.est[0], L.force);
+        prev_separate = false;
+        packed = true;
         launch_reduce_partials(d_partial_, nb, 1, d_sums_, st_);
-        launch_jacobian_min(est, L.dx, L.dy, L.P, L.part.p, scal + 2, st_);
         OF2D_HIP(hipMemcpyAsync(hs_.sums, d_sums_, sizeof(double) * 2, hipMemcpyDeviceToHost, st_));
         OF2D_HIP(hipMemcpyAsync(hs_.flt, scal, sizeof(float) * 3, hipMemcpyDeviceToHost, st_));
         check_status();
@@ -188,12 +201,17 @@ int Registration::loop_fluid(Level &L, int niter) {
         }
         if (jmin < 0.5) {  // regridding (ImageRegistrationFluid.cpp:108-124)
             print("Regridding on iteration: %d\tMin Jacobian: %.3f\n", iter, (double)jmin);
-            launch_accumulate(L.motion[L.mcur].p, est, L.motion[1 - L.mcur].p, L.dx, L.dy, L.P,
-                              st_);
+            // the Logger keeps this iteration's motion; the estimate restarts at zero
+            OF2D_HIP(hipMemcpyAsync(L.tmp.base, L.est[0].base, L.tmp.bytes(),
+                                    hipMemcpyDeviceToDevice, st_));
+            prev_separate = true;
+            launch_accumulate(L.motion[L.mcur].p, L.est[0].p, L.motion[1 - L.mcur].p, L.dx, L.dy,
+                              L.P, st_);
             L.mcur ^= 1;
             L.est[0].zero(st_);
             launch_warp(L.Imov.p, L.cur_motion(), L.Iaux.p, L.dx, L.dy, L.P, st_);
             launch_gradients(L.Iref.p, L.Iaux.p, L.dI.p, L.It.p, L.dx, L.dy, L.P, st_);
+            packed = false;  // the packed force was of the old estimate and gradients
         }
     }
     return iter;

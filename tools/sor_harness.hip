@@ -2,7 +2,8 @@
 // {v, b} field and prints per-strip start/end times and polled batches.
 //   hipcc -O3 -ffp-contract=off --offload-arch=gfx950 -I opticalflow2d_amd/csrc \
 //         tools/sor_harness.hip -o tools/sor_harness
-//   tools/sor_harness DIMX DIMY [REPS] [WAVES]
+//   tools/sor_harness DIMX DIMY [REPS]
+// (-DOF2D_SOR_GLEAD=N: granule vectors N batches ahead)
 #include "../opticalflow2d_amd/csrc/fluid_kernels.hip"
 
 #include <cstdio>
@@ -15,7 +16,7 @@ using namespace of2d;
 int main(int argc, char **argv) {
     const int dimx = argc > 1 ? atoi(argv[1]) : 8192, dimy = argc > 2 ? atoi(argv[2]) : 8192;
     const int reps = argc > 3 ? atoi(argv[3]) : 5;
-    const int waves = argc > 4 ? atoi(argv[4]) : 4;
+    const int waves = kSorGLead;  // printed as the variant
     const int P = pitch_for(dimx), ns = sor_nstrips(dimx);
     const size_t rows = (size_t)sor_rows(dimx, dimy) + 1;
     std::vector<float4> h((size_t)rows * P);
@@ -37,6 +38,11 @@ int main(int argc, char **argv) {
     OF2D_HIP(hipMemset(ticket, 0, 4));
     OF2D_HIP(hipMemset(status, 0, 4));
     OF2D_HIP(hipMalloc(&trace, 24 * (size_t)ns));
+    // zero motion / gradients / It for the pack (b = 0; the pack only tags
+    // granule region 0 and rewrites vb.zw)
+    float2 *zf;
+    OF2D_HIP(hipMalloc(&zf, (size_t)dimy * P * sizeof(float2)));
+    OF2D_HIP(hipMemset(zf, 0, (size_t)dimy * P * sizeof(float2)));
     float4 *vb0 = vb;
     hipEvent_t e0, e1;
     hipEventCreate(&e0);
@@ -45,11 +51,9 @@ int main(int argc, char **argv) {
     for (int r = 0; r < reps; r++) {
         const unsigned epoch = r + 1;
         // column-0 granules for strip 0 (what sor_pack writes)
-        launch_sor_pack(vb0, (const float2 *)vb0, (const float2 *)vb0, (const float *)vb0, nullptr,
-                        dimx, dimy, P, H, epoch, 0);
+        launch_sor_pack(vb0, zf, zf, (const float *)zf, nullptr, dimx, dimy, P, H, epoch, 0);
         hipEventRecord(e0, 0);
-        launch_sor_traced(vb0, dimx, dimy, P, 0.25f, 0.0f, 0.66f, H, epoch, ticket, status, trace, 0,
-                          waves);
+        launch_sor_traced(vb0, dimx, dimy, P, 0.25f, 0.0f, 0.66f, H, epoch, ticket, status, trace, 0);
         hipEventRecord(e1, 0);
         OF2D_HIP(hipDeviceSynchronize());
         float ms;
@@ -68,7 +72,7 @@ int main(int argc, char **argv) {
         double dur = 0;
         for (int i = 0; i < ns; i++) dur += (tr[3 * i + 1] - tr[3 * i]) * 0.01;
         dur /= ns;
-        printf("waves %d %dx%d strips %d: %.3f ms (timeline %.3f ms)  start lag %.2f us/strip  strip %.1f us"
+        printf("glead %d %dx%d strips %d: %.3f ms (timeline %.3f ms)  start lag %.2f us/strip  strip %.1f us"
                " = %.1f ns/step  polled batches %llu  status %u\n",
                waves, dimx, dimy, ns, ms, (t1 - t0) * 1e-5, lag, dur, dur * 1e3 / steps, polls, st);
         if (r == reps - 1 && ns > 1) {
@@ -87,6 +91,6 @@ int main(int argc, char **argv) {
         memcpy(u, &q, 16);
         for (int k = 0; k < 4; k++) hsh = (hsh ^ u[k]) * 1099511628211ull;
     }
-    printf("waves %d %dx%d reps %d: field hash %016llx\n", waves, dimx, dimy, reps, hsh);
+    printf("glead %d %dx%d reps %d: field hash %016llx\n", waves, dimx, dimy, reps, hsh);
     return 0;
 }
