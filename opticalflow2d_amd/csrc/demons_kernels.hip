@@ -517,25 +517,30 @@ __global__ __launch_bounds__(256) void demons_fused_kernel(
                 if (valid[q]) wt[tid + 256 * (q0 + q)] = in[q] ? res[q] : 0.0f;
         }
     }
-    // Iref of the correction slots, loaded while the warp tile completes
-    constexpr int NC = (CW * CH + 255) / 256;
+    // 2. correction slot (r, cc) <-> pixel (x0 - c + cc, y0 - c + r), cc < CW,
+    // enumerated at the warped tile's pitch WW (index s = r * WW + cc; the
+    // lanes with cc >= CW idle): a wave's reads of wt are then one contiguous
+    // run with no row seam inside a 32-lane group (no LDS bank conflicts), and
+    // its writes of ct stay contiguous.  Iref of the slots is loaded while
+    // the warp tile completes.
+    constexpr int NC = (WW * CH + 255) / 256;
     float iref[NC];
 #pragma unroll
     for (int q = 0; q < NC; q++) {
-        const int s = tid + 256 * q, r = s / CW;
-        const int i = x0 - c + (s - r * CW), j = y0 - c + r;
-        iref[q] = (s < CW * CH && (unsigned)j < (unsigned)dimy) ? Iref[(long)j * P + i] : 0.0f;
+        const int s = tid + 256 * q, r = s / WW, cc = s - r * WW;
+        const int i = x0 - c + cc, j = y0 - c + r;
+        iref[q] = (s < WW * CH && cc < CW && (unsigned)j < (unsigned)dimy)
+                      ? Iref[(long)j * P + i]
+                      : 0.0f;
     }
     __syncthreads();
     {
-        // 2. slot s <-> pixel (x0 - c + s % CW, y0 - c + s / CW); j-lines
-        // outside the image hold 0 (their linear index is outside [0, N))
+        // j-lines outside the image hold 0 (their linear index is outside [0, N))
         bool zero = false;
 #pragma unroll
         for (int q = 0; q < NC; q++) {
-            const int s = tid + 256 * q;
-            if (s < CW * CH) {
-                const int r = s / CW, cc = s - r * CW;
+            const int s = tid + 256 * q, r = s / WW, cc = s - r * WW;
+            if (s < WW * CH && cc < CW) {
                 const int i = x0 - c + cc, j = y0 - c + r;
                 float2 cv = make_float2(0.0f, 0.0f);
                 if ((unsigned)j < (unsigned)dimy) {
@@ -556,7 +561,7 @@ __global__ __launch_bounds__(256) void demons_fused_kernel(
                         gy = (w[WW] - w[-WW]) / 2.0f;
                     cv = demons_corr(gx, gy, w0 - iref[q], sigma_isq, sigma_xsq, zero);
                 }
-                ct[s] = cv;
+                ct[r * CW + cc] = cv;
             }
         }
         if (zero) atomicOr(status, kStatusDivZero);
@@ -702,9 +707,23 @@ void launch_demons_update(const float *Iref, const float *Imov, const float2 *u,
     // beside it (two small launches, ~10 % of an iteration when serialised)
     const bool fork = side && ev_fork && ev_join;
     hipStream_t es = fork ? side : st;
+    // the join: st waits for everything enqueued on the side stream, also when
+    // a launch below throws
+    struct Join {
+        hipStream_t st, side;
+        hipEvent_t ev;
+        bool armed = false;
+        ~Join() {
+            if (armed) {
+                (void)hipEventRecord(ev, side);
+                (void)hipStreamWaitEvent(st, ev, 0);
+            }
+        }
+    } join{st, side, ev_join};
     if (fork) {
         OF2D_HIP(hipEventRecord(ev_fork, st));
         OF2D_HIP(hipStreamWaitEvent(side, ev_fork, 0));
+        join.armed = true;
     }
     // the correction the edge tiles' convolutions read: tile columns
     // [0, nl + 1) and [gx - nr - 1, gx) (wrapped taps reach the far edge)
@@ -713,7 +732,6 @@ void launch_demons_update(const float *Iref, const float *Imov, const float2 *u,
                        nl + 1, gx);
     OF2D_HIP(hipGetLastError());
     smooth_compose_tiles(corr, u, out, dimx, dimy, P, a, mode, nl + nr, nl, gx, es);
-    if (fork) OF2D_HIP(hipEventRecord(ev_join, side));
     const dim3 g(ni, conv_grid(dimx, dimy).y);
     auto go = [&](auto kern) {
         hipLaunchKernelGGL(kern, g, dim3(64, kCThreadsY), 0, st, Iref, Imov, u, out, dimx, dimy, P,
@@ -725,7 +743,6 @@ void launch_demons_update(const float *Iref, const float *Imov, const float2 *u,
         default: go(demons_fused_kernel<7, kCr>); break;
     }
     OF2D_HIP(hipGetLastError());
-    if (fork) OF2D_HIP(hipStreamWaitEvent(st, ev_join, 0));
 }
 
 void launch_smooth_norm(const float2 *umid, const float2 *prev, float2 *out, int dimx, int dimy,
