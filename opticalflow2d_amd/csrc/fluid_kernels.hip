@@ -248,8 +248,10 @@ __global__ __launch_bounds__(64) void sor_strip_kernel(float4 *__restrict__ vb, 
     if (lane == 0) s_strip = (int)(atomicAdd(ticket, 1u) % (unsigned)nstrips);
     __syncthreads();
     const int I = __builtin_amdgcn_readfirstlane(s_strip);
-    // optional timeline (tools/sor_harness.hip): start, end, polled batches
+    // optional timeline (tools/sor_harness.hip): start, end, polled batches,
+    // shader cycles
     const unsigned long long t_start = trace ? __builtin_amdgcn_s_memrealtime() : 0;
+    const unsigned long long c_start = trace ? __builtin_amdgcn_s_memtime() : 0;
     unsigned npoll = 0;
     const int c0 = 1 + kSorCols * I;  // lane 0's column
     const int c = c0 + lane;
@@ -369,9 +371,10 @@ __global__ __launch_bounds__(64) void sor_strip_kernel(float4 *__restrict__ vb, 
             group(Flag<true>{}, g);
     }
     if (trace && lane == 0) {
-        trace[3 * I] = t_start;
-        trace[3 * I + 1] = __builtin_amdgcn_s_memrealtime();
-        trace[3 * I + 2] = npoll;
+        trace[4 * I] = t_start;
+        trace[4 * I + 1] = __builtin_amdgcn_s_memrealtime();
+        trace[4 * I + 2] = npoll;
+        trace[4 * I + 3] = __builtin_amdgcn_s_memtime() - c_start;
     }
 }
 

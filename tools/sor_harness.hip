@@ -37,7 +37,7 @@ int main(int argc, char **argv) {
     OF2D_HIP(hipMalloc(&status, 4));
     OF2D_HIP(hipMemset(ticket, 0, 4));
     OF2D_HIP(hipMemset(status, 0, 4));
-    OF2D_HIP(hipMalloc(&trace, 24 * (size_t)ns));
+    OF2D_HIP(hipMalloc(&trace, 32 * (size_t)ns));
     // zero motion / gradients / It for the pack (b = 0; the pack only tags
     // granule region 0 and rewrites vb.zw)
     float2 *zf;
@@ -47,7 +47,7 @@ int main(int argc, char **argv) {
     hipEvent_t e0, e1;
     hipEventCreate(&e0);
     hipEventCreate(&e1);
-    std::vector<unsigned long long> tr(3 * (size_t)ns);
+    std::vector<unsigned long long> tr(4 * (size_t)ns);
     for (int r = 0; r < reps; r++) {
         const unsigned epoch = r + 1;
         // column-0 granules for strip 0 (what sor_pack writes)
@@ -63,23 +63,26 @@ int main(int argc, char **argv) {
         OF2D_HIP(hipMemcpy(tr.data(), trace, tr.size() * 8, hipMemcpyDeviceToHost));
         unsigned long long t0 = ~0ull, t1 = 0, polls = 0;
         for (int i = 0; i < ns; i++) {
-            t0 = std::min(t0, tr[3 * i]);
-            t1 = std::max(t1, tr[3 * i + 1]);
-            polls += tr[3 * i + 2];
+            t0 = std::min(t0, tr[4 * i]);
+            t1 = std::max(t1, tr[4 * i + 1]);
+            polls += tr[4 * i + 2];
         }
         const double steps = dimy + 126.0;
-        const double lag = ns > 1 ? (tr[3 * (ns - 1)] - tr[0]) * 0.01 / (ns - 1) : 0;  // us
+        const double lag = ns > 1 ? (tr[4 * (ns - 1)] - tr[0]) * 0.01 / (ns - 1) : 0;  // us
         double dur = 0;
-        for (int i = 0; i < ns; i++) dur += (tr[3 * i + 1] - tr[3 * i]) * 0.01;
+        for (int i = 0; i < ns; i++) dur += (tr[4 * i + 1] - tr[4 * i]) * 0.01;
         dur /= ns;
         printf("glead %d %dx%d strips %d: %.3f ms (timeline %.3f ms)  start lag %.2f us/strip  strip %.1f us"
                " = %.1f ns/step  polled batches %llu  status %u\n",
                waves, dimx, dimy, ns, ms, (t1 - t0) * 1e-5, lag, dur, dur * 1e3 / steps, polls, st);
+        // strip 0 never waits for a neighbour: its cycles per step and clock
+        printf("  strip 0: %.1f cycles/step, clock %.3f GHz\n", tr[3] / steps,
+               tr[3] / ((tr[1] - tr[0]) * 10.0));
         if (r == reps - 1 && ns > 1) {
             printf("  strip: start_us end_us polls\n");
             for (int i = 0; i < ns; i += std::max(1, ns / 12))
-                printf("  %4d: %9.2f %9.2f %llu\n", i, (tr[3 * i] - t0) * 0.01,
-                       (tr[3 * i + 1] - t0) * 0.01, tr[3 * i + 2]);
+                printf("  %4d: %9.2f %9.2f %llu\n", i, (tr[4 * i] - t0) * 0.01,
+                       (tr[4 * i + 1] - t0) * 0.01, tr[4 * i + 2]);
         }
     }
     // final field after `reps` sweeps from the seeded start: identical for
