@@ -586,7 +586,7 @@ __global__ __launch_bounds__(256) void demons_fused_kernel(
 // u_new = u_mid (*) G(sigma_diffusion); Logger partials sum ||u_new - prev||,
 // sum ||prev|| per block (fixed order)
 template <int KW, int R = kCr, bool PK = true>
-__global__ __launch_bounds__(256) void smooth_norm_kernel(const float2 *__restrict__ umid,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KW == 7 ? 7 : 8))) void smooth_norm_kernel(const float2 *__restrict__ umid,
                                                           const float2 *__restrict__ prev,
                                                           float2 *__restrict__ out, int dimx,
                                                           int dimy, int P, ConvArgs a,
