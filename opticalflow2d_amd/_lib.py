@@ -14,7 +14,8 @@ import numpy as np
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(PKG_DIR, "csrc")
-LIB_PATH = os.path.join(PKG_DIR, "libof2d.so")
+# OF2D_LIB_PATH: another build of the same library (tools/ A/B runs only)
+LIB_PATH = os.environ.get("OF2D_LIB_PATH") or os.path.join(PKG_DIR, "libof2d.so")
 
 OF2D_OK = 0
 OF2D_ERR_INVALID_ARGUMENT = 1
