@@ -41,7 +41,12 @@ typedef float v2f __attribute__((ext_vector_type(2)));
 // warp2d values of Imov at B pixels (a[q], b[q]) with motion u
 // (Image.cpp:137-174); in[q] = the pixel is valid and inside the image (res[q]
 // is meaningful only then).  Every load of the batch is issued before any is
-// used.
+// used, and none is conditional: a slot outside the image, or a tap pattern
+// outside it, reads element 0, and the taps g[1], g[P], g[P+1] of an in-image
+// pixel stay inside the allocation (pitch padding and the zeroed ghost j-line
+// below the last row, of2d_device.h); the reference's conditional terms are
+// selects between the sums with and without the term, so no exec-mask branch
+// is needed and every kept value is the reference's.
 template <int B>
 __device__ __forceinline__ void warp_batch(const float *__restrict__ Imov,
                                            const float2 *__restrict__ u, const int a[B],
@@ -52,9 +57,9 @@ __device__ __forceinline__ void warp_batch(const float *__restrict__ Imov,
 #pragma unroll
     for (int q = 0; q < B; q++) {
         in[q] = valid[q] && a[q] >= 0 && a[q] < dimx && b[q] >= 0 && b[q] < dimy;
-        const long idx = (long)b[q] * P + a[q];
-        m[q] = in[q] ? u[idx] : make_float2(0.0f, 0.0f);
-        own[q] = in[q] ? Imov[idx] : 0.0f;
+        const unsigned idx = in[q] ? (unsigned)(b[q] * P + a[q]) : 0u;
+        m[q] = u[idx];
+        own[q] = Imov[idx];
     }
     float t00[B], t10[B], t01[B], t11[B], fx[B], fy[B];
     bool ok[B], ax[B], ay[B];
@@ -69,34 +74,29 @@ __device__ __forceinline__ void warp_batch(const float *__restrict__ Imov,
         ok[q] = in[q] && !(dx < 0 || dx >= dimx || dy < 0 || dy >= dimy);
         ax[q] = dx < dimx - 1;
         ay[q] = dy < dimy - 1;
-        const float *g = Imov + (long)dy * P + dx;
-        t00[q] = ok[q] ? g[0] : 0.0f;
-        t10[q] = ok[q] && ax[q] ? g[1] : 0.0f;
-        t01[q] = ok[q] && ay[q] ? g[P] : 0.0f;
-        t11[q] = ok[q] && ax[q] && ay[q] ? g[P + 1] : 0.0f;
+        const float *g = Imov + (ok[q] ? (unsigned)(dy * P + dx) : 0u);
+        t00[q] = g[0];
+        t10[q] = g[1];
+        t01[q] = g[P];
+        t11[q] = g[P + 1];
     }
 #pragma unroll
     for (int q = 0; q < B; q++) {
-        float out = own[q];
-        if (ok[q]) {
-            const float gx = fx[q], gy = fy[q];
-            float val = (t00[q] * (1 - gx)) * (1 - gy);
-            float wt = (1 - gx) * (1 - gy);
-            if (ax[q]) {
-                val += (t10[q] * gx) * (1 - gy);
-                wt += gx * (1 - gy);
-            }
-            if (ay[q]) {
-                val += (t01[q] * (1 - gx)) * gy;
-                wt += (1 - gx) * gy;
-            }
-            if (ax[q] && ay[q]) {
-                val += (t11[q] * gx) * gy;
-                wt += gx * gy;
-            }
-            if (wt != 0) out = val / wt;
-        }
-        res[q] = out;
+        const float gx = fx[q], gy = fy[q];
+        float val = (t00[q] * (1 - gx)) * (1 - gy);
+        float wt = (1 - gx) * (1 - gy);
+        const float v10 = val + (t10[q] * gx) * (1 - gy), w10 = wt + gx * (1 - gy);
+        val = ax[q] ? v10 : val;
+        wt = ax[q] ? w10 : wt;
+        const float v01 = val + (t01[q] * (1 - gx)) * gy, w01 = wt + (1 - gx) * gy;
+        val = ay[q] ? v01 : val;
+        wt = ay[q] ? w01 : wt;
+        const bool axy = ax[q] && ay[q];
+        const float v11 = val + (t11[q] * gx) * gy, w11 = wt + gx * gy;
+        val = axy ? v11 : val;
+        wt = axy ? w11 : wt;
+        const float r = val / wt;
+        res[q] = (ok[q] && wt != 0) ? r : (in[q] ? own[q] : 0.0f);
     }
 }
 
@@ -352,7 +352,9 @@ __device__ __forceinline__ void convR(const float2 *tile, const ConvArgs &a, int
 // Motion::accumulate (Motion.cpp:113-178) at pixels (i, j0..j0+G-1) with
 // increments cv: u(x) <- c(x) + u_old(x + c(x)), bilinear with in-range taps
 // renormalised; out of range keeps u_old(x).  Every gather of the G pixels is
-// issued before any is used.
+// issued before any is used; as in warp_batch, no load is conditional (an
+// out-of-range tap pattern reads element 0) and the conditional terms are
+// selects.
 template <int G>
 __device__ __forceinline__ void compose_px(const float2 *__restrict__ u, int i, int j0, int dimx,
                                            int dimy, int P, const float2 cv[G], float2 o[G]) {
@@ -363,7 +365,7 @@ __device__ __forceinline__ void compose_px(const float2 *__restrict__ u, int i, 
     for (int k = 0; k < G; k++) {
         const int j = j0 + k;
         const bool in = j < dimy;
-        own[k] = in ? u[(long)j * P + i] : make_float2(0.0f, 0.0f);
+        own[k] = u[in ? (unsigned)(j * P + i) : 0u];
         const float px = (float)i + cv[k].x;
         const int dx = (int)floorf(px);
         fx[k] = px - (float)dx;
@@ -373,39 +375,36 @@ __device__ __forceinline__ void compose_px(const float2 *__restrict__ u, int i, 
         ok[k] = in && !(dx < 0 || dx >= dimx || dy < 0 || dy >= dimy);
         ax[k] = dx < dimx - 1;
         ay[k] = dy < dimy - 1;
-        const float2 *b = u + (long)dy * P + dx;
-        const float2 z = make_float2(0.0f, 0.0f);
-        t00[k] = ok[k] ? b[0] : z;
-        t10[k] = ok[k] && ax[k] ? b[1] : z;
-        t01[k] = ok[k] && ay[k] ? b[P] : z;
-        t11[k] = ok[k] && ax[k] && ay[k] ? b[P + 1] : z;
+        const float2 *b = u + (ok[k] ? (unsigned)(dy * P + dx) : 0u);
+        t00[k] = b[0];
+        t10[k] = b[1];
+        t01[k] = b[P];
+        t11[k] = b[P + 1];
     }
 #pragma unroll
     for (int k = 0; k < G; k++) {
         const float2 c = cv[k];
-        o[k] = own[k];
-        if (ok[k]) {
-            o[k] = c;
-            const float gx = fx[k], gy = fy[k];
-            const v2f wx0 = v2f{1 - gx, 1 - gx}, wx1 = v2f{gx, gx};
-            const v2f wy0 = v2f{1 - gy, 1 - gy}, wy1 = v2f{gy, gy};
-            // (t * wx) * wy per component, added in the reference's tap order
-            v2f v = (v2f{t00[k].x, t00[k].y} * wx0) * wy0;
-            float w = (1 - gx) * (1 - gy);
-            if (ax[k]) {
-                v = v + (v2f{t10[k].x, t10[k].y} * wx1) * wy0;
-                w += gx * (1 - gy);
-            }
-            if (ay[k]) {
-                v = v + (v2f{t01[k].x, t01[k].y} * wx0) * wy1;
-                w += (1 - gx) * gy;
-            }
-            if (ax[k] && ay[k]) {
-                v = v + (v2f{t11[k].x, t11[k].y} * wx1) * wy1;
-                w += gx * gy;
-            }
-            if (w != 0) o[k] = make_float2(c.x + v.x / w, c.y + v.y / w);
-        }
+        const float gx = fx[k], gy = fy[k];
+        const v2f wx0 = v2f{1 - gx, 1 - gx}, wx1 = v2f{gx, gx};
+        const v2f wy0 = v2f{1 - gy, 1 - gy}, wy1 = v2f{gy, gy};
+        // (t * wx) * wy per component, added in the reference's tap order
+        v2f v = (v2f{t00[k].x, t00[k].y} * wx0) * wy0;
+        float w = (1 - gx) * (1 - gy);
+        const v2f v10 = v + (v2f{t10[k].x, t10[k].y} * wx1) * wy0;
+        const float w10 = w + gx * (1 - gy);
+        v = ax[k] ? v10 : v;
+        w = ax[k] ? w10 : w;
+        const v2f v01 = v + (v2f{t01[k].x, t01[k].y} * wx0) * wy1;
+        const float w01 = w + (1 - gx) * gy;
+        v = ay[k] ? v01 : v;
+        w = ay[k] ? w01 : w;
+        const bool axy = ax[k] && ay[k];
+        const v2f v11 = v + (v2f{t11[k].x, t11[k].y} * wx1) * wy1;
+        const float w11 = w + gx * gy;
+        v = axy ? v11 : v;
+        w = axy ? w11 : w;
+        const float2 q = make_float2(c.x + v.x / w, c.y + v.y / w);
+        o[k] = ok[k] ? (w != 0 ? q : c) : own[k];
     }
 }
 
