@@ -536,6 +536,22 @@ __global__ __launch_bounds__(256) void demons_fused_kernel(
     {
         // j-lines outside the image hold 0 (their linear index is outside [0, N))
         bool zero = false;
+        // block-uniform: every slot has both x and both y neighbours in the
+        // image (central differences of gradients.h:9-32 everywhere)
+        const bool tin = x0 - c >= 1 && x0 - c + CW <= dimx - 1 && y0 - c >= 1 &&
+                         y0 - c + CH <= dimy - 1;
+        if (tin) {
+#pragma unroll
+            for (int q = 0; q < NC; q++) {
+                const int s = tid + 256 * q, r = s / WW, cc = s - r * WW;
+                if (s < WW * CH && cc < CW) {
+                    const float *w = wt + (r + 1) * WW + (cc + 1);
+                    const float gx = (w[1] - w[-1]) / 2.0f, gy = (w[WW] - w[-WW]) / 2.0f;
+                    ct[r * CW + cc] = demons_corr(gx, gy, w[0] - iref[q], sigma_isq, sigma_xsq,
+                                                  zero);
+                }
+            }
+        } else {
 #pragma unroll
         for (int q = 0; q < NC; q++) {
             const int s = tid + 256 * q, r = s / WW, cc = s - r * WW;
@@ -562,6 +578,7 @@ __global__ __launch_bounds__(256) void demons_fused_kernel(
                 }
                 ct[r * CW + cc] = cv;
             }
+        }
         }
         if (zero) atomicOr(status, kStatusDivZero);
     }
