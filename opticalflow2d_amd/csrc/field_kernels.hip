@@ -184,38 +184,40 @@ void launch_upsample_motion(const float2 *in, int dxi, int dyi, int Pi, float2 *
 // Image::warp2d (src/Image.cpp:119-182): pull-back bilinear sample of src at
 // (i + u.x, j + u.y); out-of-range floor keeps the original pixel; at the
 // right/top edge only in-range taps are used, renormalised by their weight.
+//
+// Branch-free: the taps are loaded unconditionally (an out-of-range tap
+// pattern reads element 0; g[1], g[P], g[P+1] of an in-image pixel stay in the
+// allocation: pitch padding and the zeroed ghost j-line below the last row)
+// and the reference's conditional terms are selects.
 __global__ void warp_kernel(const float *__restrict__ src, const float2 *__restrict__ u,
                             float *__restrict__ dst, int dimx, int dimy, int P) {
     OF2D_PX_PROLOGUE(dimx, dimy)
     const long idx = (long)j * P + i;
     const float2 m = u[idx];
-    float out = src[idx];
+    const float own = src[idx];
     const float px = (float)i + m.x;
     const int dx = (int)floorf(px);
     const float fx = px - (float)dx;
     const float py = (float)j + m.y;
     const int dy = (int)floorf(py);
     const float fy = py - (float)dy;
-    if (!(dx < 0 || dx >= dimx || dy < 0 || dy >= dimy)) {
-        const float *b = src + (long)dy * P + dx;
-        float val = (b[0] * (1 - fx)) * (1 - fy);
-        float w = (1 - fx) * (1 - fy);
-        const bool ax = dx < dimx - 1, ay = dy < dimy - 1;
-        if (ax) {
-            val += (b[1] * fx) * (1 - fy);
-            w += fx * (1 - fy);
-        }
-        if (ay) {
-            val += (b[P] * (1 - fx)) * fy;
-            w += (1 - fx) * fy;
-        }
-        if (ax && ay) {
-            val += (b[P + 1] * fx) * fy;
-            w += fx * fy;
-        }
-        if (w != 0) out = val / w;
-    }
-    dst[idx] = out;
+    const bool ok = !(dx < 0 || dx >= dimx || dy < 0 || dy >= dimy);
+    const bool ax = dx < dimx - 1, ay = dy < dimy - 1;
+    const float *b = src + (ok ? (unsigned)(dy * P + dx) : 0u);
+    const float t00 = b[0], t10 = b[1], t01 = b[P], t11 = b[P + 1];
+    float val = (t00 * (1 - fx)) * (1 - fy);
+    float w = (1 - fx) * (1 - fy);
+    const float v10 = val + (t10 * fx) * (1 - fy), w10 = w + fx * (1 - fy);
+    val = ax ? v10 : val;
+    w = ax ? w10 : w;
+    const float v01 = val + (t01 * (1 - fx)) * fy, w01 = w + (1 - fx) * fy;
+    val = ay ? v01 : val;
+    w = ay ? w01 : w;
+    const float v11 = val + (t11 * fx) * fy, w11 = w + fx * fy;
+    val = (ax && ay) ? v11 : val;
+    w = (ax && ay) ? w11 : w;
+    const float q = val / w;
+    dst[idx] = (ok && w != 0) ? q : own;
 }
 void launch_warp(const float *src, const float2 *u, float *dst, int dimx, int dimy, int P,
                  hipStream_t st) {
@@ -264,43 +266,43 @@ void launch_gradients(const float *Iref, const float *Iaux, float2 *dI, float *I
 // ------------------------------------------------------------ composition
 // Motion::accumulate (src/Motion.cpp:113-178): u(x) <- v(x) + u_old(x + v(x))
 // (bilinear, renormalised); out-of-range keeps u_old(x).
+// Branch-free as warp_kernel.
 __global__ void accumulate_kernel(const float2 *__restrict__ mo, const float2 *__restrict__ v,
                                   float2 *__restrict__ mn, int dimx, int dimy, int P) {
     OF2D_PX_PROLOGUE(dimx, dimy)
     const long idx = (long)j * P + i;
     const float2 c = v[idx];
-    float2 out = mo[idx];
+    const float2 own = mo[idx];
     const float px = (float)i + c.x;
     const int dx = (int)floorf(px);
     const float fx = px - (float)dx;
     const float py = (float)j + c.y;
     const int dy = (int)floorf(py);
     const float fy = py - (float)dy;
-    if (!(dx < 0 || dx >= dimx || dy < 0 || dy >= dimy)) {
-        out = c;
-        const float2 *b = mo + (long)dy * P + dx;
-        float vx = (b[0].x * (1 - fx)) * (1 - fy);
-        float vy = (b[0].y * (1 - fx)) * (1 - fy);
-        float w = (1 - fx) * (1 - fy);
-        const bool ax = dx < dimx - 1, ay = dy < dimy - 1;
-        if (ax) {
-            vx = vx + (b[1].x * fx) * (1 - fy);
-            vy = vy + (b[1].y * fx) * (1 - fy);
-            w += fx * (1 - fy);
-        }
-        if (ay) {
-            vx = vx + (b[P].x * (1 - fx)) * fy;
-            vy = vy + (b[P].y * (1 - fx)) * fy;
-            w += (1 - fx) * fy;
-        }
-        if (ax && ay) {
-            vx = vx + (b[P + 1].x * fx) * fy;
-            vy = vy + (b[P + 1].y * fx) * fy;
-            w += fx * fy;
-        }
-        if (w != 0) out = make_float2(c.x + vx / w, c.y + vy / w);
-    }
-    mn[idx] = out;
+    const bool ok = !(dx < 0 || dx >= dimx || dy < 0 || dy >= dimy);
+    const bool ax = dx < dimx - 1, ay = dy < dimy - 1, axy = ax && ay;
+    const float2 *b = mo + (ok ? (unsigned)(dy * P + dx) : 0u);
+    const float2 t00 = b[0], t10 = b[1], t01 = b[P], t11 = b[P + 1];
+    float vx = (t00.x * (1 - fx)) * (1 - fy);
+    float vy = (t00.y * (1 - fx)) * (1 - fy);
+    float w = (1 - fx) * (1 - fy);
+    const float x10 = vx + (t10.x * fx) * (1 - fy), y10 = vy + (t10.y * fx) * (1 - fy);
+    const float w10 = w + fx * (1 - fy);
+    vx = ax ? x10 : vx;
+    vy = ax ? y10 : vy;
+    w = ax ? w10 : w;
+    const float x01 = vx + (t01.x * (1 - fx)) * fy, y01 = vy + (t01.y * (1 - fx)) * fy;
+    const float w01 = w + (1 - fx) * fy;
+    vx = ay ? x01 : vx;
+    vy = ay ? y01 : vy;
+    w = ay ? w01 : w;
+    const float x11 = vx + (t11.x * fx) * fy, y11 = vy + (t11.y * fx) * fy;
+    const float w11 = w + fx * fy;
+    vx = axy ? x11 : vx;
+    vy = axy ? y11 : vy;
+    w = axy ? w11 : w;
+    const float2 q = make_float2(c.x + vx / w, c.y + vy / w);
+    mn[idx] = ok ? (w != 0 ? q : c) : own;
 }
 void launch_accumulate(const float2 *m_old, const float2 *v, float2 *m_new, int dimx, int dimy,
                        int P, hipStream_t st) {
