@@ -1,10 +1,10 @@
 #!/bin/bash
-# Round-2 GPU session r: final-state check after the fluid / Demons changes:
-# the GPU suite, smoke, bench (driver command), rocprofv3 kernel stats of the
+# Round-2 GPU session r: final-state check (GPU suite, smoke, bench driver command,
+# rocprofv3 kernel stats of the
 # driver command, the secondary configurations with their kernel stats.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-OUT=gpurun_out/r02r
+OUT=gpurun_out/${R02_TAG:-r02r}
 mkdir -p $OUT
 R=$PWD
 step() {  # step <name> <timeout> <cmd...>
