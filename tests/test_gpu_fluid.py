@@ -99,12 +99,29 @@ def test_elastic_wide_sweep(gpu, oracle):
 
 
 def test_fluid_config4_full_size_8192(gpu, oracle):
-    """BASELINE config 4 at its full size: 8192^2, 3-level pyramid, one fixed
-    iteration per level (130 wavefront strips at the finest level), bit for bit
+    """BASELINE config 4 at its full size: 8192^2, 3-level pyramid, two fixed
+    iterations per level (130 wavefront strips at the finest level; the second
+    iteration sweeps the force the first one's fused step packed), bit for bit
     with identical printed Dumax lines."""
     ref, mov = S.shifted_disk(8192)
-    g, w, gt, ot = run_both(gpu, oracle, (8192, 8192), [1, 1, 1], 2, 5, [0.25, 0.0], 1, ref, mov,
+    g, w, gt, ot = run_both(gpu, oracle, (8192, 8192), [2, 2, 2], 2, 5, [0.25, 0.0], 1, ref, mov,
                             fixed_iters=1)
     assert g["iters"] == w["iters"]
     assert np.array_equal(g["motion"], w["motion"])
     assert body(gt) == body(ot)
+
+
+def test_fluid_timestep_skip_and_integrate(gpu, oracle):
+    """A faint difference image (mov = ref + 0.08 (texture shift - ref)) keeps
+    maxabs(R) small at first: dt = 0.65 / maxabs >= 65 and the reference skips
+    the integration (OpticalFlowFluid.cpp:135-137), so the fused step copies u
+    unchanged; later iterations integrate, and some skip again."""
+    ref, mov = S.texture_pair(96, seed=5)
+    mov = ref + 0.08 * (mov - ref)
+    g, w, gt, ot = run_both(gpu, oracle, (96, 96), [25], 0, 5, [0.25, 0.0], 1, ref, mov,
+                            fixed_iters=1)
+    assert g["iters"] == w["iters"]
+    assert np.array_equal(g["motion"], w["motion"])
+    assert body(gt) == body(ot)
+    dts = [float(l.split("Timestep:")[1]) for l in body(gt) if "Timestep:" in l]
+    assert any(t >= 65.0 for t in dts) and any(t < 65.0 for t in dts), dts
