@@ -8,7 +8,7 @@ TAG=$1 CFG=$2 N=${3:-2} TF=$4
 OUT=gpurun_out/ab_$TAG
 mkdir -p $OUT
 B=$PWD/tools/lib_alt.so
-if [ -n "$TF" ]; then
+if [ -n "$TF" ] && [ "$TF" != "-" ]; then
   OF2D_LIB_PATH=$B timeout -k 10 600 python -u -m pytest $TF -x -q --timeout 300 --timeout-method thread > $OUT/tests_B.log 2>&1 || { tail -n 20 $OUT/tests_B.log; exit 1; }
   tail -n 1 $OUT/tests_B.log
 fi
