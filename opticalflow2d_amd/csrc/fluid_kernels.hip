@@ -182,6 +182,15 @@ constexpr int kSorGLead = OF2D_SOR_GLEAD;
 constexpr int kSorGLead = 2;  // granule vectors are loaded this many batches ahead
 #endif
 static_assert(kSorGLead >= 1 && kSorGLead <= kSorNB, "granule vectors rotate through GV[kSorNB]");
+// cache policy of the row loads / value stores (tools/sor_harness A/B builds
+// override them): the row loads are non-temporal (aux 2), 0.5-1 % per sweep
+// at 4096^2 and 8192^2 (profiles/r02_w_sor_cache_ab.log)
+#ifndef OF2D_SOR_LD_AUX
+#define OF2D_SOR_LD_AUX 2
+#endif
+#ifndef OF2D_SOR_ST_AUX
+#define OF2D_SOR_ST_AUX 0
+#endif
 constexpr unsigned kOob = 0x40000000u;   // voffset beyond num_records: the access is dropped
 constexpr int kNumRecords = 0x20000000;  // bytes addressable from a moving rsrc base
 constexpr int kRsrcFlags = 0x00020000;
@@ -322,7 +331,8 @@ __global__ __launch_bounds__(64) void sor_strip_kernel(float4 *__restrict__ vb, 
             if ((unsigned)(r - 1) >= (unsigned)(dimy - 2)) out = C;  // boundary row: OLD value
         }
         __builtin_amdgcn_raw_buffer_store_b64(
-            v2u{__float_as_uint(out.x), __float_as_uint(out.y)}, rs, voff_st, j * (int)P16, 0);
+            v2u{__float_as_uint(out.x), __float_as_uint(out.y)}, rs, voff_st, j * (int)P16,
+            OF2D_SOR_ST_AUX);
         __builtin_amdgcn_raw_buffer_store_b128(
             v4u{epoch, __float_as_uint(out.x), __float_as_uint(out.y), epoch}, ps,
             voff_pub + (unsigned)j * 16u, 0, 16 /* sc1 */);
@@ -359,8 +369,8 @@ __global__ __launch_bounds__(64) void sor_strip_kernel(float4 *__restrict__ vb, 
             // batch b of the next group: rows 32 further down
 #pragma unroll
             for (int j = 0; j < kSorB; j++)
-                X[b][j] = __builtin_amdgcn_raw_buffer_load_b128(rs, voff_ld,
-                                                                (4 + kSorG + j) * (int)P16, 0);
+                X[b][j] = __builtin_amdgcn_raw_buffer_load_b128(
+                    rs, voff_ld, (4 + kSorG + j) * (int)P16, OF2D_SOR_LD_AUX);
         }
     };
 
