@@ -174,7 +174,14 @@ __device__ __forceinline__ float wide_min(float m) {
 namespace {
 constexpr int kSorCols = 63;  // real columns per strip (lanes 0..62)
 constexpr int kSorB = 8;      // rows per batch
-constexpr int kSorNB = 4;     // batches per group
+// batches per group: the row loads run one group (kSorNB * 8 rows) ahead.  40
+// rows: 1.4-3.4 % per sweep faster than 32 at 2048^2-8192^2 (the loads wait on
+// HBM at 32); 48 spill into AGPR moves (profiles/r02_x_sor_lead_ab.log)
+#ifdef OF2D_SOR_NB  // tools/sor_harness.hip A/B builds
+constexpr int kSorNB = OF2D_SOR_NB;
+#else
+constexpr int kSorNB = 5;
+#endif
 constexpr int kSorG = kSorB * kSorNB;
 #ifdef OF2D_SOR_GLEAD  // tools/sor_harness.hip A/B builds only
 constexpr int kSorGLead = OF2D_SOR_GLEAD;
