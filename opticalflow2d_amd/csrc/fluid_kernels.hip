@@ -287,16 +287,19 @@ __global__ __launch_bounds__(64) void sor_strip_kernel(float4 *__restrict__ vb, 
 
     const int s0 = -3;
     const int s1 = dimy + 122;  // lane 62 publishes ghost row dimy - 1 at this step
-    // skewed row of the first step of batch b of the group starting at step g
-    auto vrs = [&](int g, int b) {
-        return rsrc_at(vbc0 + (long)(2 * c0 + g + kSorB * b + 1) * P16);
-    };
-    auto grs = [&](int g) { return rsrc_at(gin + (long)(g + 2) * 16); };
+    // running bases, advanced per batch / group (no 64-bit multiply per
+    // batch): vrow = skewed row of the next batch's first step (column c0),
+    // prow = the granule row lane 62 publishes at that step, grow = the ghost
+    // granule row of the current group's first step + 2
+    const char *vrow = vbc0 + (long)(2 * c0 + s0 + 1) * P16;
+    const char *prow = gout + (long)(s0 - 123) * 16;
+    const char *grow = gin + (long)(s0 + 2) * 16;
+    const long vstep = (long)kSorB * P16;
 
     // window rows r..r+3 of the first step, batches of the first group
     v4u W0, W1, W2, W3, X[kSorNB][kSorB], GV[kSorNB];
     {
-        const auto rs = vrs(s0, 0);
+        const auto rs = rsrc_at(vrow);
         W0 = __builtin_amdgcn_raw_buffer_load_b128(rs, voff_ld, 0, 0);
         W1 = __builtin_amdgcn_raw_buffer_load_b128(rs, voff_ld, (int)P16, 0);
         W2 = __builtin_amdgcn_raw_buffer_load_b128(rs, voff_ld, 2 * (int)P16, 0);
@@ -307,7 +310,7 @@ __global__ __launch_bounds__(64) void sor_strip_kernel(float4 *__restrict__ vb, 
             for (int j = 0; j < kSorB; j++)
                 X[b][j] = __builtin_amdgcn_raw_buffer_load_b128(rs, voff_ld,
                                                                 (4 + kSorB * b + j) * (int)P16, 0);
-        const auto gr = grs(s0);
+        const auto gr = rsrc_at(grow);
 #pragma unroll
         for (int b = 0; b < kSorGLead; b++)
             GV[b] = __builtin_amdgcn_raw_buffer_load_b128(gr, voff_gin, kSorB * b * 16, 16);
@@ -355,23 +358,24 @@ __global__ __launch_bounds__(64) void sor_strip_kernel(float4 *__restrict__ vb, 
     };
 
     auto group = [&](auto chk, int g) {
+        const auto gr = rsrc_at(grow);
 #pragma unroll
         for (int b = 0; b < kSorNB; b++) {
             const int sb = g + kSorB * b;
             // ghost rows sb+2 .. sb+9: check the tags, start the lead batch's load
             v4u gv = GV[b];
             if (!granules_ready(gv, sb + 2, dimy, epoch)) {
-                gv = granule_poll(grs(g), voff_gin, kSorB * b * 16, sb + 2, dimy, epoch, status);
+                gv = granule_poll(gr, voff_gin, kSorB * b * 16, sb + 2, dimy, epoch, status);
                 npoll++;
             }
             G = lo2(gv);
             {
                 const int bl = b + kSorGLead;  // batch index counted from this group
-                GV[bl % kSorNB] = __builtin_amdgcn_raw_buffer_load_b128(grs(g), voff_gin,
+                GV[bl % kSorNB] = __builtin_amdgcn_raw_buffer_load_b128(gr, voff_gin,
                                                                         kSorB * bl * 16, 16);
             }
-            const auto rs = vrs(g, b);
-            const auto ps = rsrc_at(gout + (long)(sb - 123) * 16);
+            const auto rs = rsrc_at(vrow);
+            const auto ps = rsrc_at(prow);
 #pragma unroll
             for (int j = 0; j < kSorB; j++) step(chk, sb + j, j, rs, ps, X[b][j]);
             // batch b of the next group: rows 32 further down
@@ -379,7 +383,10 @@ __global__ __launch_bounds__(64) void sor_strip_kernel(float4 *__restrict__ vb, 
             for (int j = 0; j < kSorB; j++)
                 X[b][j] = __builtin_amdgcn_raw_buffer_load_b128(
                     rs, voff_ld, (4 + kSorG + j) * (int)P16, OF2D_SOR_LD_AUX);
+            vrow += vstep;
+            prow += kSorB * 16;
         }
+        grow += kSorG * 16;
     };
 
     for (int g = s0; g <= s1; g += kSorG) {
