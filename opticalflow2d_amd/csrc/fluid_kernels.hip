@@ -167,11 +167,14 @@ __device__ __forceinline__ float wide_min(float m) {
 //     stores of lanes that own no interior column are dropped by the buffer
 //     range check (voffset past num_records), not masked.
 // Loads run one group (kSorNB batches of 8 rows) ahead; granules (lane k of a
-// vector = ghost row q + k, {x, y, epoch, epoch}: the 16-B store is one
-// transaction and the epoch in both upper words tags it; x, y in the lower
-// half are an even register pair a packed result lands in without copies)
-// two batches ahead, are tag-checked once per batch and rotated one lane per
-// step by DPP.  Groups whose rows are interior for every lane skip the
+// vector = ghost row q + k, {x, y, epoch, epoch}) two batches ahead, are
+// tag-checked once per batch and rotated one lane per step by DPP.  A granule
+// is written by ONE 16-B-aligned dwordx4 sc1 store from one lane and read by
+// one 16-B-aligned dwordx4 sc1 load: a single request on both sides, inside
+// one 64-B memory sector, so the tag in the upper half vouches for x, y in
+// the lower half (the 8-B form, a tag in each half, costs two register moves
+// per step: x, y leave the packed result's even register pair; 3.5-5 % per
+// sweep, profiles/r02_ab_sor_halftag.log).  Groups whose rows are interior for every lane skip the
 // boundary-row select.
 namespace {
 constexpr int kSorCols = 63;  // real columns per strip (lanes 0..62)
