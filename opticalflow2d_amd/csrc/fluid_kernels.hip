@@ -440,18 +440,47 @@ void launch_sor(float4 *vb, int dimx, int dimy, int P, float mu, float lambda, f
 // 16 lanes on distinct banks.  Block dim3(64, 4).
 constexpr int kSkI = 64, kSkJ = 32;
 static_assert(kSkJ == kFieldRows && kSkI == 64, "field kernels tile 64 x kFieldRows");
+constexpr int kSkIts = 10;  // skewed runs per thread
+// pixel (ii, jj) of the thread's run `it`, and whether it is one of the tile's
+// pixels inside the image
+__device__ __forceinline__ bool skew_slot(int it, int i0, int j0, int dimx, int dimy, int &ii,
+                                          int &jj) {
+    const int q = threadIdx.x >> 4, k = threadIdx.x & 15;
+    const int s = 16 * it + 4 * (int)threadIdx.y + q;  // < 2 * 63 + 31 + 1 = 158
+    ii = max(0, (s - 30) >> 1) + k;                    // ceil((s - 31) / 2) + k
+    jj = s - 2 * ii;
+    return s < 2 * (kSkI - 1) + kSkJ && ii < kSkI && jj >= 0 && jj < kSkJ && i0 + ii < dimx &&
+           j0 + jj < dimy;
+}
 template <class F>
 __device__ __forceinline__ void skew_tile_for_each(int i0, int j0, int dimx, int dimy, F f) {
-    const int q = threadIdx.x >> 4, k = threadIdx.x & 15;
 #pragma unroll
-    for (int it = 0; it < 10; it++) {
-        const int s = 16 * it + 4 * (int)threadIdx.y + q;  // < 2 * 63 + 31 + 1 = 158
-        const int ii = max(0, (s - 30) >> 1) + k;         // ceil((s - 31) / 2) + k
-        const int jj = s - 2 * ii;
-        if (s < 2 * (kSkI - 1) + kSkJ && ii < kSkI && jj >= 0 && jj < kSkJ && i0 + ii < dimx &&
-            j0 + jj < dimy)
-            f(ii, jj);
+    for (int it = 0; it < kSkIts; it++) {
+        int ii, jj;
+        if (skew_slot(it, i0, j0, dimx, dimy, ii, jj)) f(ii, jj);
     }
+}
+// vb.zw <- f(ii, jj) over the tile's skewed runs, keeping vb.xy: every granule
+// of the thread is loaded before the first is written back (a read-modify-
+// write per run would wait for each load in turn: the compiler cannot prove
+// the runs' addresses distinct)
+template <class F>
+__device__ __forceinline__ void skew_tile_set_zw(float4 *__restrict__ vb, int i0, int j0, int dimx,
+                                                 int dimy, int P, F f) {
+    float4 o[kSkIts];
+    int ii[kSkIts], jj[kSkIts];
+    bool ok[kSkIts];
+#pragma unroll
+    for (int it = 0; it < kSkIts; it++) {
+        ok[it] = skew_slot(it, i0, j0, dimx, dimy, ii[it], jj[it]);
+        o[it] = vb[ok[it] ? sor_index(i0 + ii[it], j0 + jj[it], P) : 0];
+    }
+#pragma unroll
+    for (int it = 0; it < kSkIts; it++)
+        if (ok[it]) {
+            const float2 z = f(ii[it], jj[it]);
+            vb[sor_index(i0 + ii[it], j0 + jj[it], P)] = make_float4(o[it].x, o[it].y, z.x, z.y);
+        }
 }
 
 // vb.zw <- force(u, dI, It) (OpticalFlow.cpp:15-39); with pack_v also vb.xy <- v.
@@ -481,16 +510,16 @@ __global__ __launch_bounds__(256) void sor_pack_kernel(float4 *__restrict__ vb,
         }
     }
     __syncthreads();
-    skew_tile_for_each(i0, j0, dimx, dimy, [&](int ii, int jj) {
-        const float4 q = tile[jj][ii];
-        float4 *dst = vb + sor_index(i0 + ii, j0 + jj, P);
-        if (v) {
-            *dst = q;
-        } else {  // whole 16-B granules (a masked 8-B store per granule measured slower)
-            const float4 o = *dst;
-            *dst = make_float4(o.x, o.y, q.z, q.w);
-        }
-    });
+    if (v) {
+        skew_tile_for_each(i0, j0, dimx, dimy, [&](int ii, int jj) {
+            vb[sor_index(i0 + ii, j0 + jj, P)] = tile[jj][ii];
+        });
+    } else {  // whole 16-B granules (a masked 8-B store per granule measured slower)
+        skew_tile_set_zw(vb, i0, j0, dimx, dimy, P, [&](int ii, int jj) {
+            const float4 q = tile[jj][ii];
+            return make_float2(q.z, q.w);
+        });
+    }
 }
 void launch_sor_pack(float4 *vb, const float2 *u, const float2 *dI, const float *It,
                      const float2 *v, int dimx, int dimy, int P, void *H, unsigned epoch,
@@ -616,33 +645,58 @@ __global__ __launch_bounds__(256) void fluid_step_kernel(
     const float dt = scal[1];
     const bool integ = dt < 65.0f;  // OpticalFlowFluid.cpp:135-137
     const int tid = threadIdx.y * 64 + threadIdx.x;
-    // 1. new u over the tile and its one-pixel cross halo (corners unused)
-    for (int s = tid; s < TW * TH; s += 256) {
-        const int r = s / TW, c = s - r * TW;
+    // 1. new u over the tile and its one-pixel cross halo (corners unused);
+    // every load of the thread is issued before the first is used (slots
+    // outside the image read element 0 and are not stored)
+    constexpr int NS = (TW * TH + 255) / 256;
+    float2 mu[NS], mr[NS];
+    bool okq[NS];
+#pragma unroll
+    for (int q = 0; q < NS; q++) {
+        const int s = tid + 256 * q, r = s / TW, c = s - r * TW;
         const int i = i0 - 1 + c, j = j0 - 1 + r;
         const bool corner = (r == 0 || r == TH - 1) && (c == 0 || c == TW - 1);
-        if (corner || (unsigned)i >= (unsigned)dimx || (unsigned)j >= (unsigned)dimy) continue;
-        const long idx = (long)j * P + i;
-        float2 m = u[idx];
-        if (integ) {
-            const float2 q = R[idx];
-            m = make_float2(m.x + q.x * dt, m.y + q.y * dt);
-        }
-        un[r][c] = m;
+        okq[q] = s < TW * TH && !corner && (unsigned)i < (unsigned)dimx &&
+                 (unsigned)j < (unsigned)dimy;
+        const unsigned idx = okq[q] ? (unsigned)(j * P + i) : 0u;
+        mu[q] = u[idx];
+        mr[q] = R[idx];
+    }
+#pragma unroll
+    for (int q = 0; q < NS; q++) {
+        const int s = tid + 256 * q, r = s / TW, c = s - r * TW;
+        float2 m = mu[q];
+        if (integ) m = make_float2(m.x + mr[q].x * dt, m.y + mr[q].y * dt);
+        if (okq[q]) un[r][c] = m;
+    }
+    // 2. per pixel; thread (x, y) sums the Logger terms of rows y, y + 4, ...
+    // in order; its loads first
+    constexpr int NK = kSkJ / 4;
+    const int i = i0 + threadIdx.x;
+    float2 pvk[NK], gk[NK];
+    float itk[NK];
+    bool okk[NK];
+#pragma unroll
+    for (int k = 0; k < NK; k++) {
+        const int j = j0 + 4 * k + threadIdx.y;
+        okk[k] = i < dimx && j < dimy;
+        const unsigned idx = okk[k] ? (unsigned)(j * P + i) : 0u;
+        pvk[k] = kPrev ? prev[idx] : u[idx];
+        gk[k] = dI[idx];
+        itk[k] = It[idx];
     }
     __syncthreads();
-    // 2. per pixel; thread (x, y) sums the Logger terms of rows y, y + 4, ... in order
-    const int i = i0 + threadIdx.x;
     double sd = 0.0, sp = 0.0;
     float jm = __builtin_inff();
-    for (int k = 0; k < kSkJ / 4; k++) {
+#pragma unroll
+    for (int k = 0; k < NK; k++) {
+        if (!okk[k]) continue;
         const int rr = 4 * k + threadIdx.y;
         const int j = j0 + rr;
-        if (i >= dimx || j >= dimy) break;
         const long idx = (long)j * P + i;
         const int r = rr + 1, c = threadIdx.x + 1;
         const float2 m = un[r][c];
-        const float2 pv = kPrev ? prev[idx] : u[idx];
+        const float2 pv = pvk[k];
         uo[idx] = m;
         const float ex = m.x - pv.x, ey = m.y - pv.y;
         sd += (double)__builtin_sqrtf(ex * ex + ey * ey);
@@ -672,8 +726,8 @@ __global__ __launch_bounds__(256) void fluid_step_kernel(
         const float q = (1.0f + dx.x) * (1.0f + dy.y) - dx.y * dy.x;  // Image.cpp:189-218
         jm = (q < jm) ? q : jm;
         // OpticalFlow::get_force (OpticalFlow.cpp:15-39) of the new u
-        const float2 g = dI[idx];
-        const float sc = (It[idx] + m.x * g.x) + m.y * g.y;
+        const float2 g = gk[k];
+        const float sc = (itk[k] + m.x * g.x) + m.y * g.y;
         fo[rr][threadIdx.x] = make_float2(g.x * sc, g.y * sc);
         if (i == 0 && H) {  // ghost column of strip 0 for the next sweep
             const float2 x = reinterpret_cast<const float2 *>(vb + sor_index(0, j, P))[0];
@@ -684,12 +738,7 @@ __global__ __launch_bounds__(256) void fluid_step_kernel(
     jm = block_min(jm);
     if (threadIdx.x == 0 && threadIdx.y == 0) jpart[(long)blockIdx.y * gridDim.x + blockIdx.x] = jm;
     // 3. vb.zw <- force along the skewed rows (whole 16-B granules, as sor_pack)
-    skew_tile_for_each(i0, j0, dimx, dimy, [&](int ii, int jj) {
-        const float2 f = fo[jj][ii];
-        float4 *dst = vb + sor_index(i0 + ii, j0 + jj, P);
-        const float4 o = *dst;
-        *dst = make_float4(o.x, o.y, f.x, f.y);
-    });
+    skew_tile_set_zw(vb, i0, j0, dimx, dimy, P, [&](int ii, int jj) { return fo[jj][ii]; });
 }
 
 void launch_fluid_step(const float2 *u, const float2 *R, float2 *uo, const float2 *prev,
