@@ -189,12 +189,8 @@ void launch_upsample_motion(const float2 *in, int dxi, int dyi, int Pi, float2 *
 // pattern reads element 0; g[1], g[P], g[P+1] of an in-image pixel stay in the
 // allocation: pitch padding and the zeroed ghost j-line below the last row)
 // and the reference's conditional terms are selects.
-__global__ void warp_kernel(const float *__restrict__ src, const float2 *__restrict__ u,
-                            float *__restrict__ dst, int dimx, int dimy, int P) {
-    OF2D_PX_PROLOGUE(dimx, dimy)
-    const long idx = (long)j * P + i;
-    const float2 m = u[idx];
-    const float own = src[idx];
+__device__ __forceinline__ float warp_px(const float *__restrict__ src, float2 m, float own, int i,
+                                         int j, int dimx, int dimy, int P) {
     const float px = (float)i + m.x;
     const int dx = (int)floorf(px);
     const float fx = px - (float)dx;
@@ -217,7 +213,13 @@ __global__ void warp_kernel(const float *__restrict__ src, const float2 *__restr
     val = (ax && ay) ? v11 : val;
     w = (ax && ay) ? w11 : w;
     const float q = val / w;
-    dst[idx] = (ok && w != 0) ? q : own;
+    return (ok && w != 0) ? q : own;
+}
+__global__ void warp_kernel(const float *__restrict__ src, const float2 *__restrict__ u,
+                            float *__restrict__ dst, int dimx, int dimy, int P) {
+    OF2D_PX_PROLOGUE(dimx, dimy)
+    const long idx = (long)j * P + i;
+    dst[idx] = warp_px(src, u[idx], src[idx], i, j, dimx, dimy, P);
 }
 void launch_warp(const float *src, const float2 *u, float *dst, int dimx, int dimy, int P,
                  hipStream_t st) {
@@ -267,12 +269,9 @@ void launch_gradients(const float *Iref, const float *Iaux, float2 *dI, float *I
 // Motion::accumulate (src/Motion.cpp:113-178): u(x) <- v(x) + u_old(x + v(x))
 // (bilinear, renormalised); out-of-range keeps u_old(x).
 // Branch-free as warp_kernel.
-__global__ void accumulate_kernel(const float2 *__restrict__ mo, const float2 *__restrict__ v,
-                                  float2 *__restrict__ mn, int dimx, int dimy, int P) {
-    OF2D_PX_PROLOGUE(dimx, dimy)
-    const long idx = (long)j * P + i;
-    const float2 c = v[idx];
-    const float2 own = mo[idx];
+__device__ __forceinline__ float2 accumulate_px(const float2 *__restrict__ mo, float2 c,
+                                                float2 own, int i, int j, int dimx, int dimy,
+                                                int P) {
     const float px = (float)i + c.x;
     const int dx = (int)floorf(px);
     const float fx = px - (float)dx;
@@ -302,12 +301,41 @@ __global__ void accumulate_kernel(const float2 *__restrict__ mo, const float2 *_
     vy = axy ? y11 : vy;
     w = axy ? w11 : w;
     const float2 q = make_float2(c.x + vx / w, c.y + vy / w);
-    mn[idx] = ok ? (w != 0 ? q : c) : own;
+    return ok ? (w != 0 ? q : c) : own;
+}
+__global__ void accumulate_kernel(const float2 *__restrict__ mo, const float2 *__restrict__ v,
+                                  float2 *__restrict__ mn, int dimx, int dimy, int P) {
+    OF2D_PX_PROLOGUE(dimx, dimy)
+    const long idx = (long)j * P + i;
+    mn[idx] = accumulate_px(mo, v[idx], mo[idx], i, j, dimx, dimy, P);
 }
 void launch_accumulate(const float2 *m_old, const float2 *v, float2 *m_new, int dimx, int dimy,
                        int P, hipStream_t st) {
     hipLaunchKernelGGL(accumulate_kernel, grid2d(dimx, dimy), dim3(kBx, kBy), 0, st, m_old, v,
                        m_new, dimx, dimy, P);
+    OF2D_HIP(hipGetLastError());
+}
+
+// Fluid regridding (ImageRegistrationFluid.cpp:108-124) in one pass: the
+// motion accumulates the estimate (Motion::accumulate), the next estimate
+// starts at zero (a second buffer: the Logger keeps the old one), and the
+// moving image is warped by the new motion (Image::warp2d); per pixel the
+// operations of accumulate_kernel then warp_kernel.
+__global__ void regrid_kernel(const float2 *__restrict__ mo, const float2 *__restrict__ est,
+                              float2 *__restrict__ est0, float2 *__restrict__ mn,
+                              const float *__restrict__ Imov, float *__restrict__ Iaux, int dimx,
+                              int dimy, int P) {
+    OF2D_PX_PROLOGUE(dimx, dimy)
+    const long idx = (long)j * P + i;
+    const float2 m = accumulate_px(mo, est[idx], mo[idx], i, j, dimx, dimy, P);
+    mn[idx] = m;
+    est0[idx] = make_float2(0.0f, 0.0f);
+    Iaux[idx] = warp_px(Imov, m, Imov[idx], i, j, dimx, dimy, P);
+}
+void launch_regrid(const float2 *m_old, const float2 *est, float2 *est0, float2 *m_new,
+                   const float *Imov, float *Iaux, int dimx, int dimy, int P, hipStream_t st) {
+    hipLaunchKernelGGL(regrid_kernel, grid2d(dimx, dimy), dim3(kBx, kBy), 0, st, m_old, est, est0,
+                       m_new, Imov, Iaux, dimx, dimy, P);
     OF2D_HIP(hipGetLastError());
 }
 

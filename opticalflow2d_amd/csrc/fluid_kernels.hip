@@ -529,6 +529,69 @@ void launch_sor_pack(float4 *vb, const float2 *u, const float2 *dI, const float 
     OF2D_HIP(hipGetLastError());
 }
 
+// ------------------------------------------------------------ regrid pack
+// After a fluid regrid (ImageRegistrationFluid.cpp:118-123): set_derivatives
+// of the new warped image (IterativeSolver.cpp:22-56, gradients.h:9-32; the
+// same taps and operations as gradients_kernel) and the next sweep's force of
+// the zeroed estimate into vb.zw (get_force with u = +0, the operations of
+// sor_pack_kernel), in one pass over a 64 x 32 tile.
+__global__ __launch_bounds__(256) void regrid_pack_kernel(
+    const float *__restrict__ Iref, const float *__restrict__ Ia, float2 *__restrict__ dI,
+    float *__restrict__ It, float4 *__restrict__ vb, int dimx, int dimy, int P,
+    v4u *__restrict__ H, unsigned epoch) {
+    __shared__ float2 fo[kSkJ][kSkI];
+    const int i0 = blockIdx.x * kSkI, j0 = blockIdx.y * kSkJ;
+    const int i = i0 + threadIdx.x;
+    constexpr int NK = kSkJ / 4;
+    // taps of every row of the thread first (border rows and columns pick the
+    // one-sided taps; rows outside the image read element 0)
+    float ia[NK], ib[NK], ja[NK], jb[NK], io[NK], ir[NK];
+    bool okk[NK];
+    const bool xl = i == 0, xr = !xl && i == dimx - 1;
+#pragma unroll
+    for (int k = 0; k < NK; k++) {
+        const int j = j0 + 4 * k + threadIdx.y;
+        okk[k] = i < dimx && j < dimy;
+        const int idx = okk[k] ? j * P + i : 0;
+        const bool yl = j == 0, yr = !yl && j == dimy - 1;
+        ia[k] = Ia[okk[k] ? (xr ? idx : idx + 1) : 0];
+        ib[k] = Ia[okk[k] ? (xl ? idx : idx - 1) : 0];
+        ja[k] = Ia[okk[k] ? (yr ? idx : idx + P) : 0];
+        jb[k] = Ia[okk[k] ? (yl ? idx : idx - P) : 0];
+        io[k] = Ia[idx];
+        ir[k] = Iref[idx];
+    }
+#pragma unroll
+    for (int k = 0; k < NK; k++) {
+        if (!okk[k]) continue;
+        const int rr = 4 * k + threadIdx.y;
+        const int j = j0 + rr;
+        const long idx = (long)j * P + i;
+        const bool yl = j == 0, yr = !yl && j == dimy - 1;
+        const float gx = (xl || xr) ? ia[k] - ib[k] : (ia[k] - ib[k]) / 2.0f;
+        const float gy = (yl || yr) ? ja[k] - jb[k] : (ja[k] - jb[k]) / 2.0f;
+        const float t = io[k] - ir[k];
+        dI[idx] = make_float2(gx, gy);
+        It[idx] = t;
+        const float z = 0.0f;  // the estimate after the regrid
+        const float sc = (t + z * gx) + z * gy;
+        fo[rr][threadIdx.x] = make_float2(gx * sc, gy * sc);
+        if (i == 0 && H) {
+            const float2 x = reinterpret_cast<const float2 *>(vb + sor_index(0, j, P))[0];
+            H[kSorPadRows + j] = v4u{__float_as_uint(x.x), __float_as_uint(x.y), epoch, epoch};
+        }
+    }
+    __syncthreads();
+    skew_tile_set_zw(vb, i0, j0, dimx, dimy, P, [&](int ii, int jj) { return fo[jj][ii]; });
+}
+void launch_regrid_pack(const float *Iref, const float *Iaux, float2 *dI, float *It, float4 *vb,
+                        int dimx, int dimy, int P, void *H, unsigned epoch, hipStream_t st) {
+    hipLaunchKernelGGL(regrid_pack_kernel,
+                       dim3((dimx + kSkI - 1) / kSkI, (dimy + kSkJ - 1) / kSkJ), dim3(64, 4), 0,
+                       st, Iref, Iaux, dI, It, vb, dimx, dimy, P, (v4u *)H, epoch);
+    OF2D_HIP(hipGetLastError());
+}
+
 // ------------------------------------------------------------ pointwise force
 // OpticalFlow::get_force (OpticalFlow.cpp:15-39): f = dI * ((It + u.x dI.x) + u.y dI.y)
 __global__ void force_kernel(const float2 *__restrict__ u, const float2 *__restrict__ dI,

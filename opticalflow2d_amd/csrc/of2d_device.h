@@ -218,6 +218,10 @@ void launch_gradients_rows(const float *Iref, const float *Iaux, float2 *dI, flo
                            int nrows, int P, int row0, int dimy, hipStream_t st);
 void launch_accumulate(const float2 *m_old, const float2 *v, float2 *m_new, int dimx, int dimy,
                        int P, hipStream_t st);
+// Fluid regridding: m_new <- accumulate(m_old, est), est0 <- 0 over the image
+// pixels (ghost lines and pitch padding are never written), Iaux <- warp(Imov, m_new)
+void launch_regrid(const float2 *m_old, const float2 *est, float2 *est0, float2 *m_new,
+                   const float *Imov, float *Iaux, int dimx, int dimy, int P, hipStream_t st);
 void launch_compose_zero(const float2 *v, float2 *out, int dimx, int nrows, int P, int row0,
                          int dimy, hipStream_t st);
 void launch_add_motion(const float2 *a, const float2 *b, float2 *out, int dimx, int dimy, int P,
@@ -295,6 +299,10 @@ void launch_sor(float4 *vb, int dimx, int dimy, int P, float mu, float lambda, f
 void launch_sor_pack(float4 *vb, const float2 *u, const float2 *dI, const float *It,
                      const float2 *v, int dimx, int dimy, int P, void *H, unsigned epoch,
                      hipStream_t st);
+// after a regrid: dI, It <- gradients of Iaux (set_derivatives) and vb.zw <-
+// force of a zero estimate, granule region 0 <- column 0 of vb.xy tagged epoch
+void launch_regrid_pack(const float *Iref, const float *Iaux, float2 *dI, float *It, float4 *vb,
+                        int dimx, int dimy, int P, void *H, unsigned epoch, hipStream_t st);
 void launch_force(const float2 *u, const float2 *dI, const float *It, float2 *f, int dimx,
                   int dimy, int P, hipStream_t st);
 int increment_nblocks(int dimx, int dimy);

@@ -165,16 +165,20 @@ int Registration::loop_fluid(Level &L, int niter) {
     // not the iteration's input estimate (first iteration, after a regrid);
     // packed: vb.zw already holds the force of the estimate, tagged with the
     // next epoch (fluid_step of the previous iteration).
-    bool prev_separate = true, packed = false;
+    bool prev_separate = true, packed = false, regridded = false;
     last_err_.clear();
     int iter;
     for (iter = 0; iter < niter; iter++) {
         float2 *est = L.est[0].p;
         // get_force(force, motion) into vb.zw, then the SOR sweep of the velocity vb.xy
         const unsigned ep = ++epoch_;
-        if (!packed)
+        if (!packed && regridded)  // gradients of the new warped image + force of est = 0
+            launch_regrid_pack(L.Iref.p, L.Iaux.p, L.dI.p, L.It.p, L.vb.p, L.dx, L.dy, L.P,
+                               L.sorH.p, ep, st_);
+        else if (!packed)
             launch_sor_pack(L.vb.p, est, L.dI.p, L.It.p, nullptr, L.dx, L.dy, L.P, L.sorH.p, ep,
                             st_);
+        regridded = false;
         launch_sor(L.vb.p, L.dx, L.dy, L.P, mu, lambda, omega, L.sorH.p, ep, L.sorTicket.p,
                    d_status_, st_);
         launch_increment(est, L.vb.p, L.increment.p, L.dx, L.dy, L.P, L.part.p, scal, st_);
@@ -201,17 +205,19 @@ int Registration::loop_fluid(Level &L, int niter) {
         }
         if (jmin < 0.5) {  // regridding (ImageRegistrationFluid.cpp:108-124)
             print("Regridding on iteration: %d\tMin Jacobian: %.3f\n", iter, (double)jmin);
-            // the Logger keeps this iteration's motion; the estimate restarts at zero
-            OF2D_HIP(hipMemcpyAsync(L.tmp.base, L.est[0].base, L.tmp.bytes(),
-                                    hipMemcpyDeviceToDevice, st_));
+            // the Logger keeps this iteration's motion (the buffers trade places:
+            // L.tmp takes the estimate, the old Logger buffer becomes the
+            // estimate, zeroed by the regrid pass); motion accumulates the
+            // estimate, the moving image is warped by it, and the next
+            // iteration starts with its gradients and force (launch_regrid_pack)
+            std::swap(L.tmp, L.est[0]);
+            prev = L.tmp.p;
             prev_separate = true;
-            launch_accumulate(L.motion[L.mcur].p, L.est[0].p, L.motion[1 - L.mcur].p, L.dx, L.dy,
-                              L.P, st_);
+            launch_regrid(L.motion[L.mcur].p, L.tmp.p, L.est[0].p, L.motion[1 - L.mcur].p,
+                          L.Imov.p, L.Iaux.p, L.dx, L.dy, L.P, st_);
             L.mcur ^= 1;
-            L.est[0].zero(st_);
-            launch_warp(L.Imov.p, L.cur_motion(), L.Iaux.p, L.dx, L.dy, L.P, st_);
-            launch_gradients(L.Iref.p, L.Iaux.p, L.dI.p, L.It.p, L.dx, L.dy, L.P, st_);
             packed = false;  // the packed force was of the old estimate and gradients
+            regridded = true;
         }
     }
     return iter;
