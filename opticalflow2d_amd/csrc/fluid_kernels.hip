@@ -179,15 +179,22 @@ __device__ __forceinline__ float wide_min(float m) {
 namespace {
 constexpr int kSorCols = 63;  // real columns per strip (lanes 0..62)
 constexpr int kSorB = 8;      // rows per batch
-// batches per group: the row loads run one group (kSorNB * 8 rows) ahead.  40
-// rows: 1.4-3.4 % per sweep faster than 32 at 2048^2-8192^2 (the loads wait on
-// HBM at 32); 48 spill into AGPR moves (profiles/r02_x_sor_lead_ab.log)
+// batches per group: the row loads run one group (kSorNB * 8 rows) ahead.
+// 40 rows: 1.4-3.4 % per sweep faster than 32 at 2048^2-8192^2 (the loads
+// wait on HBM at 32); 48 rows spilled into AGPR moves with one group per loop
+// trip (profiles/r02_x_sor_lead_ab.log), and are 0.3-1.2 % faster than 40 with
+// the unrolled interior loop (profiles/r02_ag_sor_lead_unrolled_ab.log)
 #ifdef OF2D_SOR_NB  // tools/sor_harness.hip A/B builds
 constexpr int kSorNB = OF2D_SOR_NB;
 #else
-constexpr int kSorNB = 5;
+constexpr int kSorNB = 6;
 #endif
 constexpr int kSorG = kSorB * kSorNB;
+#ifdef OF2D_SOR_UNROLL  // tools/sor_harness.hip A/B builds
+constexpr int kSorUnroll = OF2D_SOR_UNROLL;
+#else
+constexpr int kSorUnroll = 3;  // interior groups per loop trip (2: -3 %, 3: -4 %, 4: -4 % per sweep)
+#endif
 #ifdef OF2D_SOR_GLEAD  // tools/sor_harness.hip A/B builds only
 constexpr int kSorGLead = OF2D_SOR_GLEAD;
 #else
@@ -392,12 +399,22 @@ __global__ __launch_bounds__(64) void sor_strip_kernel(float4 *__restrict__ vb, 
         grow += kSorG * 16;
     };
 
-    for (int g = s0; g <= s1; g += kSorG) {
-        if (g >= 124 && g + kSorG - 1 <= dimy - 3)
-            group(Flag<false>{}, g);
-        else
-            group(Flag<true>{}, g);
+    // three loops: head groups with the boundary-row select, interior groups
+    // without it, tail groups with it.  The interior loop runs kSorUnroll
+    // groups per trip: its back edge copies ~32 row registers (the allocator
+    // does not keep the row ring in place across a trip) and waits on their
+    // loads, so fewer trips cost less (one group per trip, both kinds of
+    // group in one loop: 186 cycles per step of strip 0 at 8192^2; three
+    // loops, 3 groups per trip: 164; profiles/r02_af_sor_loops_ab.log)
+    int g = s0;
+    for (; g <= s1 && g < 124; g += kSorG) group(Flag<true>{}, g);
+    for (; g + (kSorUnroll - 1) * kSorG <= s1 && g + kSorUnroll * kSorG - 1 <= dimy - 3;
+         g += kSorUnroll * kSorG) {
+#pragma unroll
+        for (int q = 0; q < kSorUnroll; q++) group(Flag<false>{}, g + q * kSorG);
     }
+    for (; g <= s1 && g + kSorG - 1 <= dimy - 3; g += kSorG) group(Flag<false>{}, g);
+    for (; g <= s1; g += kSorG) group(Flag<true>{}, g);
     if (trace && lane == 0) {
         trace[4 * I] = t_start;
         trace[4 * I + 1] = __builtin_amdgcn_s_memrealtime();
