@@ -200,6 +200,16 @@ constexpr int kSorGLead = OF2D_SOR_GLEAD;
 #else
 constexpr int kSorGLead = 2;  // granule vectors are loaded this many batches ahead
 #endif
+#ifdef OF2D_SOR_GISSUE  // tools/sor_harness.hip A/B builds only
+constexpr int kSorGIssue = OF2D_SOR_GISSUE;
+#else
+constexpr int kSorGIssue = 6;  // ... issued before this step of the batch: a 10-step lead
+// (0: 16 steps, 1.4 % slower per sweep; GLEAD 1 with 0: 8 steps, 35 % slower;
+// profiles/r02_ah_sor_granule_issue_ab.log)
+#endif
+#ifdef OF2D_SOR_HTRACE
+constexpr int kSorHtMax = 4096;  // batches recorded per strip
+#endif
 static_assert(kSorGLead >= 1 && kSorGLead <= kSorNB, "granule vectors rotate through GV[kSorNB]");
 // cache policy of the row loads / value stores (tools/sor_harness A/B builds
 // override them): the row loads are non-temporal (aux 2), 0.5-1 % per sweep
@@ -374,20 +384,33 @@ __global__ __launch_bounds__(64) void sor_strip_kernel(float4 *__restrict__ vb, 
             const int sb = g + kSorB * b;
             // ghost rows sb+2 .. sb+9: check the tags, start the lead batch's load
             v4u gv = GV[b];
+#ifdef OF2D_SOR_HTRACE  // tools/sor_harness.hip: per-batch hand-off timeline
+            unsigned long long polled = 0;
+#endif
             if (!granules_ready(gv, sb + 2, dimy, epoch)) {
                 gv = granule_poll(gr, voff_gin, kSorB * b * 16, sb + 2, dimy, epoch, status);
                 npoll++;
+#ifdef OF2D_SOR_HTRACE
+                polled = 1ull << 63;
+#endif
             }
             G = lo2(gv);
-            {
-                const int bl = b + kSorGLead;  // batch index counted from this group
-                GV[bl % kSorNB] = __builtin_amdgcn_raw_buffer_load_b128(gr, voff_gin,
-                                                                        kSorB * bl * 16, 16);
-            }
+#ifdef OF2D_SOR_HTRACE
+            if (lane == 0)
+                trace[4 * nstrips + (long)I * kSorHtMax + (sb - s0) / kSorB] =
+                    __builtin_amdgcn_s_memrealtime() | polled;
+#endif
             const auto rs = rsrc_at(vrow);
             const auto ps = rsrc_at(prow);
 #pragma unroll
-            for (int j = 0; j < kSorB; j++) step(chk, sb + j, j, rs, ps, X[b][j]);
+            for (int j = 0; j < kSorB; j++) {
+                if (j == kSorGIssue) {  // the lead batch's granules
+                    const int bl = b + kSorGLead;  // batch index counted from this group
+                    GV[bl % kSorNB] = __builtin_amdgcn_raw_buffer_load_b128(gr, voff_gin,
+                                                                            kSorB * bl * 16, 16);
+                }
+                step(chk, sb + j, j, rs, ps, X[b][j]);
+            }
             // batch b of the next group: rows 32 further down
 #pragma unroll
             for (int j = 0; j < kSorB; j++)

@@ -9,6 +9,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <algorithm>
 #include <vector>
 
 using namespace of2d;
@@ -37,7 +38,12 @@ int main(int argc, char **argv) {
     OF2D_HIP(hipMalloc(&status, 4));
     OF2D_HIP(hipMemset(ticket, 0, 4));
     OF2D_HIP(hipMemset(status, 0, 4));
-    OF2D_HIP(hipMalloc(&trace, 32 * (size_t)ns));
+#ifdef OF2D_SOR_HTRACE
+    const size_t ntr = 4 * (size_t)ns + (size_t)ns * kSorHtMax;
+#else
+    const size_t ntr = 4 * (size_t)ns;
+#endif
+    OF2D_HIP(hipMalloc(&trace, 8 * ntr));
     // zero motion / gradients / It for the pack (b = 0; the pack only tags
     // granule region 0 and rewrites vb.zw)
     float2 *zf;
@@ -47,7 +53,7 @@ int main(int argc, char **argv) {
     hipEvent_t e0, e1;
     hipEventCreate(&e0);
     hipEventCreate(&e1);
-    std::vector<unsigned long long> tr(4 * (size_t)ns);
+    std::vector<unsigned long long> tr(ntr);
     for (int r = 0; r < reps; r++) {
         const unsigned epoch = r + 1;
         // column-0 granules for strip 0 (what sor_pack writes)
@@ -78,6 +84,56 @@ int main(int argc, char **argv) {
         // strip 0 never waits for a neighbour: its cycles per step and clock
         printf("  strip 0: %.1f cycles/step, clock %.3f GHz\n", tr[3] / steps,
                tr[3] / ((tr[1] - tr[0]) * 10.0));
+#ifdef OF2D_SOR_HTRACE
+        // hand-off slack: strip I's batch b (ghost rows up to sb + 9) checked
+        // ready at T_c(I, b); its producer I-1 publishes row sb + 9 at step
+        // sb + 132, i.e. in its batch b + 16 (4.5 steps in)
+        if (r == reps - 1 && ns > 12) {
+            const int nb = (dimy + 125 + 3) / kSorB + 1;
+            auto T = [&](int I, int b) { return tr[4 * ns + (size_t)I * kSorHtMax + b]; };
+            std::vector<double> slack, period, lagv;
+            long np = 0, nt = 0;
+            for (int I = 5; I < ns - 5; I++)
+                for (int b = 24; b + 40 < nb; b++) {
+                    const unsigned long long c = T(I, b), pr = T(I - 1, b + 16);
+                    const unsigned long long m = ~(1ull << 63);
+                    slack.push_back(((long long)(c & m) - (long long)(pr & m)) * 0.01);
+                    period.push_back(((long long)(T(I, b + 1) & m) - (long long)(c & m)) * 0.01);
+                    lagv.push_back(((long long)(c & m) - (long long)(T(I - 1, b) & m)) * 0.01);
+                    np += (c >> 63) & 1;
+                    nt++;
+                }
+            auto pct = [](std::vector<double> v, double q) {
+                std::sort(v.begin(), v.end());
+                return v.empty() ? 0.0 : v[(size_t)(q * (v.size() - 1))];
+            };
+            printf("  handoff: slack us p10 %.2f p50 %.2f p90 %.2f | batch period us p50 %.3f p90 %.3f |"
+                   " strip lag us p50 %.2f | polled %.1f %%\n",
+                   pct(slack, 0.1), pct(slack, 0.5), pct(slack, 0.9), pct(period, 0.5),
+                   pct(period, 0.9), pct(lagv, 0.5), 100.0 * np / std::max(1l, nt));
+            // slack early and late in the sweep, and where the strips poll
+            std::vector<double> e, l;
+            long pe = 0, pl = 0, pm = 0;
+            for (int I = 5; I < ns - 5; I++) {
+                const unsigned long long m = ~(1ull << 63);
+                e.push_back(((long long)(T(I, 24) & m) - (long long)(T(I - 1, 40) & m)) * 0.01);
+                l.push_back(((long long)(T(I, nb - 60) & m) - (long long)(T(I - 1, nb - 44) & m)) * 0.01);
+                for (int b = 0; b < nb; b++)
+                    if (T(I, b) >> 63) (b < 24 ? pe : (b + 60 < nb ? pm : pl))++;
+            }
+            printf("  slack us: batch 24 p50 %.2f, batch nb-60 p50 %.2f | polls per strip: first 24 batches %.1f,"
+                   " middle %.1f, last 60 %.1f\n",
+                   pct(e, 0.5), pct(l, 0.5), (double)pe / (ns - 10), (double)pm / (ns - 10),
+                   (double)pl / (ns - 10));
+            // one strip's batch periods around its polls
+            const int I = ns / 2;
+            printf("  strip %d periods (us, * = polled):", I);
+            for (int b = 100; b < 160; b++)
+                printf(" %.2f%s", ((T(I, b + 1) & ~(1ull << 63)) - (T(I, b) & ~(1ull << 63))) * 0.01,
+                       (T(I, b) >> 63) ? "*" : "");
+            printf("\n");
+        }
+#endif
         if (r == reps - 1 && ns > 1) {
             printf("  strip: start_us end_us polls\n");
             for (int i = 0; i < ns; i += std::max(1, ns / 12))
