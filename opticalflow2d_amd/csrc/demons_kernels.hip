@@ -27,6 +27,8 @@
 // exactly like the scalar multiply and add).
 #include "of2d_device.h"
 
+#include <cmath>
+
 namespace of2d {
 
 namespace {
@@ -101,9 +103,15 @@ __device__ __forceinline__ void warp_batch(const float *__restrict__ Imov,
 }
 
 // Demons.cpp:57: dI * It / (dI.x^2 + dI.y^2 + It*It*sigma_isq/sigma_xsq) * -1
+// SXP: sigma_xsq is a power of two 2^k (|k| <= 126; the default sigma_x = 0.25
+// gives 2^-4) and `sxq` holds its reciprocal 2^-k: t * 2^-k and t / 2^k are the
+// same exact value, correctly rounded by both (denormals preserved), so the
+// multiply gives the division's bits.  Otherwise `sxq` is sigma_xsq.
+template <bool SXP = false>
 __device__ __forceinline__ float2 demons_corr(float gx, float gy, float it, float sigma_isq,
-                                              float sigma_xsq, bool &zero) {
-    const float den = (gx * gx + gy * gy) + ((it * it) * sigma_isq) / sigma_xsq;
+                                              float sxq, bool &zero) {
+    const float t = (it * it) * sigma_isq;
+    const float den = (gx * gx + gy * gy) + (SXP ? t * sxq : t / sxq);
     zero |= den == 0.0f;
     return make_float2(((gx * it) / den) * -1.0f, ((gy * it) / den) * -1.0f);
 }
@@ -113,6 +121,15 @@ __device__ __forceinline__ float2 demons_corr(float gx, float gy, float it, floa
 __device__ __forceinline__ int tile_x(int ntl, int gxt) {
     const int b = (int)blockIdx.x;
     return b < ntl ? b : gxt - ((int)gridDim.x - b);
+}
+
+// d = 2^k with |k| <= 126: *r = 2^-k (exact, normal) and true
+bool pow2_reciprocal(float d, float *r) {
+    int e = 0;
+    const float m = std::frexp(d, &e);  // d = m 2^e, m in [0.5, 1)
+    if (m != 0.5f || e - 1 < -126 || e - 1 > 126) return false;
+    *r = std::ldexp(1.0f, 1 - e);
+    return true;
 }
 }  // namespace
 
@@ -301,7 +318,9 @@ __device__ __forceinline__ bool conv_px(const float2 *tile, const ConvArgs &a, i
 // each tap column are read once and shared by the R outputs (each output
 // still sums ii outer / jj inner, the reference's order), x and y as one
 // packed pair (PK) or as two scalars; otherwise per pixel.
-template <int KW, int R, bool PK>
+// W1: the interior weight sum (float)wfull is exactly 1 (a normalised kernel,
+// the reference's set_gaussian / set_average), so acc / wf is acc itself
+template <int KW, int R, bool PK, bool W1 = false>
 __device__ __forceinline__ void convR(const float2 *tile, const ConvArgs &a, int i, int j0,
                                       int tx, int ty0, int dimx, int dimy, long N, float2 res[R],
                                       bool has[R]) {
@@ -336,8 +355,9 @@ __device__ __forceinline__ void convR(const float2 *tile, const ConvArgs &a, int
             const float wf = (float)a.wfull;
 #pragma unroll
             for (int k = 0; k < R; k++) {
-                has[k] = a.wfull != 0;
-                res[k] = make_float2(acc[k].x / wf, acc[k].y / wf);
+                has[k] = W1 || a.wfull != 0;
+                res[k] = W1 ? make_float2(acc[k].x, acc[k].y)
+                            : make_float2(acc[k].x / wf, acc[k].y / wf);
             }
             return;
         }
@@ -481,10 +501,12 @@ __global__ __launch_bounds__(256) void smooth_compose_kernel(
 // halo into LDS (the halo is recomputed by the neighbouring tiles); 3. the
 // sigma_fluid convolution and the motion update.  Per pixel the arithmetic of
 // demons_force_kernel + smooth_compose_kernel: bit-identical.
-template <int KW, int R>
+// FAST: (float)ca.wfull == 1 and sigma_xsq a power of two whose reciprocal
+// `sxq` carries (convR W1, demons_corr SXP); otherwise `sxq` is sigma_xsq
+template <int KW, int R, bool FAST>
 __global__ __launch_bounds__(256) void demons_fused_kernel(
     const float *__restrict__ Iref, const float *__restrict__ Imov, const float2 *__restrict__ u,
-    float2 *__restrict__ out, int dimx, int dimy, int P, float sigma_isq, float sigma_xsq,
+    float2 *__restrict__ out, int dimx, int dimy, int P, float sigma_isq, float sxq,
     ConvArgs ca, int mode, unsigned *__restrict__ status, int bx0) {
     constexpr int c = (KW - 1) / 2;
     constexpr int CY = kCThreadsY * R;
@@ -547,8 +569,8 @@ __global__ __launch_bounds__(256) void demons_fused_kernel(
                 if (s < WW * CH && cc < CW) {
                     const float *w = wt + (r + 1) * WW + (cc + 1);
                     const float gx = (w[1] - w[-1]) / 2.0f, gy = (w[WW] - w[-WW]) / 2.0f;
-                    ct[r * CW + cc] = demons_corr(gx, gy, w[0] - iref[q], sigma_isq, sigma_xsq,
-                                                  zero);
+                    ct[r * CW + cc] = demons_corr<FAST>(gx, gy, w[0] - iref[q], sigma_isq, sxq,
+                                                        zero);
                 }
             }
         } else {
@@ -574,7 +596,7 @@ __global__ __launch_bounds__(256) void demons_fused_kernel(
                         gy = w0 - w[-WW];
                     else
                         gy = (w[WW] - w[-WW]) / 2.0f;
-                    cv = demons_corr(gx, gy, w0 - iref[q], sigma_isq, sigma_xsq, zero);
+                    cv = demons_corr<FAST>(gx, gy, w0 - iref[q], sigma_isq, sxq, zero);
                 }
                 ct[r * CW + cc] = cv;
             }
@@ -589,7 +611,7 @@ __global__ __launch_bounds__(256) void demons_fused_kernel(
     const int r0 = (int)__builtin_amdgcn_readfirstlane(threadIdx.y) * R;
     float2 sm[R];
     bool has[R];
-    convR<KW, R, true>(ct, ca, i, y0 + r0, threadIdx.x, r0, dimx, dimy, N, sm, has);
+    convR<KW, R, true, FAST>(ct, ca, i, y0 + r0, threadIdx.x, r0, dimx, dimy, N, sm, has);
     float2 cv[R];
 #pragma unroll
     for (int k = 0; k < R; k++) {
@@ -601,7 +623,7 @@ __global__ __launch_bounds__(256) void demons_fused_kernel(
 
 // u_new = u_mid (*) G(sigma_diffusion); Logger partials sum ||u_new - prev||,
 // sum ||prev|| per block (fixed order)
-template <int KW, int R = kCr, bool PK = true>
+template <int KW, int R = kCr, bool PK = true, bool W1 = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KW == 7 ? 7 : 8))) void smooth_norm_kernel(const float2 *__restrict__ umid,
                                                           const float2 *__restrict__ prev,
                                                           float2 *__restrict__ out, int dimx,
@@ -619,7 +641,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KW == 7 ? 7
         const int r0 = (int)__builtin_amdgcn_readfirstlane(threadIdx.y) * R;
         float2 sm[R];
         bool has[R];
-        convR<KW, R, PK>(tile, a, i, y0 + r0, threadIdx.x, r0, dimx, dimy, N, sm, has);
+        convR<KW, R, PK, W1>(tile, a, i, y0 + r0, threadIdx.x, r0, dimx, dimy, N, sm, has);
 #pragma unroll
         for (int k = 0; k < R; k++) {
             const int j = y0 + r0 + k;
@@ -749,14 +771,19 @@ void launch_demons_update(const float *Iref, const float *Imov, const float2 *u,
     OF2D_HIP(hipGetLastError());
     smooth_compose_tiles(corr, u, out, dimx, dimy, P, a, mode, nl + nr, nl, gx, es);
     const dim3 g(ni, conv_grid(dimx, dimy).y);
+    float rsx = 0.0f;
+    const bool fast = (float)wfull == 1.0f && pow2_reciprocal(sigma_xsq, &rsx);
     auto go = [&](auto kern) {
         hipLaunchKernelGGL(kern, g, dim3(64, kCThreadsY), 0, st, Iref, Imov, u, out, dimx, dimy, P,
-                           sigma_isq, sigma_xsq, a, mode, status, nl);
+                           sigma_isq, fast ? rsx : sigma_xsq, a, mode, status, nl);
     };
-    switch (kw) {
-        case 3: go(demons_fused_kernel<3, kCr>); break;
-        case 5: go(demons_fused_kernel<5, kCr>); break;
-        default: go(demons_fused_kernel<7, kCr>); break;
+    switch (kw * 2 + fast) {
+        case 6: go(demons_fused_kernel<3, kCr, false>); break;
+        case 7: go(demons_fused_kernel<3, kCr, true>); break;
+        case 10: go(demons_fused_kernel<5, kCr, false>); break;
+        case 11: go(demons_fused_kernel<5, kCr, true>); break;
+        case 15: go(demons_fused_kernel<7, kCr, true>); break;
+        default: go(demons_fused_kernel<7, kCr, false>); break;
     }
     OF2D_HIP(hipGetLastError());
 }
@@ -770,10 +797,14 @@ void launch_smooth_norm(const float2 *umid, const float2 *prev, float2 *out, int
         hipLaunchKernelGGL(kern, conv_grid(dimx, dimy), dim3(64, kCThreadsY),
                            conv_lds_bytes(c, c), st, umid, prev, out, dimx, dimy, P, a, partial);
     };
-    switch (kw) {
-        case 3: go(smooth_norm_kernel<3>); break;
-        case 5: go(smooth_norm_kernel<5>); break;
-        case 7: go(smooth_norm_kernel<7>); break;
+    const bool w1 = (float)wfull == 1.0f;
+    switch (w1 ? kw : -kw) {
+        case 3: go(smooth_norm_kernel<3, kCr, true, true>); break;
+        case -3: go(smooth_norm_kernel<3>); break;
+        case 5: go(smooth_norm_kernel<5, kCr, true, true>); break;
+        case -5: go(smooth_norm_kernel<5>); break;
+        case 7: go(smooth_norm_kernel<7, kCr, true, true>); break;
+        case -7: go(smooth_norm_kernel<7>); break;
         default: go(smooth_norm_kernel<0>); break;
     }
     OF2D_HIP(hipGetLastError());

@@ -48,14 +48,18 @@ def test_thirion_kernel_widths_and_accumulation(gpu, oracle, kw, accum):
     assert np.array_equal(g["warped"], w["warped"])
 
 
-@pytest.mark.parametrize("nx,kw,accum", [(321, 5, 0), (387, 7, 0), (388, 3, 1), (450, 5, 2)])
-def test_thirion_fused_tiles(gpu, oracle, nx, kw, accum):
+@pytest.mark.parametrize("nx,kw,accum,sx", [(321, 5, 0, 0.25), (387, 7, 0, 0.25),
+                                             (388, 3, 1, 0.25), (450, 5, 2, 0.25),
+                                             (450, 5, 0, 0.3), (387, 7, 1, 0.7)])
+def test_thirion_fused_tiles(gpu, oracle, nx, kw, accum, sx):
     """Widths at which the fused force + smoothing + update kernel runs on the
     x-interior tiles and the edge tile columns take the unfused kernels: two
     right edge columns (321: the last tile holds one column, so the tile before
-    it also reaches past dimx), one (387, 388, 450), every accumulation mode."""
+    it also reaches past dimx), one (387, 388, 450), every accumulation mode.
+    sigma_x 0.25 squares to a power of two (the kernels multiply by its
+    reciprocal); 0.3 and 0.7 do not (they divide)."""
     ref, mov = S.texture_pair(nx, seed=nx + kw, ny=150)
-    params = [1.0, 0.25, 1.5, 2.5, kw, accum]
+    params = [1.0, sx, 1.5, 2.5, kw, accum]
     g, w = both(oracle, (nx, 150), [6], 0, 3, params, 1, ref, mov, fixed_iters=1)
     assert g["iters"] == w["iters"]
     assert np.array_equal(g["motion"], w["motion"])
