@@ -38,6 +38,11 @@ constexpr int kCThreadsY = 4;
 // kCThreadsY * kCr j-lines high): a taller tile loads fewer halo rows per
 // output and shares each LDS tap column between more outputs
 constexpr int kCr = 8;
+// warped slots per thread per gather batch of the fused kernel (tools/ A/B
+// builds override it)
+#ifndef OF2D_DEMONS_BW
+#define OF2D_DEMONS_BW 6
+#endif
 typedef float v2f __attribute__((ext_vector_type(2)));
 
 // warp2d values of Imov at B pixels (a[q], b[q]) with motion u
@@ -58,7 +63,8 @@ __device__ __forceinline__ void warp_batch(const float *__restrict__ Imov,
     float own[B];
 #pragma unroll
     for (int q = 0; q < B; q++) {
-        in[q] = valid[q] && a[q] >= 0 && a[q] < dimx && b[q] >= 0 && b[q] < dimy;
+        // bitwise, not short-circuit: no exec-mask branches around the loads
+        in[q] = valid[q] & ((unsigned)a[q] < (unsigned)dimx) & ((unsigned)b[q] < (unsigned)dimy);
         const unsigned idx = in[q] ? (unsigned)(b[q] * P + a[q]) : 0u;
         m[q] = u[idx];
         own[q] = Imov[idx];
@@ -519,7 +525,7 @@ __global__ __launch_bounds__(256) void demons_fused_kernel(
     {
         // 1. slot s <-> pixel (x0 - c - 1 + s % WW, y0 - c - 1 + s / WW), in
         // batches of BW slots per thread
-        constexpr int NW = (WW * WH + 255) / 256, BW = 6;
+        constexpr int NW = (WW * WH + 255) / 256, BW = OF2D_DEMONS_BW;
 #pragma unroll
         for (int q0 = 0; q0 < NW; q0 += BW) {
             int a[BW], b[BW];
@@ -544,15 +550,17 @@ __global__ __launch_bounds__(256) void demons_fused_kernel(
     // run with no row seam inside a 32-lane group (no LDS bank conflicts), and
     // its writes of ct stay contiguous.  Iref of the slots is loaded while
     // the warp tile completes.
+    // (unconditional loads: a slot outside the image reads element 0 and keeps
+    // 0, so the loads issue back to back instead of one branch each)
     constexpr int NC = (WW * CH + 255) / 256;
     float iref[NC];
 #pragma unroll
     for (int q = 0; q < NC; q++) {
         const int s = tid + 256 * q, r = s / WW, cc = s - r * WW;
         const int i = x0 - c + cc, j = y0 - c + r;
-        iref[q] = (s < WW * CH && cc < CW && (unsigned)j < (unsigned)dimy)
-                      ? Iref[(long)j * P + i]
-                      : 0.0f;
+        const bool ok = (s < WW * CH) & (cc < CW) & ((unsigned)j < (unsigned)dimy);
+        const float t = Iref[ok ? (unsigned)(j * P + i) : 0u];
+        iref[q] = ok ? t : 0.0f;
     }
     __syncthreads();
     {
