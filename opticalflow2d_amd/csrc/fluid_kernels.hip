@@ -732,8 +732,6 @@ void launch_increment(const float2 *u, const float4 *vel, float2 *R, int dimx, i
 //   force and packs again.  One pass instead of three (integrate + Logger,
 //   Jacobian, pack: 69 instead of 101 B/px), and no prev read or write in the
 //   common case.
-__global__ __launch_bounds__(1024) void min_final_kernel(const float *__restrict__ part, int n,
-                                                         float *__restrict__ out);
 template <bool kPrev>
 __global__ __launch_bounds__(256) void fluid_step_kernel(
     const float2 *__restrict__ u, const float2 *__restrict__ R, float2 *__restrict__ uo,
@@ -847,8 +845,7 @@ __global__ __launch_bounds__(256) void fluid_step_kernel(
 void launch_fluid_step(const float2 *u, const float2 *R, float2 *uo, const float2 *prev,
                        const float *scal,
                        const float2 *dI, const float *It, float4 *vb, int dimx, int dimy, int P,
-                       void *H, unsigned epoch, double *lpart, float *jpart, float *jmin,
-                       hipStream_t st) {
+                       void *H, unsigned epoch, double *lpart, float *jpart, hipStream_t st) {
     const dim3 g = field_grid(dimx, dimy);
     if (prev)
         hipLaunchKernelGGL(fluid_step_kernel<true>, g, dim3(64, 4), 0, st, u, R, uo, prev, scal,
@@ -856,7 +853,55 @@ void launch_fluid_step(const float2 *u, const float2 *R, float2 *uo, const float
     else
         hipLaunchKernelGGL(fluid_step_kernel<false>, g, dim3(64, 4), 0, st, u, R, uo, prev, scal,
                            dI, It, vb, dimx, dimy, P, (v4u *)H, epoch, lpart, jpart);
-    hipLaunchKernelGGL(min_final_kernel, dim3(1), dim3(1024), 0, st, jpart, (int)(g.x * g.y), jmin);
+    OF2D_HIP(hipGetLastError());
+}
+
+// one 1024-thread block: the Logger sums in reduce_partials_kernel's order
+// (strided per-thread sums, wave trees, the 16 waves in order), the Jacobian
+// minimum as min_final_kernel, then the report to host memory
+__global__ __launch_bounds__(1024) void fluid_report_kernel(const double *__restrict__ p, int nb,
+                                                            const float *__restrict__ jpart,
+                                                            float *__restrict__ scal,
+                                                            const unsigned *__restrict__ status,
+                                                            FluidReport *__restrict__ rep) {
+    double a = 0.0, b = 0.0;
+    float m = __builtin_inff();
+    for (int i = threadIdx.x; i < nb; i += 1024) {
+        a += p[2 * i];
+        b += p[2 * i + 1];
+        m = (jpart[i] < m) ? jpart[i] : m;
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        a += __shfl_down(a, off);
+        b += __shfl_down(b, off);
+    }
+    __shared__ double red[2][16];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (lane == 0) {
+        red[0][wave] = a;
+        red[1][wave] = b;
+    }
+    m = wide_min(m);  // (synchronises the block)
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < 16; w++) {
+            a += red[0][w];
+            b += red[1][w];
+        }
+        scal[2] = m;
+        rep->sums[0] = a;
+        rep->sums[1] = b;
+        rep->maxabs = scal[0];
+        rep->dt = scal[1];
+        rep->jmin = m;
+        rep->status = *status;
+    }
+}
+
+void launch_fluid_report(const double *lpart, int nb, const float *jpart, float *scal,
+                         const unsigned *status, FluidReport *report, hipStream_t st) {
+    hipLaunchKernelGGL(fluid_report_kernel, dim3(1), dim3(1024), 0, st, lpart, nb, jpart, scal,
+                       status, report);
     OF2D_HIP(hipGetLastError());
 }
 
@@ -895,12 +940,4 @@ void launch_logger(const float4 *vb, float2 *u, float2 *prev, int dimx, int dimy
     OF2D_HIP(hipGetLastError());
 }
 
-// ------------------------------------------------------------ min of per-block minima
-__global__ __launch_bounds__(1024) void min_final_kernel(const float *__restrict__ part, int n,
-                                                         float *__restrict__ out) {
-    float m = __builtin_inff();
-    for (int k = threadIdx.x; k < n; k += 1024) m = (part[k] < m) ? part[k] : m;
-    m = wide_min(m);
-    if (threadIdx.x == 0) *out = m;
-}
 }  // namespace of2d

@@ -310,13 +310,28 @@ int increment_nblocks(int dimx, int dimy);
 void launch_increment(const float2 *u, const float4 *vel, float2 *R, int dimx, int dimy, int P,
                       float *part, float *scal, hipStream_t st);
 // uo <- u + R dt (dt < 65) or u; Logger partials of uo against prev (against u
-// when prev is null); per-block Jacobian minima of uo into jpart and their min
-// into *jmin; vb.zw <- force(uo) and granule region 0 tagged with `epoch` for
-// the next sweep (fluid_kernels.hip fluid_step_kernel)
+// when prev is null); per-block Jacobian minima of uo into jpart (their min:
+// launch_fluid_report); vb.zw <- force(uo) and granule region 0 tagged with
+// `epoch` for the next sweep (fluid_kernels.hip fluid_step_kernel)
 void launch_fluid_step(const float2 *u, const float2 *R, float2 *uo, const float2 *prev,
                        const float *scal, const float2 *dI, const float *It, float4 *vb, int dimx,
                        int dimy, int P, void *H, unsigned epoch, double *lpart, float *jpart,
-                       float *jmin, hipStream_t st);
+                       hipStream_t st);
+// Per-iteration report a kernel writes straight into host memory (fine-grained
+// pinned, so no copy launches): the Fluid loop's Logger sums, maxabs, dt,
+// min Jacobian and status word
+struct FluidReport {
+    double sums[2];
+    float maxabs, dt, jmin;
+    unsigned status;
+};
+// The end of a Fluid iteration's device work: the nb Logger partial pairs
+// reduced as launch_reduce_partials does (same order, same bits), the minimum
+// of the nb Jacobian partials into scal[2], and {sums, scal[0..2], *status}
+// written to the host-mapped FluidReport (one launch instead of reduce + min +
+// three copies)
+void launch_fluid_report(const double *lpart, int nb, const float *jpart, float *scal,
+                         const unsigned *status, FluidReport *report, hipStream_t st);
 void launch_logger(const float4 *vb, float2 *u, float2 *prev, int dimx, int dimy, int P,
                    double *partial, hipStream_t st);
 

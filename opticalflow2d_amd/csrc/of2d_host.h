@@ -100,6 +100,7 @@ struct HostScratch {
     double *sums = nullptr;
     unsigned *status = nullptr;
     float *flt = nullptr;
+    FluidReport *report = nullptr;  // hipHostMallocCoherent
     int cap = 0;
     void ensure(int n);
     ~HostScratch();
@@ -163,6 +164,7 @@ class Registration {
     int loop_elastic(Level &L, int niter, int &final_buf);
     int loop_curvature(Level &L, int niter, int &final_buf);
     void check_status();
+    void check_reported_status(unsigned st);
 
     int dimx_, dimy_, nscales_, nrefine_, reg_, verbose_;
     std::vector<int> niter_;

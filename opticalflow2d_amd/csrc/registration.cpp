@@ -37,6 +37,9 @@ void HostScratch::ensure(int n) {
     if (sums) (void)hipHostFree(sums);
     if (flt) (void)hipHostFree(flt);
     if (!status) OF2D_HIP(hipHostMalloc(&status, 64 * sizeof(unsigned)));
+    if (!report)
+        OF2D_HIP(hipHostMalloc(&report, sizeof(FluidReport),
+                               hipHostMallocCoherent | hipHostMallocMapped));
     OF2D_HIP(hipHostMalloc(&sums, sizeof(double) * 4 * n));
     OF2D_HIP(hipHostMalloc(&flt, sizeof(float) * 4 * n));
     cap = n;
@@ -45,6 +48,7 @@ HostScratch::~HostScratch() {
     if (sums) (void)hipHostFree(sums);
     if (flt) (void)hipHostFree(flt);
     if (status) (void)hipHostFree(status);
+    if (report) (void)hipHostFree(report);
 }
 
 bool valid_regularisation_parameters(int reg, unsigned np) {
@@ -219,7 +223,11 @@ void Registration::set_images(const double *ref, const double *mov) {
 void Registration::check_status() {
     OF2D_HIP(hipMemcpyAsync(hs_.status, d_status_, sizeof(unsigned), hipMemcpyDeviceToHost, st_));
     OF2D_HIP(hipStreamSynchronize(st_));
-    const unsigned st = hs_.status[0];
+    check_reported_status(hs_.status[0]);
+}
+
+// a status word already read back (after the stream's sync)
+void Registration::check_reported_status(unsigned st) {
     if (st) OF2D_HIP(hipMemsetAsync(d_status_, 0, sizeof(unsigned), st_));
     if (st & kStatusDivZero) throw std::runtime_error("Divide by zero exception");
     if (st & kStatusSpinTimeout)

@@ -185,18 +185,19 @@ int Registration::loop_fluid(Level &L, int niter) {
         // integrate, Logger, Jacobian and the next iteration's force in one pass
         launch_fluid_step(est, L.increment.p, L.force.p, prev_separate ? prev : nullptr, scal,
                           L.dI.p, L.It.p, L.vb.p, L.dx, L.dy, L.P, L.sorH.p, ep + 1, d_partial_,
-                          L.part.p, scal + 2, st_);
+                          L.part.p, st_);
         std::swap(L.est[0], L.force);
         prev_separate = false;
         packed = true;
-        launch_reduce_partials(d_partial_, nb, 1, d_sums_, st_);
-        OF2D_HIP(hipMemcpyAsync(hs_.sums, d_sums_, sizeof(double) * 2, hipMemcpyDeviceToHost, st_));
-        OF2D_HIP(hipMemcpyAsync(hs_.flt, scal, sizeof(float) * 3, hipMemcpyDeviceToHost, st_));
-        check_status();
-        const float maxabs = hs_.flt[0], dt = hs_.flt[1], jmin = hs_.flt[2];
+        // Logger sums, maxabs, dt, min Jacobian and the status word straight
+        // into host memory: one launch, then the one sync of the iteration
+        launch_fluid_report(d_partial_, nb, L.part.p, scal, d_status_, hs_.report, st_);
+        OF2D_HIP(hipStreamSynchronize(st_));
+        check_reported_status(hs_.report->status);
+        const float maxabs = hs_.report->maxabs, dt = hs_.report->dt, jmin = hs_.report->jmin;
         print("Dumax: %.3f\tMaxabs increment: %.3f\t Timestep: %.3f\n", (double)0.65f,
               (double)maxabs, (double)dt);
-        const float err = logger_error(hs_.sums[0], hs_.sums[1], npx);
+        const float err = logger_error(hs_.report->sums[0], hs_.report->sums[1], npx);
         last_err_.push_back(err);
         if (verbose_) print("Iteration: %d\tError:%.4f\n", iter, (double)err);
         if (!fixed_ && err < 0.001f && iter > 1) {
