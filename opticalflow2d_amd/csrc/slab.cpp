@@ -66,6 +66,10 @@ struct of2d_slab {
     unsigned *d_status = nullptr;
     of2d::HostScratch hs;
     int chunk = 33;  // eleven fused triples per chunk
+    // a fixed-iteration run has no break to replay, so its chunks only set how
+    // often the partial rows are reduced: 33 triples per reduction launch
+    int chunk_fixed = 99;
+    int chunk_cap() const { return chunk > chunk_fixed ? chunk : chunk_fixed; }
     int fin = 0;    // buffer holding the final motion
     int start = 0;  // zeroed buffer the next run starts from (motion_est->reset())
     // the triple kernel takes the gradients from Iaux (= Imov) instead of dI:
@@ -348,7 +352,7 @@ static int slab_create(of2d_slab **out, int dimx, int dimy, float alpha, int ran
         s->Iref.alloc(dimx, s->nrows, 3);
         s->Imov.alloc(dimx, s->nrows, 3);
         const int nb = slab_geometry(s).nb;
-        OF2D_HIP(hipMalloc(&s->d_partial, sizeof(double) * 2 * (size_t)nb * s->chunk));
+        OF2D_HIP(hipMalloc(&s->d_partial, sizeof(double) * 2 * (size_t)nb * s->chunk_cap()));
         OF2D_HIP(hipMalloc(&s->d_sums, sizeof(double) * 2 * s->chunk));
         OF2D_HIP(hipMalloc(&s->d_status, 64 * sizeof(unsigned)));
         OF2D_HIP(hipMemset(s->d_status, 0, 64 * sizeof(unsigned)));
@@ -360,7 +364,7 @@ static int slab_create(of2d_slab **out, int dimx, int dimy, float alpha, int ran
             if (grp->n != nranks) throw std::invalid_argument("slab: group size != nranks");
             OF2D_HIP(hipEventCreateWithFlags(&s->ev_ready, hipEventDisableTiming));
             OF2D_HIP(hipEventCreateWithFlags(&s->ev_done, hipEventDisableTiming));
-            OF2D_HIP(hipMalloc(&s->d_red, sizeof(double) * 2 * (size_t)s->chunk));
+            OF2D_HIP(hipMalloc(&s->d_red, sizeof(double) * 2 * (size_t)s->chunk_cap()));
             std::lock_guard<std::mutex> lk(grp->m);
             if (grp->slabs[rank]) throw std::invalid_argument("slab: rank already in the group");
             grp->slabs[rank] = s;
@@ -557,7 +561,7 @@ int of2d_slab_run(of2d_slab *s, int niter, int fixed_iters, int *iters_done) {
         // at the end of the previous run (below)
         int a = s->start, k0 = 0, done = -1;
         while (k0 < niter && done < 0) {
-            const int C = std::min(s->chunk, niter - k0);
+            const int C = std::min(fixed_iters ? s->chunk_fixed : s->chunk, niter - k0);
             auto part = [&](int t) { return s->d_partial + (size_t)t * nb * 2; };
             // triples (then a pair / single tail) alternate between the two
             // buffers other than the chunk's start buffer a, which stays intact
