@@ -219,6 +219,22 @@ def test_slab_single_rank_equals_registration(gpu):
     s.close()
 
 
+def test_time_kernel_leaves_motion_intact(gpu):
+    """of2d_slab_time_kernel launches into scratch (include/of2d.h): the last
+    run's motion stays readable, and a later run is unchanged by it."""
+    ref, mov = S.texture_pair(256, seed=5)
+    s = SlabSolver(256, 256, 0.1)
+    s.set_images(ref, mov)
+    for fixed, niter in ((True, 40), (False, 300)):
+        done = s.run(niter, fixed_iters=fixed)
+        m = s.motion()
+        assert s.time_kernel(7) > 0
+        assert np.array_equal(s.motion(), m)
+        assert s.run(niter, fixed_iters=fixed) == done
+        assert np.array_equal(s.motion(), m)
+    s.close()
+
+
 def test_slab_full_size_4096_bitwise(gpu, oracle):
     """BASELINE config 2 grid (4096^2): a few Jacobi iterations bit for bit
     against the oracle's HS loop on the same gradients."""
