@@ -37,7 +37,16 @@ constexpr int kCThreadsY = 4;
 // j-lines per thread of the product smoothing kernels (the tile is
 // kCThreadsY * kCr j-lines high): a taller tile loads fewer halo rows per
 // output and shares each LDS tap column between more outputs
-constexpr int kCr = 8;
+// waves-per-SIMD floor of the fused kernel (tools/ A/B builds set it)
+#ifndef OF2D_DEMONS_WPE
+#define OF2D_DEMONS_FUSED_ATTR
+#else
+#define OF2D_DEMONS_FUSED_ATTR __attribute__((amdgpu_waves_per_eu(OF2D_DEMONS_WPE)))
+#endif
+#ifndef OF2D_DEMONS_CR
+#define OF2D_DEMONS_CR 8
+#endif
+constexpr int kCr = OF2D_DEMONS_CR;
 // warped slots per thread per gather batch of the fused kernel (tools/ A/B
 // builds override it)
 #ifndef OF2D_DEMONS_BW
@@ -510,7 +519,7 @@ __global__ __launch_bounds__(256) void smooth_compose_kernel(
 // FAST: (float)ca.wfull == 1 and sigma_xsq a power of two whose reciprocal
 // `sxq` carries (convR W1, demons_corr SXP); otherwise `sxq` is sigma_xsq
 template <int KW, int R, bool FAST>
-__global__ __launch_bounds__(256) void demons_fused_kernel(
+__global__ __launch_bounds__(256) OF2D_DEMONS_FUSED_ATTR void demons_fused_kernel(
     const float *__restrict__ Iref, const float *__restrict__ Imov, const float2 *__restrict__ u,
     float2 *__restrict__ out, int dimx, int dimy, int P, float sigma_isq, float sxq,
     ConvArgs ca, int mode, unsigned *__restrict__ status, int bx0) {
