@@ -92,7 +92,13 @@ int of2d_last_errors(const of2d_ctx *ctx, float *out, int cap);
  *   "chunk" (>=1): iterations enqueued between host convergence checks
  *   "device" (>=0): HIP device ordinal, must be set before of2d_set_images
  *   "hs_gradients_from_image" (-1 auto = default, 0, 1): as for the slab
- *   solver (of2d_slab_set_option); bit-identical results either way */
+ *   solver (of2d_slab_set_option); bit-identical results either way
+ *   "logger_fp64" (0 = default / 1): 0 computes the Logger norms as the
+ *   reference does (float running sums, of2d_motion_norms), so the break of
+ *   ImageRegistrationOpticalFlow.cpp:131-134 falls on the reference's
+ *   iteration at every size; 1 sums the magnitudes in fp64 (faster: the fused
+ *   multi-iteration kernels stay on; at >= 4096^2 the break can move by a few
+ *   iterations).  fixed_iters runs take no break and use the fp64 sums. */
 int of2d_set_option(of2d_ctx *ctx, const char *key, double value);
 
 /* ---- gateway: the process-global singleton of WrapperOpticalFlow2d.cpp:13.
@@ -181,6 +187,17 @@ int of2d_slab_group_create(of2d_slab_group **out, int nranks);
 int of2d_slab_group_destroy(of2d_slab_group *g);
 int of2d_slab_create_local(of2d_slab **out, int dimx, int dimy, float alpha, int rank,
                            int nranks, int device, of2d_slab_group *g);
+
+/* ---- kernel-level test entry: the Logger's norms ----
+ * Motion::norm (src/Motion.cpp:42-49) as Logger::update_error (src/Logger.cpp:
+ * 32-51) takes it: the float running sums, in linear order, of
+ * sqrt((double)x^2 + (double)y^2) over (cur - prev) -> sums[0] and over prev
+ * -> sums[1] (not divided by dimx*dimy), bit-identical to the reference's.
+ * cur / prev: host float [dimx*dimy*2], interleaved x, y per pixel (coord2d),
+ * idx = i + j*dimx.  resolves (optional, int[2]): tiles of 4096 terms the
+ * device walk had to resolve term by term (a cost figure, not a result). */
+int of2d_motion_norms(const float *cur, const float *prev, int dimx, int dimy, float *sums,
+                      int *resolves);
 
 /* ---- library info ---- */
 const char *of2d_version(void);

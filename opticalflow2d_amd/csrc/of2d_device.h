@@ -196,6 +196,18 @@ struct PartialRuns {
     void reduce(const double *partial, int stride, double *sums, hipStream_t st) const;
 };
 
+// ---------------------------------------------------------------- Logger norms
+// The reference's Motion::norm (src/Motion.cpp:42-49) bit for bit: the float
+// running sum S <- (float)((double)S + sqrt((double)x^2 + (double)y^2)) over
+// the pixels in linear order, of |cur - prev| (out[0]) and |prev| (out[1])
+// (Logger::update_error, src/Logger.cpp:32-51; seqnorm_kernels.hip).  out[]
+// holds the sums, not yet divided by N.  ws: seqnorm_workspace_bytes; dbg
+// (optional): tiles the walk resolved from their magnitudes, per norm.
+constexpr int kSnTile = 4096;  // consecutive terms per tile
+size_t seqnorm_workspace_bytes(int dimx, int dimy);
+void launch_seqnorm(const float2 *cur, const float2 *prev, int dimx, int dimy, int P, void *ws,
+                    float *out, int *dbg, hipStream_t st);
+
 // ---------------------------------------------------------------- fields
 void launch_d2f(const double *in, int dimx, int dimy, float *out, int P, int row_offset,
                 hipStream_t st);

@@ -172,6 +172,14 @@ class Registration {
     std::vector<int> ldx_, ldy_;
     std::vector<Level> lv_;
     bool fixed_ = false;
+    // Logger norms: the reference's float running sums (seqnorm, default) or
+    // fp64 sums of the fused partials (logger_fp64; fixed_iters runs always)
+    bool logger_fp64_ = false;
+    bool exact_norms() const { return !fixed_ && !logger_fp64_; }
+    // enqueue the exact norms of one Logger update into d_seq_[2t], [2t + 1]
+    void seqnorm(const Level &L, const float2 *cur, const float2 *prev, int t);
+    DevArray<unsigned char> d_seqws_;  // seqnorm workspace (level 0 size)
+    DevArray<float> d_seq_;            // per-iteration exact sums of a chunk
     int chunk_ = 33;  // eleven fused triples per chunk
     int gi_ = -1;     // triple kernel: dI from Iaux (1), from dI (0), by size (-1)
     int device_ = -1;

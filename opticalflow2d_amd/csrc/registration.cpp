@@ -150,6 +150,8 @@ Registration::~Registration() {
 void Registration::set_option(const std::string &key, double v) {
     if (key == "fixed_iters")
         fixed_ = v != 0;
+    else if (key == "logger_fp64")
+        logger_fp64_ = v != 0;
     else if (key == "chunk") {
         if (ready_) throw std::invalid_argument("option 'chunk' must be set before first use");
         chunk_ = std::max(1, (int)v);
@@ -198,6 +200,8 @@ void Registration::ensure_device() {
     OF2D_HIP(hipMalloc(&d_scalar_, (16 + 256) * sizeof(float)));
     OF2D_HIP(hipDeviceSynchronize());  // null-stream memset vs the non-blocking stream
     hs_.ensure(std::max(chunk_, 64));
+    d_seqws_.alloc(seqnorm_workspace_bytes(dimx_, dimy_));
+    d_seq_.alloc(2 * (size_t)std::max(chunk_, 64));
     ready_ = true;
 }
 
@@ -282,6 +286,10 @@ void Registration::estimate_level(int s) {
     }
 }
 
+void Registration::seqnorm(const Level &L, const float2 *cur, const float2 *prev, int t) {
+    launch_seqnorm(cur, prev, L.dx, L.dy, L.P, d_seqws_.p, d_seq_.p + 2 * (size_t)t, nullptr, st_);
+}
+
 // Speculative chunked iteration loop shared by every solver whose iteration
 // reads motion_est from one buffer and writes the next iterate to another
 // (HS, Demons, Elastic, Curvature).  step(src, dst, partial) enqueues one
@@ -299,6 +307,10 @@ int Registration::run_chunked(Level &L, int niter, int nb, const StepFn &step, i
         d_all_.alloc(2 * (size_t)niter);
         hs_.ensure((niter + 1) / 2);  // 4 doubles per unit of capacity
     }
+    // the reference's float norms need every iterate in memory: single steps,
+    // each followed by its seqnorm
+    const bool exact = exact_norms();
+    const bool use2 = step2 && !exact, use3 = step3 && !exact;
     int a = 0, k0 = 0;
     auto src_of = [](int a_, int t) { return t == 0 ? a_ : (t % 2 == 1 ? (a_ + 1) % 3 : (a_ + 2) % 3); };
     auto dst_of = [](int a_, int t) { return t % 2 == 0 ? (a_ + 1) % 3 : (a_ + 2) % 3; };
@@ -307,14 +319,14 @@ int Registration::run_chunked(Level &L, int niter, int nb, const StepFn &step, i
         auto part = [&](int t) { return d_partial_ + (size_t)t * nb * 2; };
         int end = -1;  // pairs: the buffer holding the chunk's last iterate
         PartialRuns runs;  // which kernel wrote how many block partials per row
-        if (step2) {
+        if (use2) {
             // fused launches (triples, then a pair / single tail) alternate
             // between the two buffers other than a
             auto other = [&](int b) { return b == (a + 1) % 3 ? (a + 2) % 3 : (a + 1) % 3; };
             int cur = a, t = 0;
             while (t < C) {
                 const int nxt = other(cur);
-                if (step3 && C - t >= 3) {
+                if (use3 && C - t >= 3) {
                     step3(L.est[cur].p, L.est[nxt].p, part(t), part(t + 1), part(t + 2));
                     runs.add(t, 3, nblk ? nblk[2] : nb);
                     t += 3;
@@ -331,37 +343,46 @@ int Registration::run_chunked(Level &L, int niter, int nb, const StepFn &step, i
             }
             end = cur;
         } else {
-            for (int t = 0; t < C; t++) step(L.est[src_of(a, t)].p, L.est[dst_of(a, t)].p, part(t));
+            for (int t = 0; t < C; t++) {
+                step(L.est[src_of(a, t)].p, L.est[dst_of(a, t)].p, part(t));
+                if (exact) seqnorm(L, L.est[dst_of(a, t)].p, L.est[src_of(a, t)].p, t);
+            }
             runs.add(0, C, nblk ? nblk[0] : nb);
         }
         if (fixed_) {
             // no break to decide: every chunk's sums stay on the device and are
             // read back once after the loop (no host round trip per chunk)
             runs.reduce(d_partial_, nb, d_all_.p + 2 * (size_t)k0, st_);
-            a = step2 ? end : dst_of(a, C - 1);
+            a = use2 ? end : dst_of(a, C - 1);
             k0 += C;
             continue;
         }
-        runs.reduce(d_partial_, nb, d_sums_, st_);
-        OF2D_HIP(hipMemcpyAsync(hs_.sums, d_sums_, sizeof(double) * 2 * C, hipMemcpyDeviceToHost,
-                                st_));
+        if (exact) {
+            OF2D_HIP(hipMemcpyAsync(hs_.flt, d_seq_.p, sizeof(float) * 2 * C,
+                                    hipMemcpyDeviceToHost, st_));
+        } else {
+            runs.reduce(d_partial_, nb, d_sums_, st_);
+            OF2D_HIP(hipMemcpyAsync(hs_.sums, d_sums_, sizeof(double) * 2 * C,
+                                    hipMemcpyDeviceToHost, st_));
+        }
         check_status();  // synchronises the stream; throws the reference's runtime_error
         for (int t = 0; t < C; t++) {
             const int k = k0 + t;
-            const float err = logger_error(hs_.sums[2 * t], hs_.sums[2 * t + 1], npx);
+            const float err = exact ? logger_error(hs_.flt[2 * t], hs_.flt[2 * t + 1], npx)
+                                    : logger_error(hs_.sums[2 * t], hs_.sums[2 * t + 1], npx);
             last_err_.push_back(err);
             if (verbose_) print("Iteration: %d\tError:%.4f\n", k, (double)err);
             if (!fixed_ && err < 0.001f && k > 1) {  // ImageRegistrationOpticalFlow.cpp:131-134
                 // dst(t) was overwritten by iteration t+2, or (pairs) never
                 // written: replay single steps from the chunk's start buffer a
-                if (step2 || t + 2 <= C - 1)
+                if (use2 || t + 2 <= C - 1)
                     for (int r = 0; r <= t; r++)
                         step(L.est[src_of(a, r)].p, L.est[dst_of(a, r)].p, d_partial_);
                 final_buf = dst_of(a, t);
                 return k + 1;
             }
         }
-        a = step2 ? end : dst_of(a, C - 1);
+        a = use2 ? end : dst_of(a, C - 1);
         k0 += C;
     }
     if (fixed_ && niter > 0) {

@@ -186,18 +186,24 @@ int Registration::loop_fluid(Level &L, int niter) {
         launch_fluid_step(est, L.increment.p, L.force.p, prev_separate ? prev : nullptr, scal,
                           L.dI.p, L.It.p, L.vb.p, L.dx, L.dy, L.P, L.sorH.p, ep + 1, d_partial_,
                           L.part.p, st_);
+        const bool exact = exact_norms();
+        if (exact) seqnorm(L, L.force.p, prev_separate ? prev : est, 0);
         std::swap(L.est[0], L.force);
         prev_separate = false;
         packed = true;
         // Logger sums, maxabs, dt, min Jacobian and the status word straight
         // into host memory: one launch, then the one sync of the iteration
         launch_fluid_report(d_partial_, nb, L.part.p, scal, d_status_, hs_.report, st_);
+        if (exact)
+            OF2D_HIP(hipMemcpyAsync(hs_.flt, d_seq_.p, 2 * sizeof(float), hipMemcpyDeviceToHost,
+                                    st_));
         OF2D_HIP(hipStreamSynchronize(st_));
         check_reported_status(hs_.report->status);
         const float maxabs = hs_.report->maxabs, dt = hs_.report->dt, jmin = hs_.report->jmin;
         print("Dumax: %.3f\tMaxabs increment: %.3f\t Timestep: %.3f\n", (double)0.65f,
               (double)maxabs, (double)dt);
-        const float err = logger_error(hs_.report->sums[0], hs_.report->sums[1], npx);
+        const float err = exact ? logger_error(hs_.flt[0], hs_.flt[1], npx)
+                                : logger_error(hs_.report->sums[0], hs_.report->sums[1], npx);
         last_err_.push_back(err);
         if (verbose_) print("Iteration: %d\tError:%.4f\n", iter, (double)err);
         if (!fixed_ && err < 0.001f && iter > 1) {
@@ -247,6 +253,7 @@ int Registration::loop_elastic(Level &L, int niter, int &final_buf) {
     };
     last_err_.clear();
     final_buf = 0;
+    const bool exact = exact_norms();
     int k0 = 0;
     while (k0 < niter) {
         const int C = std::min(chunk_, niter - k0);
@@ -254,16 +261,28 @@ int Registration::loop_elastic(Level &L, int niter, int &final_buf) {
                                 hipMemcpyDeviceToDevice, st_));
         for (int t = 0; t < C; t++) {
             update();
+            // the logger pass moves the new motion into est and prev: the
+            // exact norms read the previous motion from a copy
+            if (exact)
+                OF2D_HIP(hipMemcpyAsync(L.force.base, L.tmp.base, L.tmp.bytes(),
+                                        hipMemcpyDeviceToDevice, st_));
             launch_logger(L.vb.p, est, prev, L.dx, L.dy, L.P, d_partial_ + (size_t)t * nb * 2,
                           st_);
+            if (exact) seqnorm(L, est, L.force.p, t);
         }
-        launch_reduce_partials(d_partial_, nb, C, d_sums_, st_);
-        OF2D_HIP(hipMemcpyAsync(hs_.sums, d_sums_, sizeof(double) * 2 * C, hipMemcpyDeviceToHost,
-                                st_));
+        if (exact) {
+            OF2D_HIP(hipMemcpyAsync(hs_.flt, d_seq_.p, sizeof(float) * 2 * C,
+                                    hipMemcpyDeviceToHost, st_));
+        } else {
+            launch_reduce_partials(d_partial_, nb, C, d_sums_, st_);
+            OF2D_HIP(hipMemcpyAsync(hs_.sums, d_sums_, sizeof(double) * 2 * C,
+                                    hipMemcpyDeviceToHost, st_));
+        }
         check_status();
         for (int t = 0; t < C; t++) {
             const int k = k0 + t;
-            const float err = logger_error(hs_.sums[2 * t], hs_.sums[2 * t + 1], npx);
+            const float err = exact ? logger_error(hs_.flt[2 * t], hs_.flt[2 * t + 1], npx)
+                                    : logger_error(hs_.sums[2 * t], hs_.sums[2 * t + 1], npx);
             last_err_.push_back(err);
             if (verbose_) print("Iteration: %d\tError:%.4f\n", k, (double)err);
             if (!fixed_ && err < 0.001f && k > 1) {

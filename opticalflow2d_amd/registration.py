@@ -126,6 +126,25 @@ def OpticalFlow2d(*args, nargout: int = 0):
     return None
 
 
+# ------------------------------------------------------------------ Logger norms
+def motion_norms(cur, prev, dims: Sequence[int]):
+    """Motion::norm sums of (cur - prev) and of prev exactly as the reference's
+    Logger takes them (src/Motion.cpp:42-49, src/Logger.cpp:32-51): float
+    running sums in linear order, on the device.  ``cur`` / ``prev`` are
+    float32 ``[dimx*dimy, 2]`` (interleaved x, y per pixel, idx = i + j*dimx).
+    Returns ``(sums float32[2], resolves int32[2])``."""
+    dimx, dimy = int(dims[0]), int(dims[1])
+    c = np.ascontiguousarray(np.asarray(cur, np.float32).reshape(-1))
+    p = np.ascontiguousarray(np.asarray(prev, np.float32).reshape(-1))
+    if c.size != 2 * dimx * dimy or p.size != c.size:
+        raise ValueError("cur / prev need dimx*dimy*2 floats")
+    sums = np.zeros(2, np.float32)
+    res = np.zeros(2, np.int32)
+    L = _lib.lib()
+    check(L.of2d_motion_norms(c, p, dimx, dimy, sums, res), L.of2d_gateway_last_error().decode())
+    return sums, res
+
+
 # ------------------------------------------------------------------ object API
 class ImageRegistration:
     """Handle on one registration context (of2d_create ... of2d_destroy).
@@ -134,7 +153,7 @@ class ImageRegistration:
     values, finest level first), ``nscales``, ``reg``, ``params`` (nparams
     floats), ``nrefine``, ``verbose``.  Extra keyword options map to
     ``of2d_set_option`` (``fixed_iters``, ``chunk``, ``device``,
-    ``hs_gradients_from_image``).
+    ``hs_gradients_from_image``, ``logger_fp64``).
     """
 
     def __init__(self, dims: Sequence[int], niter: Sequence[int], nscales: int, reg: int,
@@ -217,4 +236,4 @@ class ImageRegistration:
 
 
 __all__ = ["Regularisation", "Verbose", "MotionAccumulation", "OpticalFlow2d",
-           "ImageRegistration", "set_print_sink", "Of2dError"]
+           "ImageRegistration", "set_print_sink", "Of2dError", "motion_norms"]

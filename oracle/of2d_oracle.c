@@ -188,6 +188,16 @@ static float motion_maxabs(const v2 *u, unsigned n) {
 }
 
 float oracle_motion_norm(const float *u, int n) { return motion_norm((const v2 *)u, (unsigned)n); }
+/* the float running sum of src/Motion.cpp:43-46 before the division by n
+ * (checker of the device's of2d_motion_norms) */
+float oracle_motion_norm_sum(const float *u, int n) {
+    float norm = 0.0f;
+    for (unsigned i = 0; i < (unsigned)n; i++) {
+        double px = (double)u[2 * i], py = (double)u[2 * i + 1];
+        norm = (float)((double)norm + sqrt(px * px + py * py));
+    }
+    return norm;
+}
 float oracle_motion_maxabs(const float *u, int n) {
     return motion_maxabs((const v2 *)u, (unsigned)n);
 }

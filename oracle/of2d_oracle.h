@@ -58,6 +58,7 @@ int oracle_hs_loop(float *u, const float *dI, const float *It, int dimx, int dim
 int oracle_hs_loop_mt(float *u, const float *dI, const float *It, int dimx, int dimy,
                       float alpha, int niter, int nthreads, float *errs);
 float oracle_motion_norm(const float *u, int n);
+float oracle_motion_norm_sum(const float *u, int n);
 float oracle_motion_maxabs(const float *u, int n);
 void oracle_warp2d(float *I, const float *u, int dimx, int dimy);
 void oracle_accumulate(float *u, const float *v, int dimx, int dimy);

@@ -66,6 +66,7 @@ def lib():
             "oracle_hs_loop": (i, [_f32p, _f32p, _f32p, i, i, f, i, i, _f32p]),
             "oracle_hs_loop_mt": (i, [_f32p, _f32p, _f32p, i, i, f, i, i, _f32p]),
             "oracle_motion_norm": (f, [_f32p, i]),
+            "oracle_motion_norm_sum": (f, [_f32p, i]),
             "oracle_motion_maxabs": (f, [_f32p, i]),
             "oracle_warp2d": (None, [_f32p, _f32p, i, i]),
             "oracle_accumulate": (None, [_f32p, _f32p, i, i]),

@@ -6,8 +6,10 @@ where the reference stops — the break test `err < 0.001f && iter > 1`
 Expected values are golden fixtures of the oracle (tests/golden/
 make_convergence.py; the oracle is pinned to the reference's known answers in
 reference_known_answers.json), so the 4096^2 cases need no CPU run here.  The
-"exact_norms" record of each fixture is the oracle with the Logger norms
-summed in double (oracle_set_logger_fp64), which the GPU follows.
+top-level records are the reference's semantics (Motion::norm's float running
+sums, Motion.cpp:42-49); the "exact_norms" record of each fixture is the
+oracle with the Logger norms summed in double (oracle_set_logger_fp64), which
+the library's opt-in `logger_fp64` mode follows.
 """
 import hashlib
 import json
@@ -40,34 +42,47 @@ def inputs(fx):
     return S.procedural_pair(n, 0, n)
 
 
-# GPU Logger errors against the oracle's exactly summed ones (fp64 sums of the
-# same magnitudes): the GPU adds fp32 magnitudes per lane (<= 72 terms) and
-# fp64 from there on, ~1e-7 relative
-EXACT_RTOL = 1e-5
+def run(fx, **opts):
+    ref, mov = inputs(fx)
+    n = fx["n"]
+    with ImageRegistration((n, n), fx["niter"], 0, fx["reg"], [fx["alpha"]], **opts) as r:
+        r.register(ref, mov)
+        return r.iterations(), r.motion(), r.last_errors()
 
 
 @pytest.mark.parametrize("name", ["hs_texture1024", "hs_texture4096", "hs_procedural4096"])
-def test_default_semantics_break_and_motion(gpu, name):
-    """The GPU computes the Logger's norms without the reference's fp32
-    running-sum rounding (Motion.cpp:42-49 adds each of the N magnitudes to a
-    FLOAT sum), so it breaks where the exactly summed error crosses 0.001:
-      1024^2 texture     reference 103, exact 103 (the sums agree to 3e-5)
-      4096^2 texture     reference 102, exact 107 (the float sums are 2-6 %
-                         off: at 16.7 M terms each addition rounds at ~1 ulp
-                         of the running sum)
-      4096^2 procedural  reference 397, exact 389
-    — a deliberate deviation.  Bar: the exact-norm break
-    iteration, the oracle's motion at that iteration bit for bit, errors within
-    EXACT_RTOL, and a threshold margin far outside that tolerance."""
+def test_reference_break_and_motion(gpu, name):
+    """The Logger norms are the reference's float running sums (seqnorm), so
+    the loop breaks on the reference's iteration at every size:
+      1024^2 texture     103
+      4096^2 texture     102 (the exactly summed error would break at 107)
+      4096^2 procedural  397 (exactly summed: 389)
+    Bar: the iteration count, the motion bit for bit, and every iteration's
+    error bit for bit (the float32 values of Logger::error)."""
+    fx = fixture(name)
+    it, m, errs = run(fx)
+    assert it == fx["iterations_executed"]
+    assert digest(m) == fx["motion_sha256_f32_planar"]
+    want = np.asarray(fx["errors"], np.float32)
+    assert errs.view(np.uint32).tolist() == want.view(np.uint32).tolist()
+
+
+# GPU Logger errors in the fp64 mode against the oracle's exactly summed ones
+# (fp64 sums of the same magnitudes): the GPU adds fp32 magnitudes per lane
+# (<= 72 terms) and fp64 from there on, ~1e-7 relative
+EXACT_RTOL = 1e-5
+
+
+@pytest.mark.parametrize("name", ["hs_texture4096", "hs_procedural4096"])
+def test_fp64_logger_mode(gpu, name):
+    """Opt-in `logger_fp64`: the fused three-iteration kernels stay on and the
+    norms are fp64 sums, so the break falls where the exactly summed error
+    crosses 0.001 (107 / 389 at 4096^2).  Bar: that iteration, the oracle's
+    motion at it bit for bit, errors within EXACT_RTOL, and a threshold margin
+    far outside that tolerance."""
     fx = fixture(name)
     ex = fx["exact_norms"]
-    ref, mov = inputs(fx)
-    n = fx["n"]
-    with ImageRegistration((n, n), fx["niter"], 0, fx["reg"], [fx["alpha"]]) as r:
-        r.register(ref, mov)
-        it = r.iterations()
-        m = r.motion()
-        errs = r.last_errors()
+    it, m, errs = run(fx, logger_fp64=1)
     assert it == ex["iterations_executed"]
     assert digest(m) == ex["motion_sha256_f32_planar"]
     want = np.asarray(ex["errors"], np.float64)
@@ -76,9 +91,3 @@ def test_default_semantics_break_and_motion(gpu, name):
     assert want[k] < 0.001 <= want[k - 1]
     margin = min(abs(want[k] - 0.001), abs(want[k - 1] - 0.001)) / 0.001
     assert margin > 10 * EXACT_RTOL, margin
-    if name == "hs_texture1024":
-        # here the reference's float sums stay within 3e-5 of the exact ones:
-        # the reference's own break and motion
-        assert fx["iterations_executed"] == it
-        assert fx["motion_sha256_f32_planar"] == ex["motion_sha256_f32_planar"]
-        np.testing.assert_allclose(errs[2:], np.asarray(fx["errors"])[2:], rtol=1e-4)

@@ -1,0 +1,116 @@
+"""The Logger's norms on the MI355X, bit for bit against the reference's
+float running sum (src/Motion.cpp:42-49 as Logger::update_error takes it,
+src/Logger.cpp:32-51): of2d_motion_norms against oracle_motion_norm_sum.
+
+Bar: the float32 bit patterns of both sums equal.  Cases cover the walk's
+branches: ragged tiles and odd widths, a leading run of zero magnitudes (the
+sum stays 0 across tiles), magnitudes that tie on every term once the sum's
+ulp is 2 (a constant field of unit vectors past 2^24 terms), sums past 2^24
+terms where the float sum saturates far below the exact one, tiny magnitudes
+(the sum starts below 2^-100), NaN and infinite magnitudes.
+"""
+import numpy as np
+import pytest
+
+from opticalflow2d_amd.registration import motion_norms
+
+pytestmark = pytest.mark.gpu
+
+
+def oracle_sums(oracle, cur, prev):
+    L = oracle.lib()
+    n = cur.size // 2
+    diff = np.ascontiguousarray((cur - prev).astype(np.float32).reshape(-1))
+    p = np.ascontiguousarray(prev.astype(np.float32).reshape(-1))
+    return np.array([L.oracle_motion_norm_sum(diff, n), L.oracle_motion_norm_sum(p, n)],
+                     np.float32)
+
+
+def check(oracle, cur, prev, dims):
+    cur = np.asarray(cur, np.float32).reshape(-1, 2)
+    prev = np.asarray(prev, np.float32).reshape(-1, 2)
+    got, res = motion_norms(cur, prev, dims)
+    want = oracle_sums(oracle, cur, prev)
+    nan = np.isnan(want)
+    assert np.array_equal(np.isnan(got), nan), (got, want)  # NaN payloads may differ
+    assert got[~nan].view(np.uint32).tolist() == want[~nan].view(np.uint32).tolist(), \
+        (got, want, res)
+    return res
+
+
+@pytest.mark.parametrize("dims", [(1, 1), (3, 5), (7, 1), (1, 9), (64, 64), (255, 257),
+                                  (4096, 1), (1000, 1000), (1024, 4097)])
+def test_random_fields(gpu, oracle, dims):
+    rng = np.random.default_rng(sum(dims))
+    n = dims[0] * dims[1]
+    prev = rng.normal(0, 1.5, (n, 2)).astype(np.float32)
+    cur = prev + rng.normal(0, 1e-3, (n, 2)).astype(np.float32)
+    check(oracle, cur, prev, dims)
+
+
+def test_config_scale_4096(gpu, oracle):
+    """16.7 M terms: the float sum drifts a few % from the exact one."""
+    rng = np.random.default_rng(7)
+    n = 4096 * 4096
+    prev = rng.normal(0, 1.0, (n, 2)).astype(np.float32)
+    cur = prev * np.float32(1.001) + rng.normal(0, 1e-4, (n, 2)).astype(np.float32)
+    res = check(oracle, cur, prev, (4096, 4096))
+    # a cost figure, not a result: the prediction should leave few tiles to resolve
+    assert res.max() < 200, res
+
+
+def test_past_2_24_terms_saturates(gpu, oracle):
+    """5000 x 4000 terms of magnitude ~1: past 2^24 the float sum's ulp
+    exceeds the terms and the reference's sum stalls."""
+    rng = np.random.default_rng(3)
+    n = 5000 * 4000
+    prev = rng.uniform(0.5, 1.5, (n, 2)).astype(np.float32)
+    cur = prev + rng.uniform(-1e-2, 1e-2, (n, 2)).astype(np.float32)
+    check(oracle, cur, prev, (5000, 4000))
+
+
+def test_ties_every_term(gpu, oracle):
+    """|(1, 0)| = 1 on every pixel: from S = 2^24 on each addition is an exact
+    tie (half an ulp), rounded to even."""
+    n = 4500 * 4000
+    prev = np.zeros((n, 2), np.float32)
+    prev[:, 0] = 1.0
+    cur = prev.copy()
+    cur[::3, 1] = 0.75
+    check(oracle, cur, prev, (4500, 4000))
+
+
+def test_leading_zeros_and_tiny(gpu, oracle):
+    rng = np.random.default_rng(11)
+    dims = (3000, 200)
+    n = dims[0] * dims[1]
+    prev = rng.normal(0, 1, (n, 2)).astype(np.float32)
+    prev[: 50 * 3000] = 0.0          # 37 zero tiles before anything
+    prev[50 * 3000: 50 * 3000 + 7] = np.float32(1e-38)  # sum below 2^-100, then tiny steps
+    prev[50 * 3000 + 7: 50 * 3000 + 9] = np.float32(1e-45)  # denormal components
+    cur = prev.copy()
+    cur[: 60 * 3000] = 0.0
+    check(oracle, cur, prev, dims)
+
+
+def test_all_zero(gpu, oracle):
+    z = np.zeros((640 * 480, 2), np.float32)
+    check(oracle, z, z, (640, 480))
+
+
+@pytest.mark.parametrize("special", ["nan", "inf", "overflow"])
+def test_nonfinite(gpu, oracle, special):
+    rng = np.random.default_rng(5)
+    dims = (2048, 300)
+    n = dims[0] * dims[1]
+    prev = rng.normal(0, 1, (n, 2)).astype(np.float32)
+    cur = prev + np.float32(0.01)
+    k = n // 3
+    if special == "nan":
+        prev[k, 1] = np.nan
+    elif special == "inf":
+        cur[k, 0] = np.inf
+        prev[2 * k, 0] = np.inf
+    else:  # magnitudes near FLT_MAX: the float sum overflows to inf
+        prev[k: k + 5] = np.float32(3e38)
+    check(oracle, cur, prev, dims)
