@@ -191,13 +191,17 @@ int of2d_slab_create_local(of2d_slab **out, int dimx, int dimy, float alpha, int
 /* ---- kernel-level test entry: the Logger's norms ----
  * Motion::norm (src/Motion.cpp:42-49) as Logger::update_error (src/Logger.cpp:
  * 32-51) takes it: the float running sums, in linear order, of
- * sqrt((double)x^2 + (double)y^2) over (cur - prev) -> sums[0] and over prev
- * -> sums[1] (not divided by dimx*dimy), bit-identical to the reference's.
- * cur / prev: host float [dimx*dimy*2], interleaved x, y per pixel (coord2d),
- * idx = i + j*dimx.  resolves (optional, int[2]): tiles of 4096 terms the
- * device walk had to resolve term by term (a cost figure, not a result). */
-int of2d_motion_norms(const float *cur, const float *prev, int dimx, int dimy, float *sums,
-                      int *resolves);
+ * sqrt((double)x^2 + (double)y^2) over (cur - prev) -> sums[2k] and over prev
+ * -> sums[2k+1] (not divided by dimx*dimy), bit-identical to the reference's.
+ * cur / prev: npairs host fields of float [dimx*dimy*2] each, interleaved x, y
+ * per pixel (coord2d), idx = i + j*dimx; the pairs run in order on one
+ * workspace, so pair k's walk predicts pair k+1's, as in a Logger loop.
+ * stats (optional, int[8*npairs], cost figures, not results): per pair the
+ * tiles the device walk resolved below tile level (|cur - prev|, |prev|), the
+ * 64-term segments it stepped term by term (same order), the tiles whose
+ * entries were recomputed, 0, 0, 0. */
+int of2d_motion_norms(const float *cur, const float *prev, int dimx, int dimy, int npairs,
+                      float *sums, int *stats);
 
 /* ---- library info ---- */
 const char *of2d_version(void);

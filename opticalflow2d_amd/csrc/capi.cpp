@@ -154,31 +154,33 @@ int of2d_set_option(of2d_ctx *ctx, const char *key, double value) {
     return guarded(ctx->err, [&] { ctx->reg->set_option(key, value); });
 }
 
-int of2d_motion_norms(const float *cur, const float *prev, int dimx, int dimy, float *sums,
-                      int *resolves) {
-    if (!cur || !prev || !sums || dimx <= 0 || dimy <= 0) return OF2D_ERR_INVALID_ARGUMENT;
+int of2d_motion_norms(const float *cur, const float *prev, int dimx, int dimy, int npairs,
+                      float *sums, int *stats) {
+    if (!cur || !prev || !sums || dimx <= 0 || dimy <= 0 || npairs <= 0)
+        return OF2D_ERR_INVALID_ARGUMENT;
     std::string err;
     int rc = guarded(err, [&] {
         of2d::Field<float2> c, p;
         c.alloc(dimx, dimy);
         p.alloc(dimx, dimy);
+        const size_t n = (size_t)dimx * dimy * 2;
         const size_t row = (size_t)dimx * sizeof(float2), pitch = (size_t)c.P * sizeof(float2);
-        OF2D_HIP(hipMemcpy2D(c.p, pitch, cur, row, row, dimy, hipMemcpyHostToDevice));
-        OF2D_HIP(hipMemcpy2D(p.p, pitch, prev, row, row, dimy, hipMemcpyHostToDevice));
         of2d::DevArray<unsigned char> ws;
         ws.alloc(of2d::seqnorm_workspace_bytes(dimx, dimy));
         of2d::DevArray<float> out;
-        out.alloc(2);
+        out.alloc(2 * (size_t)npairs);
         of2d::DevArray<int> dbg;
-        dbg.alloc(2);
-        of2d::launch_seqnorm(c.p, p.p, dimx, dimy, c.P, ws.p, out.p, dbg.p, nullptr);
-        OF2D_HIP(hipMemcpy(sums, out.p, 2 * sizeof(float), hipMemcpyDeviceToHost));
-        int r[2];
-        OF2D_HIP(hipMemcpy(r, dbg.p, sizeof r, hipMemcpyDeviceToHost));
-        if (resolves) {
-            resolves[0] = r[0];
-            resolves[1] = r[1];
+        dbg.alloc(8 * (size_t)npairs);
+        for (int k = 0; k < npairs; k++) {
+            // one workspace: each pair's walk predicts the next (its profile)
+            OF2D_HIP(hipMemcpy2D(c.p, pitch, cur + k * n, row, row, dimy, hipMemcpyHostToDevice));
+            OF2D_HIP(hipMemcpy2D(p.p, pitch, prev + k * n, row, row, dimy, hipMemcpyHostToDevice));
+            of2d::launch_seqnorm(c.p, p.p, dimx, dimy, c.P, ws.p, k > 0, out.p + 2 * k,
+                                 dbg.p + 8 * k, nullptr);
         }
+        OF2D_HIP(hipMemcpy(sums, out.p, 2 * sizeof(float) * npairs, hipMemcpyDeviceToHost));
+        if (stats)
+            OF2D_HIP(hipMemcpy(stats, dbg.p, 8 * sizeof(int) * npairs, hipMemcpyDeviceToHost));
     });
     if (rc != OF2D_OK) g_gateway_err = err;
     return rc;

@@ -201,12 +201,23 @@ struct PartialRuns {
 // running sum S <- (float)((double)S + sqrt((double)x^2 + (double)y^2)) over
 // the pixels in linear order, of |cur - prev| (out[0]) and |prev| (out[1])
 // (Logger::update_error, src/Logger.cpp:32-51; seqnorm_kernels.hip).  out[]
-// holds the sums, not yet divided by N.  ws: seqnorm_workspace_bytes; dbg
-// (optional): tiles the walk resolved from their magnitudes, per norm.
+// holds the sums, not yet divided by N.  ws: seqnorm_workspace_bytes; it also
+// keeps each call's running-sum profile, which the next call on the same grid
+// uses as its prediction when use_profile is set (the result is exact either
+// way; a poor prediction costs time).  dbg (optional): tiles the walk had to
+// resolve below tile level, per norm.
 constexpr int kSnTile = 4096;  // consecutive terms per tile
 size_t seqnorm_workspace_bytes(int dimx, int dimy);
 void launch_seqnorm(const float2 *cur, const float2 *prev, int dimx, int dimy, int P, void *ws,
-                    float *out, int *dbg, hipStream_t st);
+                    bool use_profile, float *out, int *dbg, hipStream_t st);
+// the two halves of launch_seqnorm: the bandwidth passes (tables) and the
+// latency-bound walk, so that a pipeline can run them on separate streams
+// (the walk reads what tables wrote; tables reads the profile the last walk
+// on the same workspace wrote)
+void launch_seqnorm_tables(const float2 *cur, const float2 *prev, int dimx, int dimy, int P,
+                           void *ws, bool use_profile, hipStream_t st);
+void launch_seqnorm_walk(const float2 *cur, const float2 *prev, int dimx, int dimy, int P,
+                         void *ws, float *out, int *dbg, hipStream_t st);
 
 // ---------------------------------------------------------------- fields
 void launch_d2f(const double *in, int dimx, int dimy, float *out, int P, int row_offset,

@@ -116,7 +116,7 @@ struct Level {
     Field<float2> motion[2];
     int mcur = 0;
     Field<float2> dI;
-    Field<float2> est[3];
+    Field<float2> est[5];  // [3], [4]: only for the exact-norm loop's ring
     Field<float2> force, velocity, increment, corr, tmp;
     DevArray<double> cbuf[2];              // Curvature: two x|y double plane pairs (pitch P)
     DevArray<double> cC1T, cC0, cD1T, cD0;  // Curvature: REDFT10 / REDFT01 matrices
@@ -177,9 +177,17 @@ class Registration {
     bool logger_fp64_ = false;
     bool exact_norms() const { return !fixed_ && !logger_fp64_; }
     // enqueue the exact norms of one Logger update into d_seq_[2t], [2t + 1]
+    // (synchronous loops: Elastic, Fluid; workspace 0, on st_)
     void seqnorm(const Level &L, const float2 *cur, const float2 *prev, int t);
-    DevArray<unsigned char> d_seqws_;  // seqnorm workspace (level 0 size)
-    DevArray<float> d_seq_;            // per-iteration exact sums of a chunk
+    // run_chunked with the reference's float norms: single steps into a ring
+    // of four buffers; each iteration's tables on sn_st_ and walk on wk_st_,
+    // alternating between two workspaces
+    int run_chunked_exact(Level &L, int niter, int nb, const StepFn &step, int &final_buf);
+    hipStream_t sn_st_ = nullptr, wk_st_ = nullptr;
+    hipEvent_t ev_step_[4] = {}, ev_fix_[4] = {}, ev_walk_[4] = {};
+    DevArray<unsigned char> d_seqws_[2];  // seqnorm workspaces (level 0 size)
+    DevArray<float> d_seq_;               // per-iteration exact sums of a chunk
+    int seq_dx_[2] = {0, 0}, seq_dy_[2] = {0, 0};  // grid of each workspace's last call
     int chunk_ = 33;  // eleven fused triples per chunk
     int gi_ = -1;     // triple kernel: dI from Iaux (1), from dI (0), by size (-1)
     int device_ = -1;

@@ -144,6 +144,13 @@ Registration::~Registration() {
     if (ev_fork_) (void)hipEventDestroy(ev_fork_);
     if (ev_join_) (void)hipEventDestroy(ev_join_);
     if (side_st_) (void)hipStreamDestroy(side_st_);
+    if (sn_st_) (void)hipStreamDestroy(sn_st_);
+    if (wk_st_) (void)hipStreamDestroy(wk_st_);
+    for (int k = 0; k < 4; k++) {
+        if (ev_step_[k]) (void)hipEventDestroy(ev_step_[k]);
+        if (ev_fix_[k]) (void)hipEventDestroy(ev_fix_[k]);
+        if (ev_walk_[k]) (void)hipEventDestroy(ev_walk_[k]);
+    }
     if (st_) (void)hipStreamDestroy(st_);
 }
 
@@ -170,6 +177,13 @@ void Registration::ensure_device() {
     if (device_ >= 0) OF2D_HIP(hipSetDevice(device_));
     OF2D_HIP(hipStreamCreateWithFlags(&st_, hipStreamNonBlocking));
     OF2D_HIP(hipStreamCreateWithFlags(&side_st_, hipStreamNonBlocking));
+    OF2D_HIP(hipStreamCreateWithFlags(&sn_st_, hipStreamNonBlocking));
+    OF2D_HIP(hipStreamCreateWithFlags(&wk_st_, hipStreamNonBlocking));
+    for (int k = 0; k < 4; k++) {
+        OF2D_HIP(hipEventCreateWithFlags(&ev_step_[k], hipEventDisableTiming));
+        OF2D_HIP(hipEventCreateWithFlags(&ev_fix_[k], hipEventDisableTiming));
+        OF2D_HIP(hipEventCreateWithFlags(&ev_walk_[k], hipEventDisableTiming));
+    }
     OF2D_HIP(hipEventCreateWithFlags(&ev_fork_, hipEventDisableTiming));
     OF2D_HIP(hipEventCreateWithFlags(&ev_join_, hipEventDisableTiming));
     lv_.resize(nscales_ + 1);
@@ -200,7 +214,7 @@ void Registration::ensure_device() {
     OF2D_HIP(hipMalloc(&d_scalar_, (16 + 256) * sizeof(float)));
     OF2D_HIP(hipDeviceSynchronize());  // null-stream memset vs the non-blocking stream
     hs_.ensure(std::max(chunk_, 64));
-    d_seqws_.alloc(seqnorm_workspace_bytes(dimx_, dimy_));
+    for (auto &w : d_seqws_) w.alloc(seqnorm_workspace_bytes(dimx_, dimy_));
     d_seq_.alloc(2 * (size_t)std::max(chunk_, 64));
     ready_ = true;
 }
@@ -287,7 +301,82 @@ void Registration::estimate_level(int s) {
 }
 
 void Registration::seqnorm(const Level &L, const float2 *cur, const float2 *prev, int t) {
-    launch_seqnorm(cur, prev, L.dx, L.dy, L.P, d_seqws_.p, d_seq_.p + 2 * (size_t)t, nullptr, st_);
+    // the profile of the last call predicts this one when it was on the same grid
+    const bool use_prof = seq_dx_[0] == L.dx && seq_dy_[0] == L.dy;
+    seq_dx_[0] = L.dx;
+    seq_dy_[0] = L.dy;
+    launch_seqnorm(cur, prev, L.dx, L.dy, L.P, d_seqws_[0].p, use_prof, d_seq_.p + 2 * (size_t)t,
+                   nullptr, st_);
+}
+
+// The chunked loop of run_chunked with the reference's float norms.  Every
+// iterate must be in memory for its norms, so the iterations run as single
+// steps into a ring of the four buffers other than the chunk's start buffer a
+// (kept for a replay).  The norms of iteration t run behind step t on two
+// streams: the bandwidth passes (seqnorm tables, sn_st_) and the
+// latency-bound walk (wk_st_), on workspace t mod 2, whose last walk (t - 2)
+// also predicts them (its profile).  Step t + 4 reuses t's buffer and waits
+// for the walk of t + 1, the last reader of t's iterate.
+int Registration::run_chunked_exact(Level &L, int niter, int nb, const StepFn &step,
+                                    int &final_buf) {
+    const double npx = (double)L.dx * L.dy;
+    last_err_.clear();
+    for (int b = 3; b < 5; b++)
+        if (!L.est[b].p) L.est[b].alloc(L.dx, L.dy);
+    auto ring = [](int a, int t) {  // the (t mod 4)-th buffer other than a
+        const int i = t & 3;
+        return i < a ? i : i + 1;
+    };
+    auto src_of = [&](int a, int t) { return t == 0 ? a : ring(a, t - 1); };
+    // a new loop: its first two calls per workspace start from a fresh state
+    bool walked[2] = {false, false};
+    int a = 0, k0 = 0;
+    while (k0 < niter) {
+        const int C = std::min(chunk_, niter - k0);
+        for (int t = 0; t < C; t++) {
+            const int src = src_of(a, t), dst = ring(a, t), w = (k0 + t) & 1;
+            if (t >= 4) OF2D_HIP(hipStreamWaitEvent(st_, ev_walk_[(t - 3) & 3], 0));
+            step(L.est[src].p, L.est[dst].p, d_partial_ + (size_t)t * nb * 2);
+            OF2D_HIP(hipEventRecord(ev_step_[t & 3], st_));
+            OF2D_HIP(hipStreamWaitEvent(sn_st_, ev_step_[t & 3], 0));
+            // workspace w: the walk two iterations back has read it and left
+            // its profile (wk_st_ runs the walks in order)
+            if (t >= 2) OF2D_HIP(hipStreamWaitEvent(sn_st_, ev_walk_[(t - 2) & 3], 0));
+            const bool use_prof = walked[w] && seq_dx_[w] == L.dx && seq_dy_[w] == L.dy;
+            seq_dx_[w] = L.dx;
+            seq_dy_[w] = L.dy;
+            walked[w] = true;
+            launch_seqnorm_tables(L.est[dst].p, L.est[src].p, L.dx, L.dy, L.P, d_seqws_[w].p,
+                                  use_prof, sn_st_);
+            OF2D_HIP(hipEventRecord(ev_fix_[t & 3], sn_st_));
+            OF2D_HIP(hipStreamWaitEvent(wk_st_, ev_fix_[t & 3], 0));
+            launch_seqnorm_walk(L.est[dst].p, L.est[src].p, L.dx, L.dy, L.P, d_seqws_[w].p,
+                                d_seq_.p + 2 * (size_t)t, nullptr, wk_st_);
+            OF2D_HIP(hipEventRecord(ev_walk_[t & 3], wk_st_));
+        }
+        OF2D_HIP(hipStreamWaitEvent(st_, ev_walk_[(C - 1) & 3], 0));
+        OF2D_HIP(hipMemcpyAsync(hs_.flt, d_seq_.p, sizeof(float) * 2 * C, hipMemcpyDeviceToHost,
+                                st_));
+        check_status();  // synchronises st_ (and with it every norm of the chunk)
+        for (int t = 0; t < C; t++) {
+            const int k = k0 + t;
+            const float err = logger_error(hs_.flt[2 * t], hs_.flt[2 * t + 1], npx);
+            last_err_.push_back(err);
+            if (verbose_) print("Iteration: %d\tError:%.4f\n", k, (double)err);
+            if (err < 0.001f && k > 1) {  // ImageRegistrationOpticalFlow.cpp:131-134
+                // iteration t's buffer was reused by iteration t + 4: replay
+                if (t + 4 <= C - 1)
+                    for (int r = 0; r <= t; r++)
+                        step(L.est[src_of(a, r)].p, L.est[ring(a, r)].p, d_partial_);
+                final_buf = ring(a, t);
+                return k + 1;
+            }
+        }
+        a = ring(a, C - 1);
+        k0 += C;
+    }
+    final_buf = a;
+    return niter;
 }
 
 // Speculative chunked iteration loop shared by every solver whose iteration
@@ -301,16 +390,14 @@ void Registration::seqnorm(const Level &L, const float2 *cur, const float2 *prev
 // src_of(a, t) and writes dst_of(a, t)).
 int Registration::run_chunked(Level &L, int niter, int nb, const StepFn &step, int &final_buf,
                               const StepFn2 &step2, const StepFn3 &step3, const int *nblk) {
+    if (exact_norms()) return run_chunked_exact(L, niter, nb, step, final_buf);
     const double npx = (double)L.dx * L.dy;
     last_err_.clear();
     if (fixed_ && d_all_.n < 2 * (size_t)niter) {
         d_all_.alloc(2 * (size_t)niter);
         hs_.ensure((niter + 1) / 2);  // 4 doubles per unit of capacity
     }
-    // the reference's float norms need every iterate in memory: single steps,
-    // each followed by its seqnorm
-    const bool exact = exact_norms();
-    const bool use2 = step2 && !exact, use3 = step3 && !exact;
+    const bool use2 = bool(step2), use3 = bool(step3);
     int a = 0, k0 = 0;
     auto src_of = [](int a_, int t) { return t == 0 ? a_ : (t % 2 == 1 ? (a_ + 1) % 3 : (a_ + 2) % 3); };
     auto dst_of = [](int a_, int t) { return t % 2 == 0 ? (a_ + 1) % 3 : (a_ + 2) % 3; };
@@ -343,10 +430,7 @@ int Registration::run_chunked(Level &L, int niter, int nb, const StepFn &step, i
             }
             end = cur;
         } else {
-            for (int t = 0; t < C; t++) {
-                step(L.est[src_of(a, t)].p, L.est[dst_of(a, t)].p, part(t));
-                if (exact) seqnorm(L, L.est[dst_of(a, t)].p, L.est[src_of(a, t)].p, t);
-            }
+            for (int t = 0; t < C; t++) step(L.est[src_of(a, t)].p, L.est[dst_of(a, t)].p, part(t));
             runs.add(0, C, nblk ? nblk[0] : nb);
         }
         if (fixed_) {
@@ -357,19 +441,13 @@ int Registration::run_chunked(Level &L, int niter, int nb, const StepFn &step, i
             k0 += C;
             continue;
         }
-        if (exact) {
-            OF2D_HIP(hipMemcpyAsync(hs_.flt, d_seq_.p, sizeof(float) * 2 * C,
-                                    hipMemcpyDeviceToHost, st_));
-        } else {
-            runs.reduce(d_partial_, nb, d_sums_, st_);
-            OF2D_HIP(hipMemcpyAsync(hs_.sums, d_sums_, sizeof(double) * 2 * C,
-                                    hipMemcpyDeviceToHost, st_));
-        }
+        runs.reduce(d_partial_, nb, d_sums_, st_);
+        OF2D_HIP(hipMemcpyAsync(hs_.sums, d_sums_, sizeof(double) * 2 * C, hipMemcpyDeviceToHost,
+                                st_));
         check_status();  // synchronises the stream; throws the reference's runtime_error
         for (int t = 0; t < C; t++) {
             const int k = k0 + t;
-            const float err = exact ? logger_error(hs_.flt[2 * t], hs_.flt[2 * t + 1], npx)
-                                    : logger_error(hs_.sums[2 * t], hs_.sums[2 * t + 1], npx);
+            const float err = logger_error(hs_.sums[2 * t], hs_.sums[2 * t + 1], npx);
             last_err_.push_back(err);
             if (verbose_) print("Iteration: %d\tError:%.4f\n", k, (double)err);
             if (!fixed_ && err < 0.001f && k > 1) {  // ImageRegistrationOpticalFlow.cpp:131-134

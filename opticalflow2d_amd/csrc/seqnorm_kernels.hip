@@ -20,25 +20,33 @@
 // depends on the parity of M).  So while M plus the running sum of m_k(e)
 // stays <= 2^24 - 1 (no binade crossing) and no tie occurs, S after a run of
 // terms is (M + sum m_k(e)) u exactly: an integer prefix sum.  Crossings (a
-// few dozen per norm: S doubles between them) and ties are stepped one term
-// at a time with the reference's own two roundings.
+// few dozen per norm: S doubles between them) are stepped one term at a time
+// with the reference's own two roundings; inside the walk's term-level scans
+// ties are composed exactly (a run of terms is M -> M + (M even ? a : b)).
 //
 // Pipeline for the pair of norms of one Logger update (|cur - prev| and
-// |prev|), in tiles of kSnTile consecutive terms:
-//   seqnorm_tile_sums    fp64 sum of each tile's magnitudes (a prediction)
-//   seqnorm_candidates   fp64 prefix over the tiles -> per tile the <= 4
-//                        binades the running sum can lie in across the tile
-//   seqnorm_tables       per tile and candidate binade: sum of m_k(e) and a
-//                        tie / NaN flag
-//   seqnorm_walk         one block per norm walks the tiles in order, 1024
-//                        tiles per step (saturating block scan of their table
-//                        entries for the current binade); a tile whose entry
-//                        does not apply (a crossing, a tie, a binade outside
-//                        its candidates) is resolved from its magnitudes.
-// The prediction only decides how much resolving is needed: the walk's result
-// is the reference's float sum whatever it predicted.
+// |prev|), in tiles of kSnTile consecutive terms, segments of 64:
+//   seqnorm_tables<true>   one pass over cur / prev: fp64 tile sums, the
+//                          nonzero-segment masks, and per candidate binade
+//                          (predicted from the previous update's exact
+//                          running sums, the "profile") the ulp sums of each
+//                          segment and of the tile
+//   seqnorm_check          fp64 prefix over the tiles -> the binades the float
+//                          sum can be in across each tile (the fp64 sum +-1/8);
+//                          tiles whose candidates miss one are marked pending
+//   seqnorm_tables<false>  the pending tiles again, with those binades
+//   seqnorm_walk           one wave per norm walks the tiles in order, 64 per
+//                          step (saturating wave scan of their entries for the
+//                          current binade); at a tile whose entry does not
+//                          apply (a crossing, a tie, a binade outside its
+//                          candidates) it scans the tile's segment entries,
+//                          and the one segment that holds the crossing term by
+//                          term.  It writes the profile of the next update.
+// Predictions only decide how much work the walk and the pending pass do: the
+// walk's result is the reference's float sum whatever they predicted.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 
 #include "of2d_device.h"
@@ -46,20 +54,23 @@
 namespace of2d {
 namespace {
 
-constexpr int kSnThreads = 256;        // tile kernels
-constexpr int kSnPerThread = kSnTile / kSnThreads;
-constexpr int kSnWalk = 1024;          // walk block: tiles per step, terms / 4 per resolve
-constexpr int kSnTerms = kSnTile / kSnWalk;
-constexpr int kSnCand = 4;            // candidate binades per tile
-constexpr int kSnEmin = -100;          // below 2^-100 the sum is "low": stepped per nonzero term
+constexpr int kSnThreads = 256;                 // table kernels: 4 waves
+constexpr int kSnSegs = kSnTile / 64;           // 64-term segments per tile
+constexpr int kSnRounds = kSnSegs / (kSnThreads / 64);
+constexpr int kSnCand = 4;                      // candidate binades per tile and norm
+constexpr int kSnScan = 1024;                   // seqnorm_check block
+constexpr int kSnEmin = -100;  // below 2^-100 the sum is "low": stepped per nonzero term
 constexpr int kSnLow = -1000;
 constexpr int kSnNonfinite = 1000;
 constexpr unsigned kSnSat = 1u << 25;           // saturated sum of m: certainly a crossing
 constexpr unsigned kSnLimit = (1u << 24) - 1u;  // largest M + sum that stays in the binade
 constexpr unsigned kSnBad = 1u << 31;           // table entry: a tie or NaN among the terms
-// header word of a tile / norm (seqnorm_candidates)
-constexpr unsigned kHdrZero = 1u << 30;  // every magnitude of the tile is 0: a no-op
-constexpr unsigned kHdrNan = 1u << 29;   // a NaN magnitude
+// header word of a tile / norm
+constexpr unsigned kHdrZero = 1u << 30;     // every magnitude of the tile is 0: a no-op
+constexpr unsigned kHdrNan = 1u << 29;      // a NaN magnitude
+constexpr unsigned kHdrPending = 1u << 28;  // candidates changed: tile entries to recompute
+constexpr unsigned kHdrSegReq = 1u << 27;   // segment entries requested (seqnorm_check)
+constexpr unsigned kHdrSeg = 1u << 26;      // segment entries valid for the candidates
 __host__ __device__ constexpr unsigned hdr_pack(int elo, int nc) {
     return (unsigned)(elo + 512) | ((unsigned)nc << 16);
 }
@@ -76,7 +87,7 @@ __device__ __forceinline__ int sn_region(float S) {
 __device__ __forceinline__ unsigned sn_mant(float S) {
     return (__float_as_uint(S) & 0x7fffffu) | 0x800000u;
 }
-// the float (M + s) ulps in binade e, M + s <= kSnLimit
+// the float M ulps in binade e, 2^23 <= M <= kSnLimit
 __device__ __forceinline__ float sn_make(int e, unsigned M) {
     return __uint_as_float(((unsigned)(e + 127) << 23) | (M - 0x800000u));
 }
@@ -89,6 +100,9 @@ __device__ __forceinline__ unsigned sn_sat(unsigned a, unsigned b) {
 __device__ __forceinline__ double sn_mag(float x, float y) {
     const double a = x, b = y;
     return sqrt(a * a + b * b);
+}
+__device__ __forceinline__ double sn_scale(int e) {
+    return __longlong_as_double((long long)(52 - e + 1023) << 52);
 }
 // ulps that (float)((double)S + d) adds to S = M 2^(e-23) while the result
 // stays in the binade; `bad` on a tie (parity-dependent) or NaN.  scale =
@@ -107,182 +121,12 @@ __device__ __forceinline__ unsigned sn_incr(double d, double scale, bool &bad) {
     bad |= (fr == 0.5);
     return (unsigned)m0 + (fr > 0.5 ? 1u : 0u);
 }
-__device__ __forceinline__ double sn_scale(int e) {
-    return __longlong_as_double((long long)(52 - e + 1023) << 52);
-}
 
-// The tile's terms of thread `tid`: kSnPerThread terms, strided by the block
-// (term t = r * kSnThreads + tid), so a wave reads 64 consecutive pixels.
-__device__ __forceinline__ void sn_tile_terms(const float2 *__restrict__ cur,
-                                              const float2 *__restrict__ prev, unsigned base,
-                                              unsigned N, int dimx, int P, double *dd,
-                                              double *dp) {
-    unsigned L = base + threadIdx.x;
-    unsigned j = L / (unsigned)dimx, i = L - j * (unsigned)dimx;
-#pragma unroll
-    for (int r = 0; r < kSnPerThread; r++) {
-        if (L < N) {
-            const size_t off = (size_t)j * (size_t)P + i;
-            const float2 c = cur[off], p = prev[off];
-            dd[r] = sn_mag(c.x - p.x, c.y - p.y);  // Field::operator- (Field.tpp:305-334)
-            dp[r] = sn_mag(p.x, p.y);
-        } else {
-            dd[r] = 0.0;
-            dp[r] = 0.0;
-        }
-        L += kSnThreads;
-        i += kSnThreads;
-        while (i >= (unsigned)dimx) {
-            i -= (unsigned)dimx;
-            j++;
-        }
-    }
-}
-
-template <class T, class Op>
-__device__ __forceinline__ T wave_reduce(T v, Op op) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = op(v, __shfl_xor(v, o, 64));
-    return v;
-}
-
-// ---------------------------------------------------------------- kernels
-__global__ __launch_bounds__(kSnThreads) void seqnorm_tile_sums(const float2 *__restrict__ cur,
-                                                               const float2 *__restrict__ prev,
-                                                               unsigned N, int dimx, int P,
-                                                               double *__restrict__ A) {
-    double dd[kSnPerThread], dp[kSnPerThread];
-    sn_tile_terms(cur, prev, blockIdx.x * (unsigned)kSnTile, N, dimx, P, dd, dp);
-    double sd = 0.0, sp = 0.0;
-#pragma unroll
-    for (int r = 0; r < kSnPerThread; r++) {
-        sd += dd[r];
-        sp += dp[r];
-    }
-    auto add = [](double a, double b) { return a + b; };
-    sd = wave_reduce(sd, add);
-    sp = wave_reduce(sp, add);
-    __shared__ double ws[2][kSnThreads / 64];
-    const int w = threadIdx.x / 64;
-    if ((threadIdx.x & 63) == 0) {
-        ws[0][w] = sd;
-        ws[1][w] = sp;
-    }
-    __syncthreads();
-    if (threadIdx.x < 2) {
-        double s = 0.0;
-        for (int k = 0; k < kSnThreads / 64; k++) s += ws[threadIdx.x][k];
-        A[2 * (size_t)blockIdx.x + threadIdx.x] = s;
-    }
-}
-
-// binade of a double bound, clamped to the float range
-__device__ __forceinline__ int sn_region_d(double v) {
-    if (!(v >= 0x1p-100)) return kSnLow;
-    if (v >= 0x1p127) return 127;
-    int ex;
-    (void)frexp(v, &ex);
-    return ex - 1;
-}
-
-__global__ __launch_bounds__(kSnWalk) void seqnorm_candidates(const double *__restrict__ A,
-                                                              unsigned ntiles,
-                                                              unsigned *__restrict__ H) {
-    const unsigned chunk = (ntiles + kSnWalk - 1) / kSnWalk;
-    const unsigned b0 = threadIdx.x * chunk;
-    const unsigned b1 = min(ntiles, b0 + chunk);
-    __shared__ double sh[2][kSnWalk];
-    for (int n = 0; n < 2; n++) {
-        double s = 0.0;
-        for (unsigned b = b0; b < b1; b++) s += A[2 * (size_t)b + n];
-        sh[n][threadIdx.x] = s;
-    }
-    __syncthreads();
-    // exclusive prefix of the chunk sums (Hillis-Steele on LDS; a prediction, any order)
-    for (int o = 1; o < kSnWalk; o <<= 1) {
-        double v0 = 0.0, v1 = 0.0;
-        if ((int)threadIdx.x >= o) {
-            v0 = sh[0][threadIdx.x - o];
-            v1 = sh[1][threadIdx.x - o];
-        }
-        __syncthreads();
-        sh[0][threadIdx.x] += v0;
-        sh[1][threadIdx.x] += v1;
-        __syncthreads();
-    }
-    for (int n = 0; n < 2; n++) {
-        double Pb = threadIdx.x ? sh[n][threadIdx.x - 1] : 0.0;
-        for (unsigned b = b0; b < b1; b++) {
-            const double a = A[2 * (size_t)b + n];
-            unsigned h;
-            if (a == 0.0) {
-                h = kHdrZero;
-            } else if (!(a < INFINITY) || !(Pb < INFINITY)) {
-                h = hdr_pack(0, 0) | (a != a ? kHdrNan : 0u);
-            } else {
-                // the float sum's drift from the fp64 one stays within a few %
-                // at the grid sizes the break test sees; 1/8 either side
-                const int ehi = sn_region_d((Pb + a) * 1.125);
-                int elo = sn_region_d(Pb * 0.875);
-                if (elo == kSnLow) elo = kSnEmin;
-                if (ehi == kSnLow) {
-                    h = hdr_pack(0, 0);
-                } else {
-                    if (ehi - elo + 1 > kSnCand) elo = ehi - kSnCand + 1;
-                    h = hdr_pack(elo, ehi - elo + 1);
-                }
-            }
-            H[2 * (size_t)b + n] = h;
-            Pb += a;
-        }
-    }
-}
-
-__global__ __launch_bounds__(kSnThreads) void seqnorm_tables(const float2 *__restrict__ cur,
-                                                            const float2 *__restrict__ prev,
-                                                            unsigned N, int dimx, int P,
-                                                            const unsigned *__restrict__ H,
-                                                            unsigned *__restrict__ T) {
-    const unsigned h0 = H[2 * (size_t)blockIdx.x], h1 = H[2 * (size_t)blockIdx.x + 1];
-    if (hdr_nc(h0) == 0 && hdr_nc(h1) == 0) return;
-    double dd[kSnPerThread], dp[kSnPerThread];
-    sn_tile_terms(cur, prev, blockIdx.x * (unsigned)kSnTile, N, dimx, P, dd, dp);
-    __shared__ unsigned ws[2][kSnCand][kSnThreads / 64];
-    const int w = threadIdx.x / 64;
-    auto sat = [](unsigned a, unsigned b) {
-        return ((a | b) & kSnBad) | sn_sat(a & ~kSnBad, b & ~kSnBad);
-    };
-    for (int n = 0; n < 2; n++) {
-        const unsigned h = n ? h1 : h0;
-        const int nc = hdr_nc(h), elo = hdr_elo(h);
-        for (int c = 0; c < nc; c++) {
-            const double scale = sn_scale(elo + c);
-            unsigned s = 0;
-            bool bad = false;
-#pragma unroll
-            for (int r = 0; r < kSnPerThread; r++)
-                s = sn_sat(s, sn_incr(n ? dp[r] : dd[r], scale, bad));
-            s = wave_reduce(s | (bad ? kSnBad : 0u), sat);
-            if ((threadIdx.x & 63) == 0) ws[n][c][w] = s;
-        }
-    }
-    __syncthreads();
-    if (threadIdx.x < 2 * kSnCand) {
-        const int n = threadIdx.x / kSnCand, c = threadIdx.x % kSnCand;
-        if (c < hdr_nc(n ? h1 : h0)) {
-            unsigned s = ws[n][c][0];
-            for (int k = 1; k < kSnThreads / 64; k++) s = sat(s, ws[n][c][k]);
-            T[(2 * (size_t)blockIdx.x + n) * kSnCand + c] = s;
-        }
-    }
-}
-
-// ---------------------------------------------------------------- the walk
 // A run of terms inside one binade as a function of the parity of M:
-// M -> M + (M even ? lo : hi), packed lo | hi << 32.  A term without a tie
-// adds m ulps either way; a tie (d rounded to exactly m0 + 1/2 ulps) rounds
-// M + m0 + 1/2 to even, i.e. adds m0 or m0 + 1 by the parity of M.  The form
-// is closed under composition, so the walk's resolves scan ties like any other
+// M -> M + (M even ? lo : hi), packed lo | hi << 32.  A term without a tie adds
+// m ulps either way; a tie (d rounded to exactly m0 + 1/2 ulps) rounds
+// M + m0 + 1/2 to even, i.e. adds m0 or m0 + 1 by the parity of M.  The form is
+// closed under composition, so term-level scans compose ties like any other
 // term (a constant field of dyadic magnitudes ties on every term).
 typedef unsigned long long sn_fn;
 __device__ __forceinline__ sn_fn fn_make(unsigned e, unsigned o) {
@@ -315,224 +159,528 @@ __device__ __forceinline__ sn_fn sn_term_fn(double d, double scale, bool &nan) {
     return fn_make(m, m);
 }
 
-// block-wide primitives of the 1024-thread walk block
-struct WalkShared {
-    unsigned wsum[kSnWalk / 64];
-    unsigned wmin[kSnWalk / 64];
-    sn_fn wfn[kSnWalk / 64];
-    unsigned base;  // exclusive prefix at the first failing tile
-    float S;
-};
+// binade of a double bound, clamped to the float range
+__device__ __forceinline__ int sn_region_d(double v) {
+    if (!(v >= 0x1p-100)) return kSnLow;
+    if (v >= 0x1p127) return 127;
+    int ex;
+    (void)frexp(v, &ex);
+    return ex - 1;
+}
+// candidate binades covering [lo, hi] (at most kSnCand, the top ones kept)
+__device__ __forceinline__ unsigned cand_window(double lo, double hi) {
+    const int ehi = sn_region_d(hi);
+    if (ehi == kSnLow) return hdr_pack(0, 0);
+    int elo = sn_region_d(lo);
+    if (elo == kSnLow) elo = kSnEmin;
+    if (ehi - elo + 1 > kSnCand) elo = ehi - kSnCand + 1;
+    return hdr_pack(elo, ehi - elo + 1);
+}
 
-__device__ __forceinline__ unsigned wave_incl_sat(unsigned v) {
-    const int lane = threadIdx.x & 63;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const unsigned t = __shfl_up(v, o, 64);
-        if (lane >= o) v = sn_sat(v, t);
+// The magnitudes of term L: 0 past the grid
+__device__ __forceinline__ void sn_terms(const float2 *__restrict__ cur,
+                                         const float2 *__restrict__ prev, unsigned L, unsigned N,
+                                         unsigned i, unsigned j, int P, double &dd, double &dp) {
+    dd = dp = 0.0;
+    if (L < N) {
+        const size_t off = (size_t)j * (size_t)P + i;
+        const float2 c = cur[off], p = prev[off];
+        dd = sn_mag(c.x - p.x, c.y - p.y);  // Field::operator- (Field.tpp:305-334)
+        dp = sn_mag(p.x, p.y);
     }
+}
+
+template <class T, class Op>
+__device__ __forceinline__ T wave_reduce(T v, Op op) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = op(v, __shfl_xor(v, o, 64));
     return v;
 }
-// saturating scan over the block in thread order: returns the inclusive
-// prefix, *excl the exclusive one (both exact while below kSnSat), *total the
-// block total
-__device__ unsigned block_scan_sat(unsigned v, WalkShared &sh, unsigned *excl, unsigned *total) {
-    const int w = threadIdx.x / 64, lane = threadIdx.x & 63;
-    const unsigned wi = wave_incl_sat(v);
-    unsigned we = __shfl_up(wi, 1, 64);
-    if (lane == 0) we = 0;
-    if (lane == 63) sh.wsum[w] = wi;
-    __syncthreads();
-    unsigned pre = 0, tot = 0;
-    for (int k = 0; k < kSnWalk / 64; k++) {
-        if (k < w) pre = sn_sat(pre, sh.wsum[k]);
-        tot = sn_sat(tot, sh.wsum[k]);
-    }
-    __syncthreads();
-    *total = tot;
-    *excl = sn_sat(pre, we);
-    return sn_sat(pre, wi);
-}
-// ordered scan of functions: *excl = composition of the earlier threads'
-// functions, returns the composition over the whole block
-__device__ sn_fn block_scan_fn(sn_fn v, WalkShared &sh, sn_fn *excl) {
-    const int w = threadIdx.x / 64, lane = threadIdx.x & 63;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const sn_fn t = __shfl_up(v, o, 64);
-        if (lane >= o) v = fn_then(t, v);
-    }
-    sn_fn we = __shfl_up(v, 1, 64);
-    if (lane == 0) we = 0;
-    if (lane == 63) sh.wfn[w] = v;
-    __syncthreads();
-    sn_fn pre = 0, tot = 0;
-    for (int k = 0; k < kSnWalk / 64; k++) {
-        if (k < w) pre = fn_then(pre, sh.wfn[k]);
-        tot = fn_then(tot, sh.wfn[k]);
-    }
-    __syncthreads();
-    *excl = fn_then(pre, we);
-    return tot;
-}
-__device__ unsigned block_min(unsigned v, WalkShared &sh) {
-    const int w = threadIdx.x / 64;
-    v = wave_reduce(v, [](unsigned a, unsigned b) { return a < b ? a : b; });
-    if ((threadIdx.x & 63) == 0) sh.wmin[w] = v;
-    __syncthreads();
-    unsigned m = sh.wmin[0];
-    for (int k = 1; k < kSnWalk / 64; k++) m = min(m, sh.wmin[k]);
-    __syncthreads();
-    return m;
-}
-__device__ bool block_any(bool v, WalkShared &sh) { return block_min(v ? 0u : 1u, sh) == 0u; }
 
-// Tile `tile` from the exact running sum S: thread tid holds terms
-// [kSnTerms tid, kSnTerms (tid + 1)) of the tile.  Each round takes the binade
-// of S, composes the terms after `pos` by an ordered block scan up to the first
-// term that leaves the binade, is NaN, or (low sum) is nonzero, and steps that
-// one term as the reference does.
-__device__ float sn_resolve(const float2 *__restrict__ cur, const float2 *__restrict__ prev,
-                            int which, unsigned tile, unsigned N, int dimx, int P, float S,
-                            WalkShared &sh) {
-    double d[kSnTerms];
-    {
-        const unsigned L = tile * (unsigned)kSnTile + kSnTerms * threadIdx.x;
-        unsigned j = L / (unsigned)dimx, i = L - j * (unsigned)dimx;
-#pragma unroll
-        for (int k = 0; k < kSnTerms; k++) {
-            d[k] = 0.0;
-            if (L + k < N) {
-                const size_t off = (size_t)j * (size_t)P + i;
-                const float2 p = prev[off];
-                if (which == 0) {
-                    const float2 c = cur[off];
-                    d[k] = sn_mag(c.x - p.x, c.y - p.y);
-                } else {
-                    d[k] = sn_mag(p.x, p.y);
-                }
-            }
-            if (++i == (unsigned)dimx) {
-                i = 0;
-                j++;
+struct SnWs {
+    double *A;              // [nt][2] fp64 tile sums
+    unsigned *H;            // [nt][2] headers
+    unsigned long long *Z;  // [nt][2] nonzero-segment masks
+    unsigned *T;            // [nt][2][kSnCand] tile entries
+    unsigned *G;            // [nt][2][kSnCand][kSnSegs] segment entries
+    float *prof;            // [2][nt + 1] exact running sum at each tile start; [nt] = total
+    double *Pp;             // [2][nt + 1] fp64 prefix at each tile start (seqnorm_check)
+    float *tot;             // [2][2] the last two totals per norm (the walk)
+    unsigned *list;         // [nt] tiles seqnorm_check listed for seqnorm_fix
+    unsigned *cnt;          // [4] list length
+};
+// The profile of the last call that predicts norm n: its own, except for
+// |prev| after a call whose prev was zero (the Logger's first update), whose
+// |cur - prev| was this |prev|
+__device__ __forceinline__ int prof_src(const SnWs &ws, int n) {
+    return (n == 1 && ws.tot[2] == 0.0f) ? 0 : n;
+}
+__device__ __forceinline__ size_t g_index(unsigned b, int n, int c, int s) {
+    return (((size_t)b * 2 + n) * kSnCand + c) * kSnSegs + s;
+}
+
+// ---------------------------------------------------------------- tables
+// Entries of one tile for the candidate binades of its two headers: the tile
+// entries T (ALL) and, for the norms whose header asks for them (SEG), the
+// 64 segment entries G.  FIRST (the pass over every tile) also writes the fp64
+// tile sums, the nonzero-segment masks and the headers: candidates from the
+// profile (use_prof), none without one.
+template <bool FIRST>
+__device__ void sn_tile_tables(const float2 *__restrict__ cur, const float2 *__restrict__ prev,
+                               unsigned N, int dimx, int P, unsigned nt, const SnWs &ws,
+                               unsigned b, unsigned h0, unsigned h1, int use_prof) {
+    const int w = threadIdx.x / 64, lane = threadIdx.x & 63;
+    unsigned h[2] = {h0, h1};
+    if (FIRST) {
+        for (int n = 0; n < 2; n++) {
+            h[n] = hdr_pack(0, 0);
+            if (use_prof) {
+                // the last call's running sums scaled by the trend of its
+                // totals (|cur - prev| shrinks from update to update)
+                const int src = prof_src(ws, n);
+                const float *pr = ws.prof + (size_t)src * (nt + 1);
+                const float t0 = ws.tot[2 * src], t1 = ws.tot[2 * src + 1];
+                double r = (src == n && t1 > 0.0f && t0 > 0.0f) ? (double)t0 / t1 : 1.0;
+                r = r < 0.25 ? 0.25 : (r > 4.0 ? 4.0 : r);
+                h[n] = cand_window((double)pr[b] * r * 0.75, (double)pr[b + 1] * r * 1.333);
             }
         }
     }
-    unsigned pos = 0;  // first term of the tile not yet added
-    for (;;) {
+    int nc[2];
+    bool tab[2], seg[2];
+    double scale[2][kSnCand];
+    for (int n = 0; n < 2; n++) {
+        tab[n] = FIRST || (h[n] & kHdrPending);
+        seg[n] = !FIRST && (h[n] & kHdrSegReq);
+        nc[n] = (tab[n] || seg[n]) ? hdr_nc(h[n]) : 0;
+#pragma unroll
+        for (int c = 0; c < kSnCand; c++)
+            scale[n][c] = sn_scale(c < nc[n] ? hdr_elo(h[n]) + c : 0);
+    }
+    unsigned tacc[2][kSnCand] = {};
+    bool tbad[2][kSnCand] = {};
+    double fs[2] = {0.0, 0.0};
+    unsigned long long zm[2] = {0ull, 0ull};
+    // segment s = kSnThreads/64 * r + w: 64 consecutive terms per wave and round
+    unsigned L = b * (unsigned)kSnTile + 64u * w + lane;
+    unsigned j = L / (unsigned)dimx, i = L - j * (unsigned)dimx;
+    for (int r = 0; r < kSnRounds; r++) {
+        const int s = (kSnThreads / 64) * r + w;
+        double d[2];
+        sn_terms(cur, prev, L, N, i, j, P, d[0], d[1]);
+#pragma unroll
+        for (int n = 0; n < 2; n++) {
+            if (FIRST) {
+                fs[n] += d[n];
+                if (__ballot(d[n] != 0.0)) zm[n] |= 1ull << s;
+            }
+#pragma unroll
+            for (int c = 0; c < kSnCand; c++) {
+                if (c >= nc[n]) continue;
+                bool bad = false;
+                const unsigned m = sn_incr(d[n], scale[n][c], bad);  // <= 2^25
+                tacc[n][c] = sn_sat(tacc[n][c], m);
+                tbad[n][c] |= bad;
+                if (seg[n]) {  // 64 of them fit in 32 bits
+                    const unsigned t = wave_reduce(m, [](unsigned a, unsigned x) { return a + x; });
+                    const unsigned e = (t < kSnSat ? t : kSnSat) | (__ballot(bad) ? kSnBad : 0u);
+                    if (lane == 0) ws.G[g_index(b, n, c, s)] = e;
+                }
+            }
+        }
+        L += kSnThreads;
+        i += kSnThreads;
+        while (i >= (unsigned)dimx) {
+            i -= (unsigned)dimx;
+            j++;
+        }
+    }
+    __shared__ unsigned st[2][kSnCand][kSnThreads / 64];
+    __shared__ double sf[2][kSnThreads / 64];
+    __shared__ unsigned long long sz[2][kSnThreads / 64];
+    auto sat = [](unsigned a, unsigned x) {
+        return ((a | x) & kSnBad) | sn_sat(a & ~kSnBad, x & ~kSnBad);
+    };
+    for (int n = 0; n < 2; n++) {
+#pragma unroll
+        for (int c = 0; c < kSnCand; c++) {
+            if (c >= nc[n]) continue;
+            const unsigned t = wave_reduce(tacc[n][c] | (tbad[n][c] ? kSnBad : 0u), sat);
+            if (lane == 0) st[n][c][w] = t;
+        }
+        if (FIRST) {
+            const double f = wave_reduce(fs[n], [](double a, double x) { return a + x; });
+            if (lane == 0) {
+                sf[n][w] = f;
+                sz[n][w] = zm[n];
+            }
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < 2) {
+        const int n = threadIdx.x;
+        if (tab[n])
+            for (int c = 0; c < nc[n]; c++) {
+                unsigned t = st[n][c][0];
+                for (int k = 1; k < kSnThreads / 64; k++) t = sat(t, st[n][c][k]);
+                ws.T[(2 * (size_t)b + n) * kSnCand + c] = t;
+            }
+        unsigned hh = h[n] & ~(kHdrPending | kHdrSegReq);
+        if (seg[n]) hh |= kHdrSeg;
+        if (FIRST)  // a tie or NaN among the entries: the walk will want segment entries
+            for (int c = 0; c < nc[n]; c++)
+                if (st[n][c][0] & kSnBad || st[n][c][1] & kSnBad || st[n][c][2] & kSnBad ||
+                    st[n][c][3] & kSnBad)
+                    hh |= kHdrSegReq;
+        if (FIRST) {
+            double a = 0.0;
+            unsigned long long z = 0;
+            for (int k = 0; k < kSnThreads / 64; k++) {
+                a += sf[n][k];
+                z |= sz[n][k];
+            }
+            ws.A[2 * (size_t)b + n] = a;
+            ws.Z[2 * (size_t)b + n] = z;
+            if (a == 0.0) hh = kHdrZero;
+            else if (a != a) hh = hdr_pack(0, 0) | kHdrNan;
+        }
+        ws.H[2 * (size_t)b + n] = hh;
+    }
+    __syncthreads();  // st / sf / sz are reused by the next tile of the block
+}
+
+__global__ __launch_bounds__(kSnThreads) void seqnorm_tables(const float2 *__restrict__ cur,
+                                                            const float2 *__restrict__ prev,
+                                                            unsigned N, int dimx, int P,
+                                                            unsigned nt, SnWs ws, int use_prof) {
+    if (blockIdx.x == 0 && threadIdx.x < 4) ws.cnt[threadIdx.x] = 0;  // seqnorm_check's list
+    sn_tile_tables<true>(cur, prev, N, dimx, P, nt, ws, blockIdx.x, 0, 0, use_prof);
+}
+
+// fp64 prefix of the tile sums (a prediction: any order) -> the binades the
+// float sum can be in across each tile: the prefix times the last call's
+// drift of the float sum from it (use_prof; 1/64 either side), or the prefix
+// alone (1/16 either side).  A tile whose entries miss one is listed for new
+// tile entries (pending); a tile across which the sum may change binade is
+// listed for segment entries (the walk resolves it).
+__global__ __launch_bounds__(kSnScan) void seqnorm_check(unsigned nt, SnWs ws, int use_prof) {
+    const unsigned chunk = (nt + kSnScan - 1) / kSnScan;
+    const unsigned b0 = threadIdx.x * chunk;
+    const unsigned b1 = min(nt, b0 + chunk);
+    __shared__ double sh[2][kSnScan];
+    for (int n = 0; n < 2; n++) {
+        double s = 0.0;
+        for (unsigned b = b0; b < b1; b++) s += ws.A[2 * (size_t)b + n];
+        sh[n][threadIdx.x] = s;
+    }
+    __syncthreads();
+    for (int o = 1; o < kSnScan; o <<= 1) {
+        double v0 = 0.0, v1 = 0.0;
+        if ((int)threadIdx.x >= o) {
+            v0 = sh[0][threadIdx.x - o];
+            v1 = sh[1][threadIdx.x - o];
+        }
+        __syncthreads();
+        sh[0][threadIdx.x] += v0;
+        sh[1][threadIdx.x] += v1;
+        __syncthreads();
+    }
+    const double del = use_prof ? 1.0 / 64 : 1.0 / 16;
+    int src[2];
+    double Pb[2], drift[2], dend[2];
+    auto drift_at = [&](int s, unsigned b) {
+        if (!use_prof) return 1.0;
+        const double f = ws.prof[(size_t)s * (nt + 1) + b], q = ws.Pp[(size_t)s * (nt + 1) + b];
+        return (q > 0.0 && f > 0.0 && f < INFINITY) ? f / q : 1.0;
+    };
+    for (int n = 0; n < 2; n++) {
+        src[n] = prof_src(ws, n);
+        Pb[n] = threadIdx.x ? sh[n][threadIdx.x - 1] : 0.0;
+        drift[n] = drift_at(src[n], b0);
+        dend[n] = drift_at(src[n], b1);  // the next thread's first tile
+    }
+    __syncthreads();  // these reads of the last call's Pp before this call's writes
+    for (unsigned b = b0; b < b1; b++) {
+        bool listed = false;
+        double dnext[2];
+        for (int n = 0; n < 2; n++) dnext[n] = b + 1 == b1 ? dend[n] : drift_at(src[n], b + 1);
+        for (int n = 0; n < 2; n++) {
+            const double a = ws.A[2 * (size_t)b + n];
+            const unsigned h = ws.H[2 * (size_t)b + n];
+            if (!(h & (kHdrZero | kHdrNan)) && a < INFINITY && Pb[n] < INFINITY) {
+                const unsigned want = cand_window(Pb[n] * drift[n] * (1.0 - del),
+                                                  (Pb[n] + a) * dnext[n] * (1.0 + del));
+                const int wl = hdr_elo(want), wn = hdr_nc(want), hl = hdr_elo(h), hn = hdr_nc(h);
+                unsigned hh = h;
+                if (wn > 0 && (wl < hl || wl + wn > hl + hn)) hh = want | kHdrPending;
+                if (wn > 1 || b == 0) hh |= kHdrSegReq;
+                if (hh != h) ws.H[2 * (size_t)b + n] = hh;
+                listed |= (hh & (kHdrPending | kHdrSegReq)) != 0;
+            }
+            drift[n] = dnext[n];
+        }
+        if (listed) ws.list[atomicAdd(&ws.cnt[0], 1u)] = b;
+        for (int n = 0; n < 2; n++) {
+            ws.Pp[(size_t)n * (nt + 1) + b] = Pb[n];
+            Pb[n] += ws.A[2 * (size_t)b + n];
+        }
+    }
+    if (b1 == nt && b0 < b1)
+        for (int n = 0; n < 2; n++) ws.Pp[(size_t)n * (nt + 1) + nt] = Pb[n];
+}
+
+// the listed tiles: new tile entries and / or segment entries
+__global__ __launch_bounds__(kSnThreads) void seqnorm_fix(const float2 *__restrict__ cur,
+                                                         const float2 *__restrict__ prev,
+                                                         unsigned N, int dimx, int P,
+                                                         unsigned nt, SnWs ws) {
+    const unsigned cnt = ws.cnt[0];
+    for (unsigned k = blockIdx.x; k < cnt; k += gridDim.x) {
+        const unsigned b = ws.list[k];
+        sn_tile_tables<false>(cur, prev, N, dimx, P, nt, ws, b, ws.H[2 * (size_t)b],
+                              ws.H[2 * (size_t)b + 1], 0);
+    }
+}
+
+// ---------------------------------------------------------------- the walk
+// Wave scans on DPP (row shifts within rows of 16, then the row broadcasts
+// of gfx9): lanes shifted in from outside read 0, the identity of both
+// operations.  Earlier lanes come first, so the ordered fn composition holds.
+template <int CTRL, int ROWS>
+__device__ __forceinline__ unsigned dpp_u(unsigned v) {
+    return (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, ROWS, 0xF, true);
+}
+template <int CTRL, int ROWS>
+__device__ __forceinline__ sn_fn dpp_fn(sn_fn v) {
+    return fn_make(dpp_u<CTRL, ROWS>(fn_e(v)), dpp_u<CTRL, ROWS>(fn_o(v)));
+}
+__device__ __forceinline__ unsigned wave_incl_sat(unsigned v) {
+    v = sn_sat(dpp_u<0x111, 0xF>(v), v);  // row_shr:1
+    v = sn_sat(dpp_u<0x112, 0xF>(v), v);  // row_shr:2
+    v = sn_sat(dpp_u<0x114, 0xF>(v), v);  // row_shr:4
+    v = sn_sat(dpp_u<0x118, 0xF>(v), v);  // row_shr:8
+    v = sn_sat(dpp_u<0x142, 0xA>(v), v);  // row_bcast:15 into rows 1, 3
+    v = sn_sat(dpp_u<0x143, 0xC>(v), v);  // row_bcast:31 into rows 2, 3
+    return v;
+}
+__device__ __forceinline__ sn_fn wave_incl_fn(sn_fn v) {
+    v = fn_then(dpp_fn<0x111, 0xF>(v), v);
+    v = fn_then(dpp_fn<0x112, 0xF>(v), v);
+    v = fn_then(dpp_fn<0x114, 0xF>(v), v);
+    v = fn_then(dpp_fn<0x118, 0xF>(v), v);
+    v = fn_then(dpp_fn<0x142, 0xA>(v), v);
+    v = fn_then(dpp_fn<0x143, 0xC>(v), v);
+    return v;
+}
+// the value of the lane below (wave_shr:1), 0 in lane 0
+__device__ __forceinline__ unsigned lane_below(unsigned v) { return dpp_u<0x138, 0xF>(v); }
+__device__ __forceinline__ sn_fn lane_below(sn_fn v) { return dpp_fn<0x138, 0xF>(v); }
+__device__ __forceinline__ unsigned lane_at(unsigned v, int q) {
+    return (unsigned)__builtin_amdgcn_readlane((int)v, q);
+}
+__device__ __forceinline__ int first_lane(unsigned long long m) { return __builtin_ctzll(m); }
+__device__ __forceinline__ unsigned long long lanes_from(int k) {
+    return k >= 64 ? 0ull : (~0ull << k);
+}
+
+// The 64 terms of segment `seg` of tile `b` (lane = term) from the exact
+// running sum S, term by term where the binade changes.
+__device__ float sn_raw_segment(const float2 *__restrict__ cur, const float2 *__restrict__ prev,
+                                int which, unsigned b, int seg, unsigned N, int dimx, int P,
+                                float S) {
+    const int lane = threadIdx.x & 63;
+    const unsigned L = b * (unsigned)kSnTile + 64u * seg + lane;
+    const unsigned j = L / (unsigned)dimx, i = L - j * (unsigned)dimx;
+    double d[2];
+    sn_terms(cur, prev, L, N, i, j, P, d[0], d[1]);
+    const double dv = which ? d[1] : d[0];
+    int pos = 0;
+    while (pos < 64) {
         const int e = sn_region(S);
         if (e == kSnNonfinite) {
-            bool nan = false;
-#pragma unroll
-            for (int k = 0; k < kSnTerms; k++)
-                nan |= (kSnTerms * threadIdx.x + k >= pos) && (d[k] != d[k]);
-            return block_any(nan, sh) ? __uint_as_float(0x7fc00000u) : S;
+            // inf stays inf unless a NaN follows; NaN stays NaN
+            if (__ballot(lane >= pos && dv != dv)) S = __uint_as_float(0x7fc00000u);
+            return S;
         }
         const bool low = (e == kSnLow);
         const unsigned M = low ? 0u : sn_mant(S);
-        const double scale = low ? 0.0 : sn_scale(e);
-        sn_fn f[kSnTerms], tf = 0;
-        bool fail[kSnTerms];
-#pragma unroll
-        for (int k = 0; k < kSnTerms; k++) {
-            bool bad = false;
-            f[k] = 0;
-            if (kSnTerms * threadIdx.x + k >= pos) {
-                if (low)
-                    bad = (d[k] != 0.0);  // NaN too
-                else
-                    f[k] = sn_term_fn(d[k], scale, bad);
-            }
-            fail[k] = bad;
-            tf = fn_then(tf, f[k]);
+        bool bad = false;
+        sn_fn f = 0;
+        if (lane >= pos) {
+            if (low)
+                bad = (dv != 0.0);  // NaN too
+            else
+                f = sn_term_fn(dv, sn_scale(e), bad);
         }
-        sn_fn excl;
-        const sn_fn tot = block_scan_fn(tf, sh, &excl);
-        // this thread's first term that fails or takes M past the binade (the
-        // running M is exact up to the block's first such term)
-        unsigned R = fn_apply(excl, M), myfirst = 0xffffffffu, mybase = 0;
-#pragma unroll
-        for (int k = 0; k < kSnTerms; k++) {
-            if (myfirst != 0xffffffffu) break;
-            const unsigned nR = fn_apply(f[k], R);
-            if (fail[k] || nR > kSnLimit) {
-                myfirst = kSnTerms * threadIdx.x + k;
-                mybase = R;
-            } else {
-                R = nR;
-            }
+        const sn_fn incl = wave_incl_fn(f);
+        const sn_fn excl = lane_below(incl);
+        const unsigned R = fn_apply(excl, M);
+        const bool fail = lane >= pos && (bad || fn_apply(f, R) > kSnLimit);
+        const unsigned long long fm = __ballot(fail);
+        if (!fm) {
+            if (!low) S = sn_make(e, fn_apply(fn_make(lane_at(fn_e(incl), 63), lane_at(fn_o(incl), 63)), M));
+            return S;
         }
-        const unsigned first = block_min(myfirst, sh);
-        if (first == 0xffffffffu) return low ? S : sn_make(e, fn_apply(tot, M));
-        if (myfirst == first) {
-            const float Sf = low ? S : sn_make(e, mybase);
-            sh.S = (float)((double)Sf + d[first - kSnTerms * threadIdx.x]);  // Motion.cpp:46
-        }
-        __syncthreads();
-        S = sh.S;
-        __syncthreads();
-        pos = first + 1;
+        const int q = first_lane(fm);
+        const float Sq = low ? S : sn_make(e, lane_at(R, q));
+        const long long db = __double_as_longlong(dv);
+        const double dq = __longlong_as_double(
+            (long long)lane_at((unsigned)db, q) | ((long long)lane_at((unsigned)(db >> 32), q) << 32));
+        S = (float)((double)Sq + dq);  // Motion.cpp:46
+        pos = q + 1;
     }
+    return S;
 }
 
-__global__ __launch_bounds__(kSnWalk) void seqnorm_walk(const float2 *__restrict__ cur,
-                                                        const float2 *__restrict__ prev,
-                                                        unsigned N, int dimx, int P,
-                                                        unsigned ntiles,
-                                                        const unsigned *__restrict__ H,
-                                                        const unsigned *__restrict__ T,
-                                                        float *__restrict__ out,
-                                                        int *__restrict__ dbg) {
-    __shared__ WalkShared sh;
-    const int n = blockIdx.x;  // 0: |cur - prev|, 1: |prev|
-    float S = 0.0f;
-    unsigned b = 0;
-    int resolves = 0;
-    bool nan = false;  // non-finite sum: a NaN magnitude after it
-    while (b < ntiles) {
-        const unsigned tb = b + threadIdx.x;
+// Tile b from the exact running sum S: its segment entries where one covers
+// the binade, raw segments where none does (a crossing, a tie, a missed
+// binade, the low sum).
+__device__ float sn_resolve(const float2 *__restrict__ cur, const float2 *__restrict__ prev,
+                            int which, unsigned b, unsigned N, int dimx, int P, float S,
+                            unsigned h, const SnWs &ws, int &raw) {
+    const int lane = threadIdx.x & 63;
+    const int nc = (h & kHdrSeg) ? hdr_nc(h) : 0, elo = hdr_elo(h);
+    const unsigned long long zm = ws.Z[2 * (size_t)b + which];
+    unsigned g[kSnCand];
+#pragma unroll
+    for (int c = 0; c < kSnCand; c++) g[c] = c < nc ? ws.G[g_index(b, which, c, lane)] : 0u;
+    int s0 = 0;
+    while (s0 < kSnSegs) {
         const int e = sn_region(S);
-        unsigned h = kHdrZero;
-        if (tb < ntiles) h = H[2 * (size_t)tb + n];
-        if (e == kSnNonfinite) {
-            nan |= (h & kHdrNan) != 0;
-            b += kSnWalk;
-            continue;
+        const int c = e - elo;
+        if (e != kSnLow && e != kSnNonfinite && c >= 0 && c < nc) {
+            unsigned gc = g[0];
+#pragma unroll
+            for (int k = 1; k < kSnCand; k++)
+                if (c == k) gc = g[k];
+            const unsigned M = sn_mant(S);
+            const unsigned v = lane >= s0 ? (gc & ~kSnBad) : 0u;
+            const unsigned incl = wave_incl_sat(v);
+            const unsigned excl = lane_below(incl);
+            const bool fail = lane >= s0 && ((gc & kSnBad) || M + incl > kSnLimit);
+            const unsigned long long fm = __ballot(fail);
+            if (!fm) return sn_make(e, M + lane_at(incl, 63));
+            const int q = first_lane(fm);
+            S = sn_make(e, M + lane_at(excl, q));  // exact: below the limit
+            s0 = q;
+        } else if (e == kSnLow) {
+            const unsigned long long nz = zm & lanes_from(s0);
+            if (!nz) return S;  // every remaining term is 0
+            s0 = first_lane(nz);
         }
-        unsigned v = 0;
-        bool fail = false;
-        if (!(h & kHdrZero)) {
-            const int c = e - hdr_elo(h);
-            if (e == kSnLow || c < 0 || c >= hdr_nc(h)) {
-                fail = true;
-            } else {
-                const unsigned w = T[(2 * (size_t)tb + n) * kSnCand + c];
-                fail = (w & kSnBad) != 0;
-                v = w & ~kSnBad;
+        S = sn_raw_segment(cur, prev, which, b, s0, N, dimx, P, S);
+        raw++;
+        s0++;
+    }
+    return S;
+}
+
+constexpr int kSnAhead = 8;  // windows loaded per step: the next step's loads hide behind them
+
+// One wave per norm walks the tiles in windows of 64 (lane = tile): the
+// saturating scan of the entries for S's binade, a resolve at each tile whose
+// entry does not apply.  Writes every tile's start sum into the profile.
+// dbg: resolves (per norm), raw segments (per norm), listed tiles.
+__global__ __launch_bounds__(64) void seqnorm_walk(const float2 *__restrict__ cur,
+                                                   const float2 *__restrict__ prev, unsigned N,
+                                                   int dimx, int P, unsigned nt, SnWs ws,
+                                                   float *__restrict__ out,
+                                                   int *__restrict__ dbg) {
+    const int n = blockIdx.x;  // 0: |cur - prev|, 1: |prev|
+    const int lane = threadIdx.x;
+    float *prof = ws.prof + (size_t)n * (nt + 1);
+    __shared__ unsigned lh[kSnAhead][64], lt[kSnAhead][kSnCand][64];
+    unsigned hn[kSnAhead], tn[kSnAhead][kSnCand];
+    auto load = [&](unsigned b0) {
+#pragma unroll
+        for (int k = 0; k < kSnAhead; k++) {
+            const unsigned t = b0 + 64u * k + lane;
+            hn[k] = kHdrZero;
+#pragma unroll
+            for (int c = 0; c < kSnCand; c++) tn[k][c] = 0;
+            if (t < nt) {
+                hn[k] = ws.H[2 * (size_t)t + n];
+#pragma unroll
+                for (int c = 0; c < kSnCand; c++)
+                    tn[k][c] = ws.T[(2 * (size_t)t + n) * kSnCand + c];
             }
         }
-        const unsigned M = (e == kSnLow) ? 0u : sn_mant(S);
-        unsigned total, excl;
-        const unsigned incl = block_scan_sat(v, sh, &excl, &total);
-        fail |= (M + incl > kSnLimit);
-        const unsigned first = block_min(fail ? threadIdx.x : 0xffffffffu, sh);
-        if (first == 0xffffffffu) {
-            if (e != kSnLow) S = sn_make(e, M + total);  // low: all tiles were zero
-            b += kSnWalk;
-            continue;
+    };
+    float S = 0.0f;
+    int resolves = 0;
+    int raw = 0;
+    bool nan = false;  // non-finite sum: a NaN magnitude after it
+    const long long c0 = wall_clock64();
+    long long cres = 0;
+    load(0);
+    for (unsigned bs = 0; bs < nt; bs += 64u * kSnAhead) {
+#pragma unroll
+        for (int k = 0; k < kSnAhead; k++) {
+            lh[k][lane] = hn[k];
+#pragma unroll
+            for (int c = 0; c < kSnCand; c++) lt[k][c][lane] = tn[k][c];
         }
-        if (threadIdx.x == first) sh.base = excl;  // exact: no earlier thread failed
-        __syncthreads();
-        if (e != kSnLow && first > 0) S = sn_make(e, M + sh.base);
-        __syncthreads();
-        S = sn_resolve(cur, prev, n, b + first, N, dimx, P, S, sh);
-        resolves++;
-        b += first + 1;
+        if (bs + 64u * kSnAhead < nt) load(bs + 64u * kSnAhead);
+        for (int k = 0; k < kSnAhead && bs + 64u * k < nt; k++) {
+            const unsigned b0 = bs + 64u * k, t = b0 + lane;
+            const unsigned h = lh[k][lane];
+            int start = 0;  // first lane of the window not yet added
+            while (start < 64) {
+                const int e = sn_region(S);
+                if (e == kSnNonfinite) {
+                    if (lane >= start && t < nt) prof[t] = S;
+                    nan |= __ballot(lane >= start && (h & kHdrNan)) != 0ull;
+                    break;
+                }
+                const bool low = (e == kSnLow);
+                const unsigned M = low ? 0u : sn_mant(S);
+                unsigned v = 0;
+                bool fail = false;
+                if (lane >= start && !(h & kHdrZero)) {
+                    const int c = e - hdr_elo(h);
+                    if (low || c < 0 || c >= hdr_nc(h)) {
+                        fail = true;
+                    } else {
+                        const unsigned w = lt[k][c][lane];
+                        fail = (w & kSnBad) != 0;
+                        v = w & ~kSnBad;
+                    }
+                }
+                const unsigned incl = wave_incl_sat(v);
+                const unsigned excl = lane_below(incl);
+                fail = fail || (lane >= start && M + incl > kSnLimit);
+                const unsigned long long fm = __ballot(fail);
+                const int q = fm ? first_lane(fm) : 64;
+                // tile start sums of the lanes up to the first failing one: exact
+                if (lane >= start && lane <= q && t < nt)
+                    prof[t] = low ? S : sn_make(e, M + excl);
+                if (!fm) {
+                    if (!low) S = sn_make(e, M + lane_at(incl, 63));
+                    break;
+                }
+                if (!low) S = sn_make(e, M + lane_at(excl, q));
+                const long long r0 = wall_clock64();
+                S = sn_resolve(cur, prev, n, b0 + q, N, dimx, P, S, lane_at(h, q), ws, raw);
+                cres += wall_clock64() - r0;
+                resolves++;
+                start = q + 1;
+            }
+        }
     }
-    if (threadIdx.x == 0) {
-        if (nan) S = __uint_as_float(0x7fc00000u);
+    if (nan) S = __uint_as_float(0x7fc00000u);
+    if (lane == 0) {
+        prof[nt] = S;
+        ws.tot[2 * n + 1] = ws.tot[2 * n];
+        ws.tot[2 * n] = S;
         out[n] = S;
-        if (dbg) dbg[n] = resolves;
+        if (dbg) {
+            dbg[n] = resolves;
+            dbg[2 + n] = raw;
+            if (n == 0) dbg[4] = (int)ws.cnt[0];
+            // wall-clock ticks (100 MHz) of the whole walk and of its resolves
+            dbg[5 + n] = (int)(wall_clock64() - c0);
+            if (n == 0) dbg[7] = (int)cres;
+        }
     }
 }
 
@@ -541,29 +689,64 @@ __global__ __launch_bounds__(kSnWalk) void seqnorm_walk(const float2 *__restrict
 size_t seqnorm_workspace_bytes(int dimx, int dimy) {
     const size_t N = (size_t)dimx * (size_t)dimy;
     const size_t nt = (N + kSnTile - 1) / kSnTile;
-    return nt * (2 * sizeof(double) + 2 * sizeof(unsigned) + 2 * kSnCand * sizeof(unsigned));
+    return nt * (2 * sizeof(double) + 2 * sizeof(unsigned long long) + 2 * sizeof(unsigned) +
+                 2 * kSnCand * sizeof(unsigned) + 2 * kSnCand * kSnSegs * sizeof(unsigned) +
+                 sizeof(unsigned)) +
+           2 * (nt + 1) * (sizeof(double) + sizeof(float)) + 4 * sizeof(float) +
+           4 * sizeof(unsigned) + 256;
 }
 
-void launch_seqnorm(const float2 *cur, const float2 *prev, int dimx, int dimy, int P, void *ws,
-                    float *out, int *dbg, hipStream_t st) {
+namespace {
+SnWs carve(void *ws, unsigned nt) {
+    SnWs w;
+    w.A = static_cast<double *>(ws);
+    w.Z = reinterpret_cast<unsigned long long *>(w.A + 2 * (size_t)nt);
+    w.H = reinterpret_cast<unsigned *>(w.Z + 2 * (size_t)nt);
+    w.T = w.H + 2 * (size_t)nt;
+    w.G = w.T + 2 * (size_t)nt * kSnCand;
+    w.Pp = reinterpret_cast<double *>(w.G + 2 * (size_t)nt * kSnCand * kSnSegs);
+    w.prof = reinterpret_cast<float *>(w.Pp + 2 * (size_t)(nt + 1));
+    w.tot = w.prof + 2 * (size_t)(nt + 1);
+    w.list = reinterpret_cast<unsigned *>(w.tot + 4);
+    w.cnt = w.list + nt;
+    return w;
+}
+unsigned check_geometry(int dimx, int dimy, int P) {
     const size_t N = (size_t)dimx * (size_t)dimy;
     if (dimx <= 0 || dimy <= 0 || P < dimx || N > 0xffffffffu)
         throw std::invalid_argument("launch_seqnorm: bad geometry");
-    const unsigned nt = (unsigned)((N + kSnTile - 1) / kSnTile);
-    double *A = static_cast<double *>(ws);
-    unsigned *H = reinterpret_cast<unsigned *>(A + 2 * (size_t)nt);
-    unsigned *T = H + 2 * (size_t)nt;
-    hipLaunchKernelGGL(seqnorm_tile_sums, dim3(nt), dim3(kSnThreads), 0, st, cur, prev,
-                       (unsigned)N, dimx, P, A);
+    return (unsigned)((N + kSnTile - 1) / kSnTile);
+}
+}  // namespace
+
+void launch_seqnorm_tables(const float2 *cur, const float2 *prev, int dimx, int dimy, int P,
+                           void *ws, bool use_profile, hipStream_t st) {
+    const unsigned nt = check_geometry(dimx, dimy, P);
+    const unsigned N = (unsigned)((size_t)dimx * dimy);
+    const SnWs w = carve(ws, nt);
+    hipLaunchKernelGGL(seqnorm_tables, dim3(nt), dim3(kSnThreads), 0, st, cur, prev, N, dimx, P,
+                       nt, w, use_profile ? 1 : 0);
     OF2D_HIP(hipGetLastError());
-    hipLaunchKernelGGL(seqnorm_candidates, dim3(1), dim3(kSnWalk), 0, st, A, nt, H);
+    hipLaunchKernelGGL(seqnorm_check, dim3(1), dim3(kSnScan), 0, st, nt, w, use_profile ? 1 : 0);
     OF2D_HIP(hipGetLastError());
-    hipLaunchKernelGGL(seqnorm_tables, dim3(nt), dim3(kSnThreads), 0, st, cur, prev, (unsigned)N,
-                       dimx, P, H, T);
+    hipLaunchKernelGGL(seqnorm_fix, dim3(std::min(nt, 1024u)), dim3(kSnThreads), 0, st, cur,
+                       prev, N, dimx, P, nt, w);
     OF2D_HIP(hipGetLastError());
-    hipLaunchKernelGGL(seqnorm_walk, dim3(2), dim3(kSnWalk), 0, st, cur, prev, (unsigned)N, dimx,
-                       P, nt, H, T, out, dbg);
+}
+
+void launch_seqnorm_walk(const float2 *cur, const float2 *prev, int dimx, int dimy, int P,
+                         void *ws, float *out, int *dbg, hipStream_t st) {
+    const unsigned nt = check_geometry(dimx, dimy, P);
+    const unsigned N = (unsigned)((size_t)dimx * dimy);
+    hipLaunchKernelGGL(seqnorm_walk, dim3(2), dim3(64), 0, st, cur, prev, N, dimx, P, nt,
+                       carve(ws, nt), out, dbg);
     OF2D_HIP(hipGetLastError());
+}
+
+void launch_seqnorm(const float2 *cur, const float2 *prev, int dimx, int dimy, int P, void *ws,
+                    bool use_profile, float *out, int *dbg, hipStream_t st) {
+    launch_seqnorm_tables(cur, prev, dimx, dimy, P, ws, use_profile, st);
+    launch_seqnorm_walk(cur, prev, dimx, dimy, P, ws, out, dbg, st);
 }
 
 }  // namespace of2d

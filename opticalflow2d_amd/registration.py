@@ -131,17 +131,25 @@ def motion_norms(cur, prev, dims: Sequence[int]):
     """Motion::norm sums of (cur - prev) and of prev exactly as the reference's
     Logger takes them (src/Motion.cpp:42-49, src/Logger.cpp:32-51): float
     running sums in linear order, on the device.  ``cur`` / ``prev`` are
-    float32 ``[dimx*dimy, 2]`` (interleaved x, y per pixel, idx = i + j*dimx).
-    Returns ``(sums float32[2], resolves int32[2])``."""
+    float32 ``[dimx*dimy, 2]`` (interleaved x, y per pixel, idx = i + j*dimx),
+    or ``[npairs, dimx*dimy, 2]`` for a sequence of Logger updates run on one
+    workspace (each predicts the next).  Returns ``(sums float32[..., 2],
+    stats int32[..., 8])``: stats are cost figures of the device walk
+    (include/of2d.h of2d_motion_norms), not results."""
     dimx, dimy = int(dims[0]), int(dims[1])
     c = np.ascontiguousarray(np.asarray(cur, np.float32).reshape(-1))
     p = np.ascontiguousarray(np.asarray(prev, np.float32).reshape(-1))
-    if c.size != 2 * dimx * dimy or p.size != c.size:
-        raise ValueError("cur / prev need dimx*dimy*2 floats")
-    sums = np.zeros(2, np.float32)
-    res = np.zeros(2, np.int32)
+    n = 2 * dimx * dimy
+    if c.size % n or p.size != c.size or c.size == 0:
+        raise ValueError("cur / prev need npairs * dimx*dimy*2 floats")
+    k = c.size // n
+    sums = np.zeros(2 * k, np.float32)
+    res = np.zeros(8 * k, np.int32)
     L = _lib.lib()
-    check(L.of2d_motion_norms(c, p, dimx, dimy, sums, res), L.of2d_gateway_last_error().decode())
+    check(L.of2d_motion_norms(c, p, dimx, dimy, k, sums, res),
+          L.of2d_gateway_last_error().decode())
+    if np.asarray(cur).ndim == 3:
+        return sums.reshape(k, 2), res.reshape(k, 8)
     return sums, res
 
 

@@ -1,0 +1,33 @@
+"""Wall time of convergence-on registrations in the two Logger modes
+(reference-exact float norms, default; fp64 sums, `logger_fp64`).
+
+    python tools/time_convergence.py [n] [reps]
+"""
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from opticalflow2d_amd import ImageRegistration, set_print_sink  # noqa: E402
+from opticalflow2d_amd import synthetic as S  # noqa: E402
+
+set_print_sink(lambda s: None)
+n = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
+reps = int(sys.argv[2]) if len(sys.argv) > 2 else 3
+cases = {"texture": S.texture_pair(n), "procedural": S.procedural_pair(n, 0, n)}
+for name, (ref, mov) in cases.items():
+    for fp64 in (0, 1):
+        with ImageRegistration((n, n), [1000], 0, 0, [0.1], logger_fp64=fp64) as r:
+            r.set_images(ref, mov)
+            r.estimate()  # warm-up
+            ts = []
+            for _ in range(reps):
+                t0 = time.perf_counter()
+                r.estimate()
+                ts.append(time.perf_counter() - t0)
+            it = r.iterations()[0]
+        # the second estimate warm-starts from the first's motion (reference
+        # semantics): iterations of the timed calls, not of the first
+        t = min(ts)
+        print(f"{name:10s} {n}^2 logger_fp64={fp64}: {it} iterations, {t*1e3:.2f} ms "
+              f"({t*1e6/it:.1f} us/iteration)", flush=True)
