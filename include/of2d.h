@@ -199,7 +199,8 @@ int of2d_slab_create_local(of2d_slab **out, int dimx, int dimy, float alpha, int
  * stats (optional, int[8*npairs], cost figures, not results): per pair the
  * tiles the device walk resolved below tile level (|cur - prev|, |prev|), the
  * 64-term segments it stepped term by term (same order), the tiles whose
- * entries were recomputed, 0, 0, 0. */
+ * entries were recomputed, the walk's wall-clock ticks at 100 MHz (same
+ * order) and those of the |cur - prev| walk's resolves. */
 int of2d_motion_norms(const float *cur, const float *prev, int dimx, int dimy, int npairs,
                       float *sums, int *stats);
 

@@ -74,7 +74,7 @@ __device__ __forceinline__ void warp_batch(const float *__restrict__ Imov,
     for (int q = 0; q < B; q++) {
         // bitwise, not short-circuit: no exec-mask branches around the loads
         in[q] = valid[q] & ((unsigned)a[q] < (unsigned)dimx) & ((unsigned)b[q] < (unsigned)dimy);
-        const unsigned idx = in[q] ? (unsigned)(b[q] * P + a[q]) : 0u;
+        const unsigned idx = in[q] ? ((unsigned)b[q] * (unsigned)P + (unsigned)a[q]) : 0u;
         m[q] = u[idx];
         own[q] = Imov[idx];
     }
@@ -91,7 +91,7 @@ __device__ __forceinline__ void warp_batch(const float *__restrict__ Imov,
         ok[q] = in[q] && !(dx < 0 || dx >= dimx || dy < 0 || dy >= dimy);
         ax[q] = dx < dimx - 1;
         ay[q] = dy < dimy - 1;
-        const float *g = Imov + (ok[q] ? (unsigned)(dy * P + dx) : 0u);
+        const float *g = Imov + (ok[q] ? ((unsigned)dy * (unsigned)P + (unsigned)dx) : 0u);
         t00[q] = g[0];
         t10[q] = g[1];
         t01[q] = g[P];
@@ -400,7 +400,7 @@ __device__ __forceinline__ void compose_px(const float2 *__restrict__ u, int i, 
     for (int k = 0; k < G; k++) {
         const int j = j0 + k;
         const bool in = j < dimy;
-        own[k] = u[in ? (unsigned)(j * P + i) : 0u];
+        own[k] = u[in ? ((unsigned)j * (unsigned)P + (unsigned)i) : 0u];
         const float px = (float)i + cv[k].x;
         const int dx = (int)floorf(px);
         fx[k] = px - (float)dx;
@@ -410,7 +410,7 @@ __device__ __forceinline__ void compose_px(const float2 *__restrict__ u, int i, 
         ok[k] = in && !(dx < 0 || dx >= dimx || dy < 0 || dy >= dimy);
         ax[k] = dx < dimx - 1;
         ay[k] = dy < dimy - 1;
-        const float2 *b = u + (ok[k] ? (unsigned)(dy * P + dx) : 0u);
+        const float2 *b = u + (ok[k] ? ((unsigned)dy * (unsigned)P + (unsigned)dx) : 0u);
         t00[k] = b[0];
         t10[k] = b[1];
         t01[k] = b[P];
@@ -568,7 +568,7 @@ __global__ __launch_bounds__(256) OF2D_DEMONS_FUSED_ATTR void demons_fused_kerne
         const int s = tid + 256 * q, r = s / WW, cc = s - r * WW;
         const int i = x0 - c + cc, j = y0 - c + r;
         const bool ok = (s < WW * CH) & (cc < CW) & ((unsigned)j < (unsigned)dimy);
-        const float t = Iref[ok ? (unsigned)(j * P + i) : 0u];
+        const float t = Iref[ok ? ((unsigned)j * (unsigned)P + (unsigned)i) : 0u];
         iref[q] = ok ? t : 0.0f;
     }
     __syncthreads();

@@ -199,7 +199,7 @@ __device__ __forceinline__ float warp_px(const float *__restrict__ src, float2 m
     const float fy = py - (float)dy;
     const bool ok = !(dx < 0 || dx >= dimx || dy < 0 || dy >= dimy);
     const bool ax = dx < dimx - 1, ay = dy < dimy - 1;
-    const float *b = src + (ok ? (unsigned)(dy * P + dx) : 0u);
+    const float *b = src + (ok ? ((unsigned)dy * (unsigned)P + (unsigned)dx) : 0u);
     const float t00 = b[0], t10 = b[1], t01 = b[P], t11 = b[P + 1];
     float val = (t00 * (1 - fx)) * (1 - fy);
     float w = (1 - fx) * (1 - fy);
@@ -280,7 +280,7 @@ __device__ __forceinline__ float2 accumulate_px(const float2 *__restrict__ mo, f
     const float fy = py - (float)dy;
     const bool ok = !(dx < 0 || dx >= dimx || dy < 0 || dy >= dimy);
     const bool ax = dx < dimx - 1, ay = dy < dimy - 1, axy = ax && ay;
-    const float2 *b = mo + (ok ? (unsigned)(dy * P + dx) : 0u);
+    const float2 *b = mo + (ok ? ((unsigned)dy * (unsigned)P + (unsigned)dx) : 0u);
     const float2 t00 = b[0], t10 = b[1], t01 = b[P], t11 = b[P + 1];
     float vx = (t00.x * (1 - fx)) * (1 - fy);
     float vy = (t00.y * (1 - fx)) * (1 - fy);

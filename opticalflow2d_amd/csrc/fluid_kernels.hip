@@ -592,7 +592,7 @@ __global__ __launch_bounds__(256) void regrid_pack_kernel(
     for (int k = 0; k < NK; k++) {
         const int j = j0 + 4 * k + threadIdx.y;
         okk[k] = i < dimx && j < dimy;
-        const int idx = okk[k] ? j * P + i : 0;
+        const unsigned idx = okk[k] ? (unsigned)j * (unsigned)P + (unsigned)i : 0u;
         const bool yl = j == 0, yr = !yl && j == dimy - 1;
         ia[k] = Ia[okk[k] ? (xr ? idx : idx + 1) : 0];
         ib[k] = Ia[okk[k] ? (xl ? idx : idx - 1) : 0];
@@ -759,7 +759,7 @@ __global__ __launch_bounds__(256) void fluid_step_kernel(
         const bool corner = (r == 0 || r == TH - 1) && (c == 0 || c == TW - 1);
         okq[q] = s < TW * TH && !corner && (unsigned)i < (unsigned)dimx &&
                  (unsigned)j < (unsigned)dimy;
-        const unsigned idx = okq[q] ? (unsigned)(j * P + i) : 0u;
+        const unsigned idx = okq[q] ? ((unsigned)j * (unsigned)P + (unsigned)i) : 0u;
         mu[q] = u[idx];
         mr[q] = R[idx];
     }
@@ -781,7 +781,7 @@ __global__ __launch_bounds__(256) void fluid_step_kernel(
     for (int k = 0; k < NK; k++) {
         const int j = j0 + 4 * k + threadIdx.y;
         okk[k] = i < dimx && j < dimy;
-        const unsigned idx = okk[k] ? (unsigned)(j * P + i) : 0u;
+        const unsigned idx = okk[k] ? ((unsigned)j * (unsigned)P + (unsigned)i) : 0u;
         pvk[k] = kPrev ? prev[idx] : u[idx];
         gk[k] = dI[idx];
         itk[k] = It[idx];

@@ -24,6 +24,12 @@ namespace of2d {
 constexpr int kPitchAlign = 128;  // elements
 
 inline int pitch_for(int dimx) { return (dimx + kPitchAlign - 1) / kPitchAlign * kPitchAlign; }
+// a pitched field of dimy + 2 * ghost j-lines (plus the alignment slack) has
+// fewer than 2^32 elements: the gather kernels' unsigned 32-bit offsets hold
+inline bool field_fits_u32(int dimx, int dimy, int ghost) {
+    return ((unsigned long long)dimy + 2ull * ghost) * (unsigned long long)pitch_for(dimx) +
+               kPitchAlign < (1ull << 32);
+}
 
 struct DeviceError : std::runtime_error {
     using std::runtime_error::runtime_error;

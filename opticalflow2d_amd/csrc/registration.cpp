@@ -88,6 +88,10 @@ Registration::Registration(int dimx, int dimy, int nscales, const int *niter, in
     if (reg < 0 || reg > 5) throw std::invalid_argument("Error: invalid regularisation given\n");
     if (dimx <= 0 || dimy <= 0 || nscales < 0)
         throw std::invalid_argument("Error: invalid image dimensions\n");
+    // the kernels index a field's elements with 32-bit unsigned offsets (the
+    // reference's own indices are unsigned int, src/Field.tpp:13)
+    if (!field_fits_u32(dimx, dimy, 3))
+        throw std::invalid_argument("Error: image too large (a field must have < 2^32 elements)\n");
     niter_.assign(niter, niter + nscales + 1);
     params_.assign(params, params + nparams);
     // ImageRegistration.cpp:56-61: dim(dimin.x/scale, dimin.y/scale) with float scale

@@ -197,6 +197,18 @@ __device__ __forceinline__ T wave_reduce(T v, Op op) {
     return v;
 }
 
+// sum over the wave (values whose total fits 32 bits): DPP inclusive scan,
+// the total read from lane 63
+__device__ __forceinline__ unsigned wave_sum(unsigned v) {
+    v += (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, true);  // row_shr:1
+    v += (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, true);  // row_shr:2
+    v += (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, true);  // row_shr:4
+    v += (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, true);  // row_shr:8
+    v += (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, true);  // row_bcast:15
+    v += (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, true);  // row_bcast:31
+    return (unsigned)__builtin_amdgcn_readlane((int)v, 63);
+}
+
 struct SnWs {
     double *A;              // [nt][2] fp64 tile sums
     unsigned *H;            // [nt][2] headers
@@ -261,13 +273,34 @@ __device__ void sn_tile_tables(const float2 *__restrict__ cur, const float2 *__r
     bool tbad[2][kSnCand] = {};
     double fs[2] = {0.0, 0.0};
     unsigned long long zm[2] = {0ull, 0ull};
-    // segment s = kSnThreads/64 * r + w: 64 consecutive terms per wave and round
-    unsigned L = b * (unsigned)kSnTile + 64u * w + lane;
-    unsigned j = L / (unsigned)dimx, i = L - j * (unsigned)dimx;
+    // segment s = kSnThreads/64 * r + w: 64 consecutive terms per wave and
+    // round; every round's loads are issued before the first is used
+    float2 cv[kSnRounds], pv[kSnRounds];
+    {
+        unsigned L = b * (unsigned)kSnTile + 64u * w + lane;
+        unsigned j = L / (unsigned)dimx, i = L - j * (unsigned)dimx;
+#pragma unroll
+        for (int r = 0; r < kSnRounds; r++) {
+            cv[r] = pv[r] = make_float2(0.0f, 0.0f);
+            if (L < N) {
+                const size_t off = (size_t)j * (size_t)P + i;
+                cv[r] = cur[off];
+                pv[r] = prev[off];
+            }
+            L += kSnThreads;
+            i += kSnThreads;
+            while (i >= (unsigned)dimx) {
+                i -= (unsigned)dimx;
+                j++;
+            }
+        }
+    }
+#pragma unroll
     for (int r = 0; r < kSnRounds; r++) {
         const int s = (kSnThreads / 64) * r + w;
         double d[2];
-        sn_terms(cur, prev, L, N, i, j, P, d[0], d[1]);
+        d[0] = sn_mag(cv[r].x - pv[r].x, cv[r].y - pv[r].y);  // Field::operator- (Field.tpp:305-334)
+        d[1] = sn_mag(pv[r].x, pv[r].y);
 #pragma unroll
         for (int n = 0; n < 2; n++) {
             if (FIRST) {
@@ -282,17 +315,11 @@ __device__ void sn_tile_tables(const float2 *__restrict__ cur, const float2 *__r
                 tacc[n][c] = sn_sat(tacc[n][c], m);
                 tbad[n][c] |= bad;
                 if (seg[n]) {  // 64 of them fit in 32 bits
-                    const unsigned t = wave_reduce(m, [](unsigned a, unsigned x) { return a + x; });
+                    const unsigned t = wave_sum(m);
                     const unsigned e = (t < kSnSat ? t : kSnSat) | (__ballot(bad) ? kSnBad : 0u);
                     if (lane == 0) ws.G[g_index(b, n, c, s)] = e;
                 }
             }
-        }
-        L += kSnThreads;
-        i += kSnThreads;
-        while (i >= (unsigned)dimx) {
-            i -= (unsigned)dimx;
-            j++;
         }
     }
     __shared__ unsigned st[2][kSnCand][kSnThreads / 64];

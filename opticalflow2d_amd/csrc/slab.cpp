@@ -331,6 +331,8 @@ static int slab_create(of2d_slab **out, int dimx, int dimy, float alpha, int ran
             throw std::invalid_argument("slab: bad rank/nranks");
         s->nrows = s->re - s->rb;
         if (s->nrows < 3) throw std::invalid_argument("slab: fewer than 3 j-lines per rank");
+        if (!of2d::field_fits_u32(dimx, s->nrows, 3))
+            throw std::invalid_argument("slab: a field must have < 2^32 elements");
         s->dimx = dimx;
         s->dimy = dimy;
         s->rank = rank;

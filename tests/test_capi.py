@@ -116,3 +116,22 @@ def test_slab_bounds_rejects_bad_args(of2d_lib):
 
 def test_version(of2d_lib):
     assert b"gfx950" in of2d_lib.of2d_version()
+
+
+@pytest.mark.parametrize("dims,ok", [((65536, 65520), True), ((65536, 65530), False),
+                                     ((70000, 70000), False), ((100000, 1), True)])
+def test_field_size_guard(of2d_lib, dims, ok):
+    """Fields are indexed with unsigned 32-bit offsets in the gather kernels
+    (the reference's indices are unsigned int, src/Field.tpp:13): a grid whose
+    pitched field (+ 3 ghost j-lines each side) reaches 2^32 elements is
+    refused at create, before any device work."""
+    from opticalflow2d_amd import ImageRegistration, InvalidArgument, set_print_sink
+    set_print_sink(lambda s: None)
+    try:
+        if ok:
+            ImageRegistration(dims, [1], 0, 0, [0.1]).close()
+        else:
+            with pytest.raises(InvalidArgument, match="2\\^32"):
+                ImageRegistration(dims, [1], 0, 0, [0.1])
+    finally:
+        set_print_sink(None)
