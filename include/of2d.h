@@ -93,6 +93,12 @@ int of2d_last_errors(const of2d_ctx *ctx, float *out, int cap);
  *   "device" (>=0): HIP device ordinal, must be set before of2d_set_images
  *   "hs_gradients_from_image" (-1 auto = default, 0, 1): as for the slab
  *   solver (of2d_slab_set_option); bit-identical results either way
+ *   "ngpus" (1 = default .. 16): Horn-Schunck levels run as that many row
+ *   slabs, rank r on device (device + r) mod count, in this process (halos and
+ *   the Logger's running sums cross the ranks by peer copies; the pyramid,
+ *   warps and accumulation stay on the registration's device).  Results are
+ *   the one-device results bit for bit with the default Logger norms.  Levels
+ *   with fewer j-lines than ranks run on one device.
  *   "logger_fp64" (0 = default / 1): 0 computes the Logger norms as the
  *   reference does (float running sums, of2d_motion_norms), so the break of
  *   ImageRegistrationOpticalFlow.cpp:131-134 falls on the reference's
@@ -105,6 +111,8 @@ int of2d_set_option(of2d_ctx *ctx, const char *key, double value);
  * Mode is keyed on (nlhs, nrhs, singleton present) exactly like mexFunction:
  *   init (0,8,no)  prhs = {[dimx dimy], niter, nscales, reg, regparams,
  *                          nparams, nrefine, verbose}
+ *   init (0,9,no)  the same plus ngpus (of2d_set_option "ngpus"): not in the
+ *                  reference, which has no multi-device mode
  *   register (0,2,yes) prhs = {Iref, Imov}
  *   get (1,0,yes)  plhs[0] = double [dimx*dimy*2]
  *   warp (1,1,yes) prhs = {Imov}, plhs[0] = double [dimx*dimy]

@@ -217,8 +217,9 @@ int of2d_gateway_output_dims(int nlhs, int nrhs, size_t *dims, int *ndims) {
 const char *of2d_gateway_last_error(void) { return g_gateway_err.c_str(); }
 
 int of2d_gateway(int nlhs, double **plhs, int nrhs, const double *const *prhs) {
-    // init (:23-83)
-    if (nlhs == 0 && nrhs == 8 && g_single == nullptr) {
+    // init (:23-83); a ninth input (this library's, not the reference's) is
+    // the number of devices HS runs on (of2d_set_option "ngpus")
+    if (nlhs == 0 && (nrhs == 8 || nrhs == 9) && g_single == nullptr) {
         const int dimx = (int)prhs[0][0], dimy = (int)prhs[0][1];
         const int nscales = (int)prhs[2][0];
         if (nscales < 0) {
@@ -237,6 +238,14 @@ int of2d_gateway(int nlhs, double **plhs, int nrhs, const double *const *prhs) {
         int rc = of2d_create(&c, dimx, dimy, niter.data(), nscales, reg, rp.data(), nparams,
                              nrefine, verbose);
         if (rc != OF2D_OK) return rc;  // message already in g_gateway_err
+        if (nrhs == 9) {
+            rc = of2d_set_option(c, "ngpus", prhs[8][0]);
+            if (rc != OF2D_OK) {
+                g_gateway_err = c->err;
+                of2d_destroy(c);
+                return rc;
+            }
+        }
         g_single = c;
         g_dimx = dimx;
         g_dimy = dimy;

@@ -222,8 +222,20 @@ void launch_seqnorm(const float2 *cur, const float2 *prev, int dimx, int dimy, i
 // on the same workspace wrote)
 void launch_seqnorm_tables(const float2 *cur, const float2 *prev, int dimx, int dimy, int P,
                            void *ws, bool use_profile, hipStream_t st);
+// s_in (optional, device float[2]): the exact running sums of the terms
+// before this grid — a row slab's norms continue its predecessor's
 void launch_seqnorm_walk(const float2 *cur, const float2 *prev, int dimx, int dimy, int P,
-                         void *ws, float *out, int *dbg, hipStream_t st);
+                         void *ws, const float *s_in, float *out, int *dbg, hipStream_t st);
+// launch_seqnorm_tables in parts for row slabs: the pass over the slab, its
+// fp64 total (returned: device double[2] inside ws), the predecessors' totals
+// summed in rank order (device pointers, peer-readable), and the check / fix
+// with that offset (p_off, device double[2], optional)
+void launch_seqnorm_pass(const float2 *cur, const float2 *prev, int dimx, int dimy, int P,
+                         void *ws, bool use_profile, hipStream_t st);
+const double *seqnorm_total(int dimx, int dimy, int P, void *ws, hipStream_t st);
+void launch_seqnorm_offsets(const double *const *totals, int r, double *out, hipStream_t st);
+void launch_seqnorm_refine(const float2 *cur, const float2 *prev, int dimx, int dimy, int P,
+                           void *ws, bool use_profile, const double *p_off, hipStream_t st);
 
 // ---------------------------------------------------------------- fields
 void launch_d2f(const double *in, int dimx, int dimy, float *out, int P, int row_offset,

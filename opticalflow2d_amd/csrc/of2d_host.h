@@ -21,6 +21,7 @@
 namespace of2d {
 
 struct DemonsKernels;
+struct MultiHS;
 void print(const char *fmt, ...) __attribute__((format(printf, 1, 2)));
 
 // ------------------------------------------------------------ device buffer
@@ -163,6 +164,12 @@ class Registration {
     int loop_fluid(Level &L, int niter);
     int loop_elastic(Level &L, int niter, int &final_buf);
     int loop_curvature(Level &L, int niter, int &final_buf);
+    // HS over ngpus_ row slabs in this process (ranks.cpp)
+    int loop_hs_multi(int s, float alpha, int &final_buf);
+    MultiHS &multi_for(int s);
+    void multi_release();
+    int ngpus_ = 1;
+    std::vector<std::shared_ptr<MultiHS>> lv_multi_;
     void check_status();
     void check_reported_status(unsigned st);
 

@@ -139,6 +139,7 @@ Registration::Registration(int dimx, int dimy, int nscales, const int *niter, in
 }
 
 Registration::~Registration() {
+    multi_release();
     if (d_stage_) (void)hipFree(d_stage_);
     if (d_partial_) (void)hipFree(d_partial_);
     if (d_sums_) (void)hipFree(d_sums_);
@@ -163,6 +164,12 @@ void Registration::set_option(const std::string &key, double v) {
         fixed_ = v != 0;
     else if (key == "logger_fp64")
         logger_fp64_ = v != 0;
+    else if (key == "ngpus") {
+        if (v < 1 || v > kMaxLocalRanks)
+            throw std::invalid_argument("option 'ngpus' must be in [1, 16]");
+        if ((int)v != ngpus_) multi_release();
+        ngpus_ = (int)v;
+    }
     else if (key == "chunk") {
         if (ready_) throw std::invalid_argument("option 'chunk' must be set before first use");
         chunk_ = std::max(1, (int)v);
@@ -285,11 +292,14 @@ void Registration::estimate_level(int s) {
     for (int refine = 0; refine < nrefine_; refine++) {
         // *Iaux = *Imov; Iaux->warp2d(*motion)
         launch_warp(L.Imov.p, L.cur_motion(), L.Iaux.p, L.dx, L.dy, L.P, st_);
-        if (!demons) launch_gradients(L.Iref.p, L.Iaux.p, L.dI.p, L.It.p, L.dx, L.dy, L.P, st_);
+        // HS over several devices: the ranks take their gradients themselves
+        const bool multi = reg_ == 0 && ngpus_ > 1 && L.dy >= ngpus_;
+        if (!demons && !multi)
+            launch_gradients(L.Iref.p, L.Iaux.p, L.dI.p, L.It.p, L.dx, L.dy, L.P, st_);
         L.est[0].zero(st_);  // motion_est starts at zero (reset() at :141 / new Motion)
         int fin = 0, it = 0;
         switch (reg_) {
-            case 0: it = loop_hs(L, niter, params_[0], fin); break;
+            case 0: it = multi ? loop_hs_multi(s, params_[0], fin) : loop_hs(L, niter, params_[0], fin); break;
             case 1: it = loop_curvature(L, niter, fin); break;
             case 2: it = loop_elastic(L, niter, fin); break;
             case 3:
@@ -355,7 +365,7 @@ int Registration::run_chunked_exact(Level &L, int niter, int nb, const StepFn &s
             OF2D_HIP(hipEventRecord(ev_fix_[t & 3], sn_st_));
             OF2D_HIP(hipStreamWaitEvent(wk_st_, ev_fix_[t & 3], 0));
             launch_seqnorm_walk(L.est[dst].p, L.est[src].p, L.dx, L.dy, L.P, d_seqws_[w].p,
-                                d_seq_.p + 2 * (size_t)t, nullptr, wk_st_);
+                                nullptr, d_seq_.p + 2 * (size_t)t, nullptr, wk_st_);
             OF2D_HIP(hipEventRecord(ev_walk_[t & 3], wk_st_));
         }
         OF2D_HIP(hipStreamWaitEvent(st_, ev_walk_[(C - 1) & 3], 0));

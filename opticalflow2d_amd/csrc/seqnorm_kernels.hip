@@ -220,6 +220,7 @@ struct SnWs {
     float *tot;             // [2][2] the last two totals per norm (the walk)
     unsigned *list;         // [nt] tiles seqnorm_check listed for seqnorm_fix
     unsigned *cnt;          // [4] list length
+    double *tot64;          // [2] fp64 total of this call (seqnorm_total: a slab's offset)
 };
 // The profile of the last call that predicts norm n: its own, except for
 // |prev| after a call whose prev was zero (the Logger's first update), whose
@@ -390,7 +391,8 @@ __global__ __launch_bounds__(kSnThreads) void seqnorm_tables(const float2 *__res
 // alone (1/16 either side).  A tile whose entries miss one is listed for new
 // tile entries (pending); a tile across which the sum may change binade is
 // listed for segment entries (the walk resolves it).
-__global__ __launch_bounds__(kSnScan) void seqnorm_check(unsigned nt, SnWs ws, int use_prof) {
+__global__ __launch_bounds__(kSnScan) void seqnorm_check(unsigned nt, SnWs ws, int use_prof,
+                                                         const double *__restrict__ p_off) {
     const unsigned chunk = (nt + kSnScan - 1) / kSnScan;
     const unsigned b0 = threadIdx.x * chunk;
     const unsigned b1 = min(nt, b0 + chunk);
@@ -420,11 +422,16 @@ __global__ __launch_bounds__(kSnScan) void seqnorm_check(unsigned nt, SnWs ws, i
         const double f = ws.prof[(size_t)s * (nt + 1) + b], q = ws.Pp[(size_t)s * (nt + 1) + b];
         return (q > 0.0 && f > 0.0 && f < INFINITY) ? f / q : 1.0;
     };
+    // threads past the last tile (nt < kSnScan) read nothing: prof / Pp hold
+    // nt + 1 entries
+    const bool active = b0 < b1;
     for (int n = 0; n < 2; n++) {
         src[n] = prof_src(ws, n);
-        Pb[n] = threadIdx.x ? sh[n][threadIdx.x - 1] : 0.0;
-        drift[n] = drift_at(src[n], b0);
-        dend[n] = drift_at(src[n], b1);  // the next thread's first tile
+        // p_off: the fp64 sum of the terms before this grid (a row slab's
+        // predecessors), so that the prediction is of the global running sum
+        Pb[n] = (threadIdx.x ? sh[n][threadIdx.x - 1] : 0.0) + (p_off ? p_off[n] : 0.0);
+        drift[n] = active ? drift_at(src[n], b0) : 1.0;
+        dend[n] = active ? drift_at(src[n], b1) : 1.0;  // the next thread's first tile
     }
     __syncthreads();  // these reads of the last call's Pp before this call's writes
     for (unsigned b = b0; b < b1; b++) {
@@ -454,6 +461,33 @@ __global__ __launch_bounds__(kSnScan) void seqnorm_check(unsigned nt, SnWs ws, i
     }
     if (b1 == nt && b0 < b1)
         for (int n = 0; n < 2; n++) ws.Pp[(size_t)n * (nt + 1) + nt] = Pb[n];
+}
+
+// fp64 total of the tile sums (a slab's contribution to its successors' p_off)
+__global__ __launch_bounds__(256) void seqnorm_total(unsigned nt, SnWs ws) {
+    double s[2] = {0.0, 0.0};
+    for (unsigned b = threadIdx.x; b < nt; b += 256)
+        for (int n = 0; n < 2; n++) s[n] += ws.A[2 * (size_t)b + n];
+    __shared__ double sh[2][4];
+    for (int n = 0; n < 2; n++) {
+        const double t = wave_reduce(s[n], [](double a, double x) { return a + x; });
+        if ((threadIdx.x & 63) == 0) sh[n][threadIdx.x / 64] = t;
+    }
+    __syncthreads();
+    if (threadIdx.x < 2) ws.tot64[threadIdx.x] = sh[threadIdx.x][0] + sh[threadIdx.x][1] +
+                                                  sh[threadIdx.x][2] + sh[threadIdx.x][3];
+}
+
+struct RankTotals {
+    const double *p[kMaxLocalRanks];
+};
+// out[n] = sum of the totals of ranks 0 .. r-1 (rank order)
+__global__ void seqnorm_offsets(RankTotals t, int r, double *__restrict__ out) {
+    if (threadIdx.x < 2) {
+        double s = 0.0;
+        for (int q = 0; q < r; q++) s += t.p[q][threadIdx.x];
+        out[threadIdx.x] = s;
+    }
 }
 
 // the listed tiles: new tile entries and / or segment entries
@@ -611,6 +645,7 @@ constexpr int kSnAhead = 8;  // windows loaded per step: the next step's loads h
 __global__ __launch_bounds__(64) void seqnorm_walk(const float2 *__restrict__ cur,
                                                    const float2 *__restrict__ prev, unsigned N,
                                                    int dimx, int P, unsigned nt, SnWs ws,
+                                                   const float *__restrict__ s_in,
                                                    float *__restrict__ out,
                                                    int *__restrict__ dbg) {
     const int n = blockIdx.x;  // 0: |cur - prev|, 1: |prev|
@@ -633,7 +668,9 @@ __global__ __launch_bounds__(64) void seqnorm_walk(const float2 *__restrict__ cu
             }
         }
     };
-    float S = 0.0f;
+    // s_in: the exact sum of the terms before this grid (the previous row
+    // slab's result), 0 without one
+    float S = s_in ? s_in[n] : 0.0f;
     int resolves = 0;
     int raw = 0;
     bool nan = false;  // non-finite sum: a NaN magnitude after it
@@ -720,7 +757,7 @@ size_t seqnorm_workspace_bytes(int dimx, int dimy) {
                  2 * kSnCand * sizeof(unsigned) + 2 * kSnCand * kSnSegs * sizeof(unsigned) +
                  sizeof(unsigned)) +
            2 * (nt + 1) * (sizeof(double) + sizeof(float)) + 4 * sizeof(float) +
-           4 * sizeof(unsigned) + 256;
+           4 * sizeof(unsigned) + 2 * sizeof(double) + 256;
 }
 
 namespace {
@@ -736,6 +773,8 @@ SnWs carve(void *ws, unsigned nt) {
     w.tot = w.prof + 2 * (size_t)(nt + 1);
     w.list = reinterpret_cast<unsigned *>(w.tot + 4);
     w.cnt = w.list + nt;
+    w.tot64 = reinterpret_cast<double *>(
+        (reinterpret_cast<uintptr_t>(w.cnt + 4) + 7) & ~static_cast<uintptr_t>(7));
     return w;
 }
 unsigned check_geometry(int dimx, int dimy, int P) {
@@ -746,34 +785,64 @@ unsigned check_geometry(int dimx, int dimy, int P) {
 }
 }  // namespace
 
-void launch_seqnorm_tables(const float2 *cur, const float2 *prev, int dimx, int dimy, int P,
-                           void *ws, bool use_profile, hipStream_t st) {
+void launch_seqnorm_pass(const float2 *cur, const float2 *prev, int dimx, int dimy, int P,
+                         void *ws, bool use_profile, hipStream_t st) {
     const unsigned nt = check_geometry(dimx, dimy, P);
     const unsigned N = (unsigned)((size_t)dimx * dimy);
     const SnWs w = carve(ws, nt);
     hipLaunchKernelGGL(seqnorm_tables, dim3(nt), dim3(kSnThreads), 0, st, cur, prev, N, dimx, P,
                        nt, w, use_profile ? 1 : 0);
     OF2D_HIP(hipGetLastError());
-    hipLaunchKernelGGL(seqnorm_check, dim3(1), dim3(kSnScan), 0, st, nt, w, use_profile ? 1 : 0);
+}
+
+const double *seqnorm_total(int dimx, int dimy, int P, void *ws, hipStream_t st) {
+    const unsigned nt = check_geometry(dimx, dimy, P);
+    const SnWs w = carve(ws, nt);
+    hipLaunchKernelGGL(seqnorm_total, dim3(1), dim3(256), 0, st, nt, w);
+    OF2D_HIP(hipGetLastError());
+    return w.tot64;
+}
+
+void launch_seqnorm_offsets(const double *const *totals, int r, double *out, hipStream_t st) {
+    if (r < 0 || r > kMaxLocalRanks) throw std::invalid_argument("launch_seqnorm_offsets: rank");
+    RankTotals t{};
+    for (int q = 0; q < r; q++) t.p[q] = totals[q];
+    hipLaunchKernelGGL(seqnorm_offsets, dim3(1), dim3(64), 0, st, t, r, out);
+    OF2D_HIP(hipGetLastError());
+}
+
+void launch_seqnorm_refine(const float2 *cur, const float2 *prev, int dimx, int dimy, int P,
+                           void *ws, bool use_profile, const double *p_off, hipStream_t st) {
+    const unsigned nt = check_geometry(dimx, dimy, P);
+    const unsigned N = (unsigned)((size_t)dimx * dimy);
+    const SnWs w = carve(ws, nt);
+    hipLaunchKernelGGL(seqnorm_check, dim3(1), dim3(kSnScan), 0, st, nt, w, use_profile ? 1 : 0,
+                       p_off);
     OF2D_HIP(hipGetLastError());
     hipLaunchKernelGGL(seqnorm_fix, dim3(std::min(nt, 1024u)), dim3(kSnThreads), 0, st, cur,
                        prev, N, dimx, P, nt, w);
     OF2D_HIP(hipGetLastError());
 }
 
+void launch_seqnorm_tables(const float2 *cur, const float2 *prev, int dimx, int dimy, int P,
+                           void *ws, bool use_profile, hipStream_t st) {
+    launch_seqnorm_pass(cur, prev, dimx, dimy, P, ws, use_profile, st);
+    launch_seqnorm_refine(cur, prev, dimx, dimy, P, ws, use_profile, nullptr, st);
+}
+
 void launch_seqnorm_walk(const float2 *cur, const float2 *prev, int dimx, int dimy, int P,
-                         void *ws, float *out, int *dbg, hipStream_t st) {
+                         void *ws, const float *s_in, float *out, int *dbg, hipStream_t st) {
     const unsigned nt = check_geometry(dimx, dimy, P);
     const unsigned N = (unsigned)((size_t)dimx * dimy);
     hipLaunchKernelGGL(seqnorm_walk, dim3(2), dim3(64), 0, st, cur, prev, N, dimx, P, nt,
-                       carve(ws, nt), out, dbg);
+                       carve(ws, nt), s_in, out, dbg);
     OF2D_HIP(hipGetLastError());
 }
 
 void launch_seqnorm(const float2 *cur, const float2 *prev, int dimx, int dimy, int P, void *ws,
                     bool use_profile, float *out, int *dbg, hipStream_t st) {
     launch_seqnorm_tables(cur, prev, dimx, dimy, P, ws, use_profile, st);
-    launch_seqnorm_walk(cur, prev, dimx, dimy, P, ws, out, dbg, st);
+    launch_seqnorm_walk(cur, prev, dimx, dimy, P, ws, nullptr, out, dbg, st);
 }
 
 }  // namespace of2d

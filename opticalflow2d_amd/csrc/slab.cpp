@@ -72,6 +72,9 @@ struct of2d_slab {
     int chunk_cap() const { return chunk > chunk_fixed ? chunk : chunk_fixed; }
     int fin = 0;    // buffer holding the final motion
     int start = 0;  // zeroed buffer the next run starts from (motion_est->reset())
+    // a run began and has not re-zeroed `start` (it threw midway): the next
+    // run zeroes it first
+    bool start_dirty = false;
     // the triple kernel takes the gradients from Iaux (= Imov) instead of dI:
     // -1 by slab size (of2d::hs3_gradients_from_image), 0 / 1 forced
     int gi = -1;
@@ -445,6 +448,7 @@ int of2d_slab_set_images(of2d_slab *s, const double *Iref_rows, const double *Im
         for (auto &f : s->u) f.zero(s->st);
         s->fin = 0;
         s->start = 0;
+        s->start_dirty = false;
         // the triple kernel's division range and the reference's divide-by-zero
         // test (coord2d.h:95-100), once per image pair: dI is fixed for every
         // iteration of every run on these images, so the test each iteration
@@ -560,7 +564,9 @@ int of2d_slab_run(of2d_slab *s, int niter, int fixed_iters, int *iters_done) {
         OF2D_HIP(hipStreamWaitEvent(s->comm_st, s->ev_int, 0));
         OF2D_HIP(hipEventRecord(s->ev_edge, s->comm_st));
         // motion_est starts at zero: buffer `start` was zeroed by set_images or
-        // at the end of the previous run (below)
+        // at the end of the previous run (below), unless that run threw midway
+        if (s->start_dirty) s->u[s->start].zero(s->st);
+        s->start_dirty = true;
         int a = s->start, k0 = 0, done = -1;
         while (k0 < niter && done < 0) {
             const int C = std::min(fixed_iters ? s->chunk_fixed : s->chunk, niter - k0);
@@ -663,6 +669,7 @@ int of2d_slab_run(of2d_slab *s, int niter, int fixed_iters, int *iters_done) {
         // behind ev1 and is not waited for here
         s->start = (s->fin + 2) % 3;
         s->u[s->start].zero(s->st);
+        s->start_dirty = false;
         OF2D_HIP(hipEventSynchronize(s->ev1));
         float ms = 0.0f;
         OF2D_HIP(hipEventElapsedTime(&ms, s->ev0, s->ev1));

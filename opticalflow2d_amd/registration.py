@@ -87,7 +87,8 @@ def OpticalFlow2d(*args, nargout: int = 0):
     """The MEX function, mode for mode (WrapperOpticalFlow2d.cpp:23-151).
 
     ``OpticalFlow2d([dimx, dimy], niter, nscales, reg, params, nparams, nrefine, verbose)``
-        initialise the process-global registration object;
+        initialise the process-global registration object (a ninth argument,
+        not in the reference: the number of devices Horn-Schunck runs on);
     ``OpticalFlow2d(Iref, Imov)``      register (estimate motion);
     ``OpticalFlow2d(nargout=1)``       return the motion field ``[dimx, dimy, 2]``;
     ``OpticalFlow2d(Imov, nargout=1)`` return Imov warped by the motion;
@@ -101,7 +102,7 @@ def OpticalFlow2d(*args, nargout: int = 0):
     keep = [np.ascontiguousarray(np.asarray(a, dtype=np.float64).reshape(-1, order="F"))
             for a in args]
     n_img = int(L.of2d_gateway_output_numel(1, 1))  # 0 when no singleton exists
-    if nargout == 0 and nrhs == 8 and n_img == 0:
+    if nargout == 0 and nrhs in (8, 9) and n_img == 0:
         nscales = int(keep[2][0]) if keep[2].size else 0
         nparams = int(keep[5][0]) if keep[5].size else 0
         if keep[0].size < 2 or keep[1].size < nscales + 1 or keep[4].size < nparams:
@@ -161,7 +162,7 @@ class ImageRegistration:
     values, finest level first), ``nscales``, ``reg``, ``params`` (nparams
     floats), ``nrefine``, ``verbose``.  Extra keyword options map to
     ``of2d_set_option`` (``fixed_iters``, ``chunk``, ``device``,
-    ``hs_gradients_from_image``, ``logger_fp64``).
+    ``hs_gradients_from_image``, ``logger_fp64``, ``ngpus``).
     """
 
     def __init__(self, dims: Sequence[int], niter: Sequence[int], nscales: int, reg: int,

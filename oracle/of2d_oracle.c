@@ -637,12 +637,21 @@ int oracle_hs_loop_mt(float *uf, const float *dIf, const float *It, int dimx, in
     const unsigned dx = (unsigned)dimx, dy = (unsigned)dimy, n = dx * dy;
     v2 *u = (v2 *)uf;
     const v2 *dI = (const v2 *)dIf;
+    const int nt = nthreads > 0 ? nthreads : 1;
     v2 *q = (v2 *)malloc(n * sizeof(v2)), *prev = (v2 *)calloc(n, sizeof(v2));
-    float *part = (float *)calloc(2 * (size_t)(nthreads > 0 ? nthreads : 1), sizeof(float));
-    if (!q || !prev || !part) return -1;
+    float *part = (float *)calloc(2 * (size_t)nt, sizeof(float));
+    if (!q || !prev || !part) {
+        free(q);
+        free(prev);
+        free(part);
+        return -1;
+    }
     const float alphasq = alpha * alpha;
     for (int it = 0; it < niter; it++) {
-#pragma omp parallel num_threads(nthreads)
+        /* slots of threads the runtime did not start stay 0 (OMP_DYNAMIC,
+         * thread limits): every slot is reset per iteration */
+        memset(part, 0, 2 * (size_t)nt * sizeof(float));
+#pragma omp parallel num_threads(nt)
         {
 #pragma omp for schedule(static)
             for (unsigned j = 0; j < dy; j++)
@@ -674,7 +683,7 @@ int oracle_hs_loop_mt(float *uf, const float *dIf, const float *It, int dimx, in
             part[2 * t + 1] = sp;
         }
         float sd = 0.0f, sp = 0.0f;
-        for (int t = 0; t < (nthreads > 0 ? nthreads : 1); t++) {
+        for (int t = 0; t < nt; t++) {
             sd += part[2 * t];
             sp += part[2 * t + 1];
         }

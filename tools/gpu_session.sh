@@ -1,6 +1,7 @@
 #!/bin/bash
-# Round-3 GPU session runner: tools/gpu_r03.sh <tag> <step>...
-#   steps: tests (all gpu tests), conv (tools/time_convergence.py),
+# GPU session runner (one gpurun call): tools/gpu_session.sh <tag> <step>...
+#   steps: tests (all gpu tests), sntests / ranks (Logger-norm / multi-device
+#          tests), diag (tools/seqnorm_diag.py), conv (tools/time_convergence.py),
 #          convprof (rocprofv3 kernel stats of conv), smoke, bench, prof (bench
 #          under rocprofv3), cfgs (bench_configs.py)
 # Stops at the first step that faults / aborts / times out (rc > 1).
@@ -21,6 +22,7 @@ step() {  # step <name> <timeout> <cmd...>
 }
 for s in "$@"; do
     case $s in
+        ranks) step ranks 600 python -u -m pytest tests/test_gpu_ranks.py -x -v --timeout 300 --timeout-method thread; rc=$?; [ $rc -le 1 ] || exit $rc ;;
         sntests) step sntests 600 python -u -m pytest tests/test_gpu_seqnorm.py tests/test_gpu_convergence.py -x -q --timeout 300 --timeout-method thread; rc=$?; [ $rc -le 1 ] || exit $rc ;;
         tests) step tests 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread; rc=$?; [ $rc -le 1 ] || exit $rc ;;
         diag) step diag 600 python -u tools/seqnorm_diag.py 4096 8 || exit $? ;;
