@@ -26,7 +26,12 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 
+NO_CPU = False
+
+
 def oracle_time(dims, niter, nscales, reg, params, ref, mov, fixed=True):
+    if NO_CPU:
+        return float("nan"), [0] * len(niter)
     from oracle import oracle as O
     O.lib().oracle_capture_output(1)
     O.lib().oracle_set_reference_loop_order(1)
@@ -151,7 +156,10 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--configs", default="1,3,4,5")
     ap.add_argument("--iters", type=int, default=0, help="override iteration counts")
+    ap.add_argument("--no-cpu", action="store_true", help="skip the oracle samples (A/B runs)")
     a = ap.parse_args()
+    global NO_CPU
+    NO_CPU = a.no_cpu
     from opticalflow2d_amd import set_print_sink
     set_print_sink(lambda s: None)
     for c in a.configs.split(","):

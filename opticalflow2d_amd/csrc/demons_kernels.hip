@@ -49,6 +49,13 @@ constexpr int kCThreadsY = 4;
 constexpr int kCr = OF2D_DEMONS_CR;
 // warped slots per thread per gather batch of the fused kernel (tools/ A/B
 // builds override it)
+// stage ablation of the fused kernel (tools/demons_abl.sh; TIMING ONLY, the
+// results are wrong): 1 no bilinear warp (the tile reads Imov at the pixel),
+// 2 no force (the correction is the gradient), 3 no sigma_fluid convolution,
+// 4 no composition (the update is an addition)
+#ifndef OF2D_DEMONS_ABL
+#define OF2D_DEMONS_ABL 0
+#endif
 #ifndef OF2D_DEMONS_BW
 #define OF2D_DEMONS_BW 6
 #endif
@@ -328,6 +335,14 @@ __device__ __forceinline__ bool conv_px(const float2 *tile, const ConvArgs &a, i
     return true;
 }
 
+// every tap of the R pixels (i, j0..j0+R-1) has its linear index in [0, N)
+template <int KW, int R>
+__device__ __forceinline__ bool conv_rows_interior(int i, int j0, int dimx, int dimy, long N) {
+    constexpr int c = KW > 0 ? (KW - 1) / 2 : 0;
+    const long lin0 = (long)j0 * dimx + i, linl = (long)(j0 + R - 1) * dimx + i;
+    return j0 + R - 1 < dimy && lin0 - c - (long)c * dimx >= 0 && linl + c + (long)c * dimx < N;
+}
+
 // The convolution at R consecutive j-lines j0..j0+R-1 of column i.  When the
 // width is known and all R pixels are interior, the R + 2c tile values of
 // each tap column are read once and shared by the R outputs (each output
@@ -341,8 +356,7 @@ __device__ __forceinline__ void convR(const float2 *tile, const ConvArgs &a, int
                                       bool has[R]) {
     if constexpr (KW > 0) {
         constexpr int c = (KW - 1) / 2, TW = kCx + 2 * c;
-        const long lin0 = (long)j0 * dimx + i, linl = (long)(j0 + R - 1) * dimx + i;
-        if (j0 + R - 1 < dimy && lin0 - c - (long)c * dimx >= 0 && linl + c + (long)c * dimx < N) {
+        if (conv_rows_interior<KW, R>(i, j0, dimx, dimy, N)) {
             v2f acc[R];
 #pragma unroll
             for (int k = 0; k < R; k++) acc[k] = v2f{0.0f, 0.0f};
@@ -547,7 +561,16 @@ __global__ __launch_bounds__(256) OF2D_DEMONS_FUSED_ATTR void demons_fused_kerne
                 b[q] = y0 - c - 1 + r;
                 valid[q] = q0 + q < NW && s < WW * WH;
             }
-            warp_batch<BW>(Imov, u, a, b, valid, dimx, dimy, P, res, in);
+            if (OF2D_DEMONS_ABL == 1) {
+#pragma unroll
+                for (int q = 0; q < BW; q++) {
+                    in[q] = valid[q] && (unsigned)a[q] < (unsigned)dimx &&
+                            (unsigned)b[q] < (unsigned)dimy;
+                    res[q] = Imov[in[q] ? ((unsigned)b[q] * (unsigned)P + (unsigned)a[q]) : 0u];
+                }
+            } else {
+                warp_batch<BW>(Imov, u, a, b, valid, dimx, dimy, P, res, in);
+            }
 #pragma unroll
             for (int q = 0; q < BW; q++)
                 if (valid[q]) wt[tid + 256 * (q0 + q)] = in[q] ? res[q] : 0.0f;
@@ -586,8 +609,10 @@ __global__ __launch_bounds__(256) OF2D_DEMONS_FUSED_ATTR void demons_fused_kerne
                 if (s < WW * CH && cc < CW) {
                     const float *w = wt + (r + 1) * WW + (cc + 1);
                     const float gx = (w[1] - w[-1]) / 2.0f, gy = (w[WW] - w[-WW]) / 2.0f;
-                    ct[r * CW + cc] = demons_corr<FAST>(gx, gy, w[0] - iref[q], sigma_isq, sxq,
-                                                        zero);
+                    ct[r * CW + cc] = OF2D_DEMONS_ABL == 2
+                                          ? make_float2(gx, gy + (w[0] - iref[q]))
+                                          : demons_corr<FAST>(gx, gy, w[0] - iref[q], sigma_isq,
+                                                              sxq, zero);
                 }
             }
         } else {
@@ -628,19 +653,30 @@ __global__ __launch_bounds__(256) OF2D_DEMONS_FUSED_ATTR void demons_fused_kerne
     const int r0 = (int)__builtin_amdgcn_readfirstlane(threadIdx.y) * R;
     float2 sm[R];
     bool has[R];
-    convR<KW, R, true, FAST>(ct, ca, i, y0 + r0, threadIdx.x, r0, dimx, dimy, N, sm, has);
+    if (OF2D_DEMONS_ABL == 3) {
+#pragma unroll
+        for (int k = 0; k < R; k++) has[k] = false;
+    } else {
+        convR<KW, R, true, FAST>(ct, ca, i, y0 + r0, threadIdx.x, r0, dimx, dimy, N, sm, has);
+    }
     float2 cv[R];
 #pragma unroll
     for (int k = 0; k < R; k++) {
         cv[k] = make_float2(0.0f, 0.0f);
         if (y0 + r0 + k < dimy) cv[k] = has[k] ? sm[k] : ct[(r0 + k + c) * CW + threadIdx.x + c];
     }
-    store_update<R>(u, out, i, y0 + r0, dimx, dimy, P, cv, mode);
+    store_update<R>(u, out, i, y0 + r0, dimx, dimy, P, cv, OF2D_DEMONS_ABL == 4 ? 1 : mode);
 }
 
 // u_new = u_mid (*) G(sigma_diffusion); Logger partials sum ||u_new - prev||,
-// sum ||prev|| per block (fixed order)
-template <int KW, int R = kCr, bool PK = true, bool W1 = false>
+// sum ||prev|| per block (fixed order).  The partials feed the fp64 Logger
+// mode only (fixed iterations, logger_fp64; the default mode takes the
+// reference's float sums from seqnorm_kernels.hip and launches NORM = false):
+// an approximation of Motion::norm's float running sum at any precision, so
+// the magnitudes take the hardware square root (<= 1 ulp) rather than the
+// correctly rounded sequence.  The R previous-motion loads of a thread are
+// issued together after the convolution, whose registers they reuse.
+template <int KW, int R = kCr, bool PK = true, bool W1 = false, bool NORM = true>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KW == 7 ? 7 : 8))) void smooth_norm_kernel(const float2 *__restrict__ umid,
                                                           const float2 *__restrict__ prev,
                                                           float2 *__restrict__ out, int dimx,
@@ -656,22 +692,35 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KW == 7 ? 7
     double sd = 0.0, sp = 0.0;
     if (i < dimx) {
         const int r0 = (int)__builtin_amdgcn_readfirstlane(threadIdx.y) * R;
+        const int j0 = y0 + r0;
         float2 sm[R];
         bool has[R];
-        convR<KW, R, PK, W1>(tile, a, i, y0 + r0, threadIdx.x, r0, dimx, dimy, N, sm, has);
+        convR<KW, R, PK, W1>(tile, a, i, j0, threadIdx.x, r0, dimx, dimy, N, sm, has);
+        // every output of the thread is the convolution's: no fallback loads
+        // of u_mid (the loads below are skipped by branch, not by select)
+        const bool conv_all = W1 && KW > 0 && conv_rows_interior<KW, R>(i, j0, dimx, dimy, N);
+        float2 pv[R];
+        if (NORM) {
+#pragma unroll
+            for (int k = 0; k < R; k++)
+                pv[k] = prev[j0 + k < dimy ? (unsigned)(j0 + k) * (unsigned)P + (unsigned)i : 0u];
+        }
 #pragma unroll
         for (int k = 0; k < R; k++) {
-            const int j = y0 + r0 + k;
+            const int j = j0 + k;
             if (j >= dimy) break;
-            const long idx = (long)j * P + i;
-            const float2 v = has[k] ? sm[k] : umid[idx];
+            const unsigned idx = (unsigned)j * (unsigned)P + (unsigned)i;
+            float2 v = sm[k];
+            if (!conv_all && !has[k]) v = umid[idx];
             out[idx] = v;
-            const float2 pv = prev[idx];
-            const float ex = v.x - pv.x, ey = v.y - pv.y;
-            sd += (double)__builtin_sqrtf(ex * ex + ey * ey);
-            sp += (double)__builtin_sqrtf(pv.x * pv.x + pv.y * pv.y);
+            if (NORM) {
+                const float ex = v.x - pv[k].x, ey = v.y - pv[k].y;
+                sd += (double)__builtin_amdgcn_sqrtf(ex * ex + ey * ey);
+                sp += (double)__builtin_amdgcn_sqrtf(pv[k].x * pv[k].x + pv[k].y * pv[k].y);
+            }
         }
     }
+    if (!NORM) return;
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) {
         sd += __shfl_down(sd, off);
@@ -815,6 +864,20 @@ void launch_smooth_norm(const float2 *umid, const float2 *prev, float2 *out, int
                            conv_lds_bytes(c, c), st, umid, prev, out, dimx, dimy, P, a, partial);
     };
     const bool w1 = (float)wfull == 1.0f;
+    // no partials wanted (the Logger's float sums come from seqnorm): no norms
+    if (!partial) {
+        switch (w1 ? kw : -kw) {
+            case 3: go(smooth_norm_kernel<3, kCr, true, true, false>); break;
+            case -3: go(smooth_norm_kernel<3, kCr, true, false, false>); break;
+            case 5: go(smooth_norm_kernel<5, kCr, true, true, false>); break;
+            case -5: go(smooth_norm_kernel<5, kCr, true, false, false>); break;
+            case 7: go(smooth_norm_kernel<7, kCr, true, true, false>); break;
+            case -7: go(smooth_norm_kernel<7, kCr, true, false, false>); break;
+            default: go(smooth_norm_kernel<0, kCr, true, false, false>); break;
+        }
+        OF2D_HIP(hipGetLastError());
+        return;
+    }
     switch (w1 ? kw : -kw) {
         case 3: go(smooth_norm_kernel<3, kCr, true, true>); break;
         case -3: go(smooth_norm_kernel<3>); break;

@@ -490,9 +490,16 @@ int of2d_slab_run(of2d_slab *s, int niter, int fixed_iters, int *iters_done) {
         const float *ia = use_gi(s) ? s->Imov.p : nullptr;
         auto src_of = [](int a, int t) { return t == 0 ? a : (t % 2 == 1 ? (a + 1) % 3 : (a + 2) % 3); };
         auto dst_of = [](int a, int t) { return t % 2 == 0 ? (a + 1) % 3 : (a + 2) % 3; };
-        // st runs after the latest edge launches / comm_st after the latest st work
-        auto join_st = [&] { OF2D_HIP(hipStreamWaitEvent(s->st, s->ev_edge, 0)); };
-        auto mark_st = [&] { OF2D_HIP(hipEventRecord(s->ev_int, s->st)); };
+        // st runs after the latest edge launches / comm_st after the latest st
+        // work.  Only split launches use comm_st: without them a wait and a
+        // record around every launch would put two barrier packets between
+        // consecutive kernels (~4-6 us per launch)
+        auto join_st = [&] {
+            if (G.split) OF2D_HIP(hipStreamWaitEvent(s->st, s->ev_edge, 0));
+        };
+        auto mark_st = [&] {
+            if (G.split) OF2D_HIP(hipEventRecord(s->ev_int, s->st));
+        };
         auto win3 = [&](hipStream_t st, int in, int out, int jlo, int jhi, int rpw, int slot,
                         double *p1, double *p2, double *p3) {
             of2d::launch_hs_jacobi3_window(s->u[in].p, s->u[out].p, s->dI.p, s->It.p, s->P,

@@ -121,6 +121,9 @@ int Registration::loop_demons(Level &L, int niter, int &final_buf) {
     }
     const int nb = conv_nblocks(L.dx, L.dy);
     const int nparts = 256;
+    // the default Logger mode sums the reference's float norms itself
+    // (run_chunked_exact): the smoothing pass then computes no partials
+    const bool partials = !exact_norms();
     return run_chunked(
         L, niter, nb,
         [&](const float2 *src, float2 *dst, double *partial) {
@@ -141,7 +144,7 @@ int Registration::loop_demons(Level &L, int niter, int &final_buf) {
                 umid = L.increment.p;
             }
             launch_smooth_norm(umid, src, dst, L.dx, L.dy, L.P, K.kf + n, K.kd + n, kw,
-                               K.wfull_diff, partial, st_);
+                               K.wfull_diff, partials ? partial : nullptr, st_);
         },
         final_buf);
 }
