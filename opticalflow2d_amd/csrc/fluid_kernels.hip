@@ -273,29 +273,18 @@ struct Flag {
 };
 }  // namespace
 
-// Strip order.  Default: a ticket in claim order, so a strip only waits on a
-// strip already running.  OF2D_SOR_XCD (measured variant): strip from the
-// workgroup id so that each XCD (workgroup w runs on XCD w mod 8) holds a
-// contiguous range of strips and all but 7 hand-offs stay inside one XCD's L2;
-// it relies on every strip being resident at once (ns <= 130 one-wave
-// workgroups at 8192^2), and the bounded spins report a violation.  With
-// OF2D_SOR_XCD_LOCALST a strip whose consumer is on its own XCD publishes with
-// plain stores (the line stays in that L2) instead of sc1 (write-through).
-#ifndef OF2D_SOR_XCD
-#define OF2D_SOR_XCD 0
-#endif
-#ifndef OF2D_SOR_XCD_LOCALST
-#define OF2D_SOR_XCD_LOCALST 0
-#endif
-template <bool LST>
-__device__ __forceinline__ void sor_strip_body(float4 *__restrict__ vb, int dimx, int dimy, int P,
-                                               float A, float B, float M, float ML,
-                                               v4u *__restrict__ H, long Hstride,
-                                               unsigned epoch, int I,
-                                               unsigned *__restrict__ status,
-                                               unsigned long long *__restrict__ trace,
-                                               int nstrips) {
+__global__ __launch_bounds__(64) void sor_strip_kernel(float4 *__restrict__ vb, int dimx, int dimy,
+                                                       int P, float A, float B, float M, float ML,
+                                                       v4u *__restrict__ H, long Hstride,
+                                                       unsigned epoch,
+                                                       unsigned *__restrict__ ticket, int nstrips,
+                                                       unsigned *__restrict__ status,
+                                                       unsigned long long *__restrict__ trace) {
     const int lane = threadIdx.x;
+    __shared__ int s_strip;
+    if (lane == 0) s_strip = (int)(atomicAdd(ticket, 1u) % (unsigned)nstrips);
+    __syncthreads();
+    const int I = __builtin_amdgcn_readfirstlane(s_strip);
     // optional timeline (tools/sor_harness.hip): start, end, polled batches,
     // shader cycles
     const unsigned long long t_start = trace ? __builtin_amdgcn_s_memrealtime() : 0;
@@ -377,7 +366,7 @@ __device__ __forceinline__ void sor_strip_body(float4 *__restrict__ vb, int dimx
             OF2D_SOR_ST_AUX);
         __builtin_amdgcn_raw_buffer_store_b128(
             v4u{__float_as_uint(out.x), __float_as_uint(out.y), epoch, epoch}, ps,
-            voff_pub + (unsigned)j * 16u, 0, LST ? 0 : 16 /* sc1 */);
+            voff_pub + (unsigned)j * 16u, 0, 16 /* sc1 */);
         D = out;
         W0 = W1;
         W1 = W2;
@@ -455,38 +444,6 @@ __device__ __forceinline__ void sor_strip_body(float4 *__restrict__ vb, int dimx
         trace[4 * I + 2] = npoll;
         trace[4 * I + 3] = __builtin_amdgcn_s_memtime() - c_start;
     }
-}
-
-__global__ __launch_bounds__(64) void sor_strip_kernel(float4 *__restrict__ vb, int dimx, int dimy,
-                                                       int P, float A, float B, float M, float ML,
-                                                       v4u *__restrict__ H, long Hstride,
-                                                       unsigned epoch,
-                                                       unsigned *__restrict__ ticket, int nstrips,
-                                                       unsigned *__restrict__ status,
-                                                       unsigned long long *__restrict__ trace) {
-    const int lane = threadIdx.x;
-    __shared__ int s_strip;
-    if (OF2D_SOR_XCD) {
-        // XCD x holds strips [base_x, base_x + count_x), count_x = the
-        // workgroups round-robin dealing gives it
-        const int w = blockIdx.x, x = w % 8, per = nstrips / 8, extra = nstrips % 8;
-        s_strip = x * per + min(x, extra) + w / 8;
-    } else {
-        if (lane == 0) s_strip = (int)(atomicAdd(ticket, 1u) % (unsigned)nstrips);
-        __syncthreads();
-    }
-    const int I = __builtin_amdgcn_readfirstlane(s_strip);
-    bool local = false;  // the consumer (strip I + 1) is on this strip's XCD
-    if (OF2D_SOR_XCD && OF2D_SOR_XCD_LOCALST) {
-        const int per = nstrips / 8, extra = nstrips % 8, x = blockIdx.x % 8;
-        local = I + 1 < x * per + min(x, extra) + per + (x < extra ? 1 : 0);
-    }
-    if (local)
-        sor_strip_body<true>(vb, dimx, dimy, P, A, B, M, ML, H, Hstride, epoch, I, status, trace,
-                             nstrips);
-    else
-        sor_strip_body<false>(vb, dimx, dimy, P, A, B, M, ML, H, Hstride, epoch, I, status, trace,
-                              nstrips);
 }
 
 int sor_nstrips(int dimx) { return dimx < 3 ? 0 : (dimx - 2 + kSorCols - 1) / kSorCols; }

@@ -1,4 +1,6 @@
 cd $GRAFT_REPO_ROOT
+# The OF2D_SOR_XCD / OF2D_SOR_XCD_LOCALST variants live in commit 06bc2d7 (fluid_kernels.hip);
+# not kept: check out that revision to rerun this A/B.
 mkdir -p gpurun_out
 for r in 1 2; do
 for v in base xcd xcdlst; do
