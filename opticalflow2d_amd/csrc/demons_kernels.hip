@@ -119,7 +119,11 @@ __device__ __forceinline__ void warp_batch(const float *__restrict__ Imov,
         const float v11 = val + (t11[q] * gx) * gy, w11 = wt + gx * gy;
         val = axy ? v11 : val;
         wt = axy ? w11 : wt;
-        const float r = val / wt;
+        // val / wt is val itself when wt rounds to exactly 1 (an interior tap
+        // pattern: 99.7 % of the lanes at 4096^2), so the division runs only
+        // for the slot batches in which some lane of the wave needs it
+        float r = val;
+        if (__builtin_expect(__builtin_amdgcn_ballot_w64(ok[q] && wt != 1.0f) != 0, 0)) r = val / wt;
         res[q] = (ok[q] && wt != 0) ? r : (in[q] ? own[q] : 0.0f);
     }
 }
@@ -452,7 +456,10 @@ __device__ __forceinline__ void compose_px(const float2 *__restrict__ u, int i, 
         const float w11 = w + gx * gy;
         v = axy ? v11 : v;
         w = axy ? w11 : w;
-        const float2 q = make_float2(c.x + v.x / w, c.y + v.y / w);
+        // v / w is v itself when w rounds to exactly 1 (as in warp_batch)
+        float2 q = make_float2(c.x + v.x, c.y + v.y);
+        if (__builtin_expect(__builtin_amdgcn_ballot_w64(ok[k] && w != 1.0f) != 0, 0))
+            q = make_float2(c.x + v.x / w, c.y + v.y / w);
         o[k] = ok[k] ? (w != 0 ? q : c) : own[k];
     }
 }
@@ -524,12 +531,19 @@ __global__ __launch_bounds__(256) void smooth_compose_kernel(
     store_update<R>(u, out, i, y0 + r0, dimx, dimy, P, cv, mode);
 }
 
-// K1 + K2 for an x-interior tile (x0 - c >= 0, x0 + 64 + c <= dimx: no tap
-// wraps into another j-line).  1. the warped image over the tile plus a
+// K1 + K2 for a 64 x CY tile.  1. the warped image over the tile plus a
 // (c + 1)-pixel halo into LDS; 2. the correction over the tile plus a c-pixel
 // halo into LDS (the halo is recomputed by the neighbouring tiles); 3. the
 // sigma_fluid convolution and the motion update.  Per pixel the arithmetic of
 // demons_force_kernel + smooth_compose_kernel: bit-identical.
+// Tiles at the x edges hold, in the halo columns past the edge, the pixels the
+// reference's LINEAR tap indices reach there: column x < 0 of j-line y is
+// pixel (x + dimx, y - 1), column x >= dimx is (x - dimx, y + 1) (Field.tpp:254,
+// idx + ii).  Every slot is warped, differentiated and corrected as the pixel
+// it holds (one-sided gradients at that pixel's own borders, whose missing
+// neighbour is exactly the column across the seam), so the convolution reads
+// the reference's tap values from LDS like anywhere else.  Needs one wrap at
+// most: dimx >= 2 * 64 (launch_demons_update).
 // FAST: (float)ca.wfull == 1 and sigma_xsq a power of two whose reciprocal
 // `sxq` carries (convR W1, demons_corr SXP); otherwise `sxq` is sigma_xsq
 template <int KW, int R, bool FAST>
@@ -545,9 +559,17 @@ __global__ __launch_bounds__(256) OF2D_DEMONS_FUSED_ATTR void demons_fused_kerne
     __shared__ __attribute__((aligned(16))) float2 ct[CH * CW];
     const int x0 = ((int)blockIdx.x + bx0) * kCx, y0 = blockIdx.y * CY;
     const int tid = threadIdx.y * 64 + threadIdx.x;
+    // block-uniform: the warped tile crosses an x edge (its slots past it
+    // hold the wrapped pixels)
+    const bool xedge = x0 - c - 1 < 0 || x0 + kCx + c + 1 > dimx;
+    auto wrap = [&](int &x, int &y) __attribute__((always_inline)) {
+        const int lo = x < 0, hi = x >= dimx;
+        x += lo ? dimx : (hi ? -dimx : 0);
+        y += hi - lo;
+    };
     {
-        // 1. slot s <-> pixel (x0 - c - 1 + s % WW, y0 - c - 1 + s / WW), in
-        // batches of BW slots per thread
+        // 1. slot s <-> pixel (x0 - c - 1 + s % WW, y0 - c - 1 + s / WW)
+        // (wrapped), in batches of BW slots per thread
         constexpr int NW = (WW * WH + 255) / 256, BW = OF2D_DEMONS_BW;
 #pragma unroll
         for (int q0 = 0; q0 < NW; q0 += BW) {
@@ -559,6 +581,7 @@ __global__ __launch_bounds__(256) OF2D_DEMONS_FUSED_ATTR void demons_fused_kerne
                 const int s = tid + 256 * (q0 + q), r = s / WW;
                 a[q] = x0 - c - 1 + (s - r * WW);
                 b[q] = y0 - c - 1 + r;
+                if (xedge) wrap(a[q], b[q]);
                 valid[q] = q0 + q < NW && s < WW * WH;
             }
             if (OF2D_DEMONS_ABL == 1) {
@@ -589,7 +612,8 @@ __global__ __launch_bounds__(256) OF2D_DEMONS_FUSED_ATTR void demons_fused_kerne
 #pragma unroll
     for (int q = 0; q < NC; q++) {
         const int s = tid + 256 * q, r = s / WW, cc = s - r * WW;
-        const int i = x0 - c + cc, j = y0 - c + r;
+        int i = x0 - c + cc, j = y0 - c + r;
+        if (xedge) wrap(i, j);
         const bool ok = (s < WW * CH) & (cc < CW) & ((unsigned)j < (unsigned)dimy);
         const float t = Iref[ok ? ((unsigned)j * (unsigned)P + (unsigned)i) : 0u];
         iref[q] = ok ? t : 0.0f;
@@ -620,7 +644,8 @@ __global__ __launch_bounds__(256) OF2D_DEMONS_FUSED_ATTR void demons_fused_kerne
         for (int q = 0; q < NC; q++) {
             const int s = tid + 256 * q, r = s / WW, cc = s - r * WW;
             if (s < WW * CH && cc < CW) {
-                const int i = x0 - c + cc, j = y0 - c + r;
+                int i = x0 - c + cc, j = y0 - c + r;
+                if (xedge) wrap(i, j);
                 float2 cv = make_float2(0.0f, 0.0f);
                 if ((unsigned)j < (unsigned)dimy) {
                     const float *w = wt + (r + 1) * WW + (cc + 1);
@@ -647,9 +672,11 @@ __global__ __launch_bounds__(256) OF2D_DEMONS_FUSED_ATTR void demons_fused_kerne
         if (zero) atomicOr(status, kStatusDivZero);
     }
     __syncthreads();
-    // 3. R consecutive j-lines per thread (every column is inside the image)
+    // 3. R consecutive j-lines per thread (the columns of the tile inside the
+    // image: the last tile may be partial)
     const long N = (long)dimx * dimy;
     const int i = x0 + threadIdx.x;
+    if (i >= dimx) return;  // no barrier follows
     const int r0 = (int)__builtin_amdgcn_readfirstlane(threadIdx.y) * R;
     float2 sm[R];
     bool has[R];
@@ -781,67 +808,26 @@ void launch_smooth_compose(const float2 *corr, const float2 *u, float2 *out, int
     smooth_compose_tiles(corr, u, out, dimx, dimy, P, a, mode, gx, gx, gx, st);
 }
 
-int demons_edge_tiles(int dimx, int kw, int *nl, int *nr) {
-    const int c = (kw - 1) / 2, gx = (dimx + kCx - 1) / kCx;
-    int l = 0, r = 0;
-    while (l < gx && kCx * l - c < 0) l++;
-    while (r < gx - l && kCx * (gx - 1 - r) + kCx + c > dimx) r++;
-    if (nl) *nl = l;
-    if (nr) *nr = r;
-    return gx - l - r;  // x-interior tiles
-}
-
 void launch_demons_update(const float *Iref, const float *Imov, const float2 *u, float2 *corr,
                           float2 *out, int dimx, int dimy, int P, float sigma_isq,
                           float sigma_xsq, const float *kf, const double *kd, int kw,
-                          double wfull, int mode, unsigned *status, hipStream_t st,
-                          hipStream_t side, hipEvent_t ev_fork, hipEvent_t ev_join) {
+                          double wfull, int mode, unsigned *status, hipStream_t st) {
     const int c = (kw - 1) / 2;
     const ConvArgs a{kf, kd, kw, c, c, wfull};
-    int nl = 0, nr = 0;
-    const int ni = demons_edge_tiles(dimx, kw, &nl, &nr);
     const int gx = (dimx + kCx - 1) / kCx;
-    if (!(kw == 3 || kw == 5 || kw == 7) || ni < 2) {
+    // the fused kernel takes every tile, the x-edge ones included, when its
+    // width is compiled in and no tile wraps more than once (dimx >= 128)
+    if (!(kw == 3 || kw == 5 || kw == 7) || dimx < 2 * kCx) {
         launch_demons_force(Iref, Imov, u, corr, dimx, dimy, P, sigma_isq, sigma_xsq, status, st);
         smooth_compose_tiles(corr, u, out, dimx, dimy, P, a, mode, gx, gx, gx, st);
         return;
     }
-    // the edge columns read u, Imov, Iref and write corr and their own columns
-    // of out, disjoint from the fused launch: with a side stream they run
-    // beside it (two small launches, ~10 % of an iteration when serialised)
-    const bool fork = side && ev_fork && ev_join;
-    hipStream_t es = fork ? side : st;
-    // the join: st waits for everything enqueued on the side stream, also when
-    // a launch below throws
-    struct Join {
-        hipStream_t st, side;
-        hipEvent_t ev;
-        bool armed = false;
-        ~Join() {
-            if (armed) {
-                (void)hipEventRecord(ev, side);
-                (void)hipStreamWaitEvent(st, ev, 0);
-            }
-        }
-    } join{st, side, ev_join};
-    if (fork) {
-        OF2D_HIP(hipEventRecord(ev_fork, st));
-        OF2D_HIP(hipStreamWaitEvent(side, ev_fork, 0));
-        join.armed = true;
-    }
-    // the correction the edge tiles' convolutions read: tile columns
-    // [0, nl + 1) and [gx - nr - 1, gx) (wrapped taps reach the far edge)
-    hipLaunchKernelGGL(demons_force_kernel, dim3(nl + nr + 2, (dimy + kFy - 1) / kFy), dim3(64, 4),
-                       0, es, Iref, Imov, u, corr, dimx, dimy, P, sigma_isq, sigma_xsq, status,
-                       nl + 1, gx);
-    OF2D_HIP(hipGetLastError());
-    smooth_compose_tiles(corr, u, out, dimx, dimy, P, a, mode, nl + nr, nl, gx, es);
-    const dim3 g(ni, conv_grid(dimx, dimy).y);
+    const dim3 g(gx, conv_grid(dimx, dimy).y);
     float rsx = 0.0f;
     const bool fast = (float)wfull == 1.0f && pow2_reciprocal(sigma_xsq, &rsx);
     auto go = [&](auto kern) {
         hipLaunchKernelGGL(kern, g, dim3(64, kCThreadsY), 0, st, Iref, Imov, u, out, dimx, dimy, P,
-                           sigma_isq, fast ? rsx : sigma_xsq, a, mode, status, nl);
+                           sigma_isq, fast ? rsx : sigma_xsq, a, mode, status, 0);
     };
     switch (kw * 2 + fast) {
         case 6: go(demons_fused_kernel<3, kCr, false>); break;

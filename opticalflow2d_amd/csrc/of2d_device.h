@@ -276,19 +276,13 @@ dim3 conv_grid(int dimx, int dimy);
 int conv_nblocks(int dimx, int dimy);
 // One correction update (DemonsThirions.cpp:20-38): force, sigma_fluid
 // smoothing and the motion update (mode as launch_smooth_compose) -> out.
-// x-interior tiles run fused (demons_fused_kernel); the edge tile columns
-// go through corr (scratch) with the unfused kernels.
+// One fused launch over every tile (demons_fused_kernel; the x-edge tiles hold
+// the wrapped tap pixels) for kw 3 / 5 / 7 and dimx >= 128; otherwise the
+// unfused kernels through corr (scratch).
 void launch_demons_update(const float *Iref, const float *Imov, const float2 *u, float2 *corr,
                           float2 *out, int dimx, int dimy, int P, float sigma_isq,
                           float sigma_xsq, const float *kf, const double *kd, int kw,
-                          double wfull, int mode, unsigned *status, hipStream_t st,
-                          hipStream_t side = nullptr, hipEvent_t ev_fork = nullptr,
-                          hipEvent_t ev_join = nullptr);
-// (with `side` and two events the edge columns run on `side` beside the fused
-// launch, and st waits for them before its next work)
-// tile columns of the fused update: returns the x-interior count, *nl / *nr
-// the edge columns on the left / right
-int demons_edge_tiles(int dimx, int kw, int *nl, int *nr);
+                          double wfull, int mode, unsigned *status, hipStream_t st);
 // mode 0 Composition, 1 Addition, 2 no update, 3 store the smoothed corr only
 void launch_smooth_compose(const float2 *corr, const float2 *u, float2 *out, int dimx, int dimy,
                            int P, const float *kf, const double *kd, int kw, double wfull,

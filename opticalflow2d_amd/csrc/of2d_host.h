@@ -200,7 +200,6 @@ class Registration {
     int device_ = -1;
     bool ready_ = false;
     hipStream_t st_ = nullptr;
-    hipStream_t side_st_ = nullptr;  // Demons edge columns beside the fused launch
     hipEvent_t ev_fork_ = nullptr, ev_join_ = nullptr;
     double *d_stage_ = nullptr;  // double staging for boundary copies
     size_t stage_count_ = 0;

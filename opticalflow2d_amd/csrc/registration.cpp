@@ -148,7 +148,6 @@ Registration::~Registration() {
     lv_.clear();
     if (ev_fork_) (void)hipEventDestroy(ev_fork_);
     if (ev_join_) (void)hipEventDestroy(ev_join_);
-    if (side_st_) (void)hipStreamDestroy(side_st_);
     if (sn_st_) (void)hipStreamDestroy(sn_st_);
     if (wk_st_) (void)hipStreamDestroy(wk_st_);
     for (int k = 0; k < 4; k++) {
@@ -187,7 +186,6 @@ void Registration::ensure_device() {
     if (ready_) return;
     if (device_ >= 0) OF2D_HIP(hipSetDevice(device_));
     OF2D_HIP(hipStreamCreateWithFlags(&st_, hipStreamNonBlocking));
-    OF2D_HIP(hipStreamCreateWithFlags(&side_st_, hipStreamNonBlocking));
     OF2D_HIP(hipStreamCreateWithFlags(&sn_st_, hipStreamNonBlocking));
     OF2D_HIP(hipStreamCreateWithFlags(&wk_st_, hipStreamNonBlocking));
     for (int k = 0; k < 4; k++) {

@@ -132,8 +132,7 @@ int Registration::loop_demons(Level &L, int niter, int &final_buf) {
             // correspondence itself, then exp() and motion->accumulate)
             launch_demons_update(L.Iref.p, L.Iaux.p, src, L.corr.p, L.tmp.p, L.dx, L.dy, L.P,
                                  sigma_isq, sigma_xsq, K.kf, K.kd, kw, K.wfull_fluid,
-                                 diffeo ? 3 : mode, d_status_, st_, side_st_, ev_fork_,
-                                 ev_join_);
+                                 diffeo ? 3 : mode, d_status_, st_);
             const float2 *umid = L.tmp.p;
             if (diffeo) {
                 float2 *cexp = nullptr;

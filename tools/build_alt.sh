@@ -14,10 +14,16 @@ mkdir -p $T $D/include
 cp include/of2d.h $D/include/
 cp $C/*.h $C/*.hip $C/*.cpp $T/
 for f in "$@"; do git show "$rev:$C/$f" > "$T/$f"; done
+# a replaced header: every object is rebuilt (class layouts must agree)
+allh=0
+for f in "$@"; do case $f in *.h) allh=1;; esac; done
 objs=""
 for o in $C/build/*.o; do
   b=$(basename "$o" .o); src=""
   for f in "$@"; do [ "${f%.*}" = "$b" ] && src=$f; done
+  if [ $allh = 1 ] && [ -z "$src" ]; then
+    for e in hip cpp; do [ -f "$T/$b.$e" ] && src=$b.$e; done
+  fi
   if [ -n "$src" ]; then
     /opt/rocm/bin/hipcc -std=c++17 -O3 -fPIC -ffp-contract=off -Wno-pass-failed --offload-arch=gfx950 \
       -I/opt/rocm/include -munsafe-fp-atomics -x hip -c "$T/$src" -o "$T/$b.o"
