@@ -212,7 +212,10 @@ __device__ __forceinline__ float warp_px(const float *__restrict__ src, float2 m
     const float v11 = val + (t11 * fx) * fy, w11 = w + fx * fy;
     val = (ax && ay) ? v11 : val;
     w = (ax && ay) ? w11 : w;
-    const float q = val / w;
+    // val / w is val itself when w rounds to exactly 1 (demons_kernels.hip
+    // warp_batch): divide only in the waves where some lane needs it
+    float q = val;
+    if (__builtin_expect(__builtin_amdgcn_ballot_w64(ok && w != 1.0f) != 0, 0)) q = val / w;
     return (ok && w != 0) ? q : own;
 }
 __global__ void warp_kernel(const float *__restrict__ src, const float2 *__restrict__ u,
@@ -300,7 +303,9 @@ __device__ __forceinline__ float2 accumulate_px(const float2 *__restrict__ mo, f
     vx = axy ? x11 : vx;
     vy = axy ? y11 : vy;
     w = axy ? w11 : w;
-    const float2 q = make_float2(c.x + vx / w, c.y + vy / w);
+    float2 q = make_float2(c.x + vx, c.y + vy);  // vx / 1.0f is vx
+    if (__builtin_expect(__builtin_amdgcn_ballot_w64(ok && w != 1.0f) != 0, 0))
+        q = make_float2(c.x + vx / w, c.y + vy / w);
     return ok ? (w != 0 ? q : c) : own;
 }
 __global__ void accumulate_kernel(const float2 *__restrict__ mo, const float2 *__restrict__ v,

@@ -571,15 +571,19 @@ __device__ __forceinline__ void progress_prio(int done, int total) {
 // the same ghost j-lines as u (rows glo .. ghi-1 readable).  Worth it when dI
 // and It do not stay resident in the 256 MB MALL between launches (the
 // launchers' callers decide, of2d_device.h hs3_gradients_from_image).
+// MID: the two intermediate iterates u1, u2 of the owned rows are stored too
+// (to m1, m2): the reference-exact Logger needs every iterate in memory
+// (registration.cpp run_chunked_exact), 16 B/px more per launch.
 template <int ROWS, int WAVES, bool XCD = true, int MINB = 1, int UNR = 4, int PRIO = 0,
-          bool ALT = false, bool GI = false>
+          bool ALT = false, bool GI = false, bool MID = false>
 __global__ __launch_bounds__(64 * WAVES, MINB) void jacobi3_kernel(
     const float2 *__restrict__ uo, float2 *__restrict__ un, const float2 *__restrict__ dI,
     const float *__restrict__ It, int P, int dimx, int nrows, int row0, int dimy, float alphasq,
     int glo, int ghi, double *__restrict__ partial, double *__restrict__ partial2,
     double *__restrict__ partial3, unsigned *__restrict__ status, int band0, int gx, int gy,
     int rows = ROWS, const unsigned *__restrict__ range_flag = nullptr, int jlo = -1,
-    int jhi = -1, const float *__restrict__ Ia = nullptr) {
+    int jhi = -1, const float *__restrict__ Ia = nullptr, float2 *__restrict__ m1 = nullptr,
+    float2 *__restrict__ m2 = nullptr) {
     int bx = (int)blockIdx.x, by = (int)blockIdx.y;
     if constexpr (XCD) {
         if (!xcd_block(gx, gy, bx, by)) return;
@@ -782,6 +786,22 @@ __global__ __launch_bounds__(64 * WAVES, MINB) void jacobi3_kernel(
         Row<2> vj1 = S(1, uj, uj1, uj2, gj1, bx_);
         Row<2> wm1 = S(-1, p0, p1, vj, gm1, bx_);
         Row<2> wj = S(0, p1, vj, vj1, gj, bx_);
+        // an owned row of an intermediate iterate (MID)
+        auto stmid = [&](float2 *m, int sp, const Row<2> &v) __attribute__((always_inline)) {
+            float2 *dst = m + (long)J(sp) * P + x;
+            if (x + 2 <= dimx)
+                *reinterpret_cast<float4 *>(dst) =
+                    make_float4(v.v[0].x, v.v[0].y, v.v[1].x, v.v[1].y);
+            else
+                dst[0] = v.v[0];
+        };
+        if constexpr (MID) {
+            if (own) {
+                stmid(m1, 0, vj);
+                if (n > 1) stmid(m1, 1, vj1);
+                stmid(m2, 0, wj);
+            }
+        }
         Row<2> nu = ldu(J(3));
         G ng;
         if constexpr (GI) {
@@ -815,6 +835,10 @@ __global__ __launch_bounds__(64 * WAVES, MINB) void jacobi3_kernel(
             const Row<2> vj2 = S(sp + 2, uj1, uj2, a3, gj2, b1);  // u1
             const Row<2> wj1 = S(sp + 1, vj, vj1, vj2, gj1, b1);  // u2
             const Row<2> z = S(sp, wm1, wj, wj1, gj, b3);         // u3
+            if (MID && own) {
+                if (sp + 2 < n) stmid(m1, sp + 2, vj2);
+                if (sp + 1 < n) stmid(m2, sp + 1, wj1);
+            }
             if (own) {
                 norms(vj, uj, s1d, s1p);
                 norms(wj, vj, s2d, s2p);

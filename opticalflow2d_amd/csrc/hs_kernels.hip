@@ -66,14 +66,20 @@ void launch_hs_jacobi2(const float2 *u_old, float2 *u_new, const float2 *dI, con
 static const auto kHsJacobi3 = &hs::jacobi3_kernel<0, kHs3Waves, true, 4, 4, 1, true>;
 // the same with the gradients derived from Iaux in the kernel (GI: 24 B/px)
 static const auto kHsJacobi3I = &hs::jacobi3_kernel<0, kHs3Waves, true, 4, 4, 1, true, true>;
+// both, storing the intermediate iterates too (MID: +16 B/px)
+static const auto kHsJacobi3M =
+    &hs::jacobi3_kernel<0, kHs3Waves, true, 4, 4, 1, true, false, true>;
+static const auto kHsJacobi3IM =
+    &hs::jacobi3_kernel<0, kHs3Waves, true, 4, 4, 1, true, true, true>;
 
 void launch_hs_jacobi3(const float2 *u_old, float2 *u_new, const float2 *dI, const float *It,
                        int P, int dimx, int nrows, int row0, int dimy, float alphasq, int glo,
                        int ghi, double *partial, double *partial2, double *partial3,
                        unsigned *status, const unsigned *range_flag, hipStream_t st,
-                       int band_lo, int band_hi, const float *Ia) {
+                       int band_lo, int band_hi, const float *Ia, float2 *u1, float2 *u2) {
     if (P % kHsStrip != 0 || nrows <= 0 || dimx > P || dimx < 2 || glo > -1 || ghi < nrows + 1)
         throw std::invalid_argument("launch_hs_jacobi3: bad geometry");
+    if (!u1 != !u2) throw std::invalid_argument("launch_hs_jacobi3: u1 and u2 go together");
     if (!range_flag) throw std::invalid_argument("launch_hs_jacobi3: no range flag");
     const int nb = hs3_nbands(dimx, nrows);
     if (band_lo < 0) band_lo = 0;
@@ -83,10 +89,11 @@ void launch_hs_jacobi3(const float2 *u_old, float2 *u_new, const float2 *dI, con
     dim3 g = hs3_grid(dimx, nrows);
     g.y = band_hi - band_lo;
     const dim3 gl(8 * ((g.x * g.y + 7) / 8));
-    hipLaunchKernelGGL(Ia ? kHsJacobi3I : kHsJacobi3, gl, dim3(64 * kHs3Waves), 0, st, u_old,
-                       u_new, dI, It, P, dimx, nrows, row0, dimy, alphasq, glo, ghi, partial,
-                       partial2, partial3, status, band_lo, (int)g.x, (int)g.y,
-                       hs3_rows(dimx, nrows), range_flag, -1, -1, Ia);
+    const auto kern = u1 ? (Ia ? kHsJacobi3IM : kHsJacobi3M) : (Ia ? kHsJacobi3I : kHsJacobi3);
+    hipLaunchKernelGGL(kern, gl, dim3(64 * kHs3Waves), 0, st, u_old, u_new, dI, It, P, dimx,
+                       nrows, row0, dimy, alphasq, glo, ghi, partial, partial2, partial3, status,
+                       band_lo, (int)g.x, (int)g.y, hs3_rows(dimx, nrows), range_flag, -1, -1, Ia,
+                       u1, u2);
     OF2D_HIP(hipGetLastError());
 }
 
@@ -107,7 +114,7 @@ int launch_hs_jacobi3_window(const float2 *u_old, float2 *u_new, const float2 *d
     hipLaunchKernelGGL(Ia ? kHsJacobi3I : kHsJacobi3, gl, dim3(64 * kHs3Waves), 0, st, u_old,
                        u_new, dI, It, P, dimx, nrows, row0, dimy, alphasq, glo, ghi, partial,
                        partial2, partial3, status, slot_band0, gx, gy, rows_per_wave, range_flag,
-                       jlo, jhi, Ia);
+                       jlo, jhi, Ia, nullptr, nullptr);
     OF2D_HIP(hipGetLastError());
     return gy;
 }

@@ -155,7 +155,10 @@ void launch_hs_jacobi3(const float2 *u_old, float2 *u_new, const float2 *dI, con
                        int P, int dimx, int nrows, int row0, int dimy, float alphasq, int glo,
                        int ghi, double *partial, double *partial2, double *partial3,
                        unsigned *status, const unsigned *range_flag, hipStream_t st,
-                       int band_lo = -1, int band_hi = -1, const float *Ia = nullptr);
+                       int band_lo = -1, int band_hi = -1, const float *Ia = nullptr,
+                       float2 *u1 = nullptr, float2 *u2 = nullptr);
+// (u1, u2 non-null: the first two iterates of the owned rows are stored there
+// too, for the reference-exact Logger; +16 B/px)
 // Once per gradient field, before the triple kernel runs on it
 // (hs_jacobi_impl.h hs_precheck_kernel): zeroes *range_flag, then sets it if
 // any gradient / denominator of the allocation [base, base + count) lies

@@ -117,7 +117,7 @@ struct Level {
     Field<float2> motion[2];
     int mcur = 0;
     Field<float2> dI;
-    Field<float2> est[5];  // [3], [4]: only for the exact-norm loop's ring
+    Field<float2> est[9];  // [3] .. [8]: only for the exact-norm loop's ring
     Field<float2> force, velocity, increment, corr, tmp;
     DevArray<double> cbuf[2];              // Curvature: two x|y double plane pairs (pitch P)
     DevArray<double> cC1T, cC0, cD1T, cD0;  // Curvature: REDFT10 / REDFT01 matrices
@@ -151,12 +151,15 @@ class Registration {
                                        double *partial2)>;
     using StepFn3 = std::function<void(const float2 *src, float2 *dst, double *partial,
                                        double *partial2, double *partial3)>;
+    // three iterations in one pass, every iterate stored (d1, d2, d3)
+    using StepFn3M =
+        std::function<void(const float2 *src, float2 *d1, float2 *d2, float2 *d3)>;
 
    private:
     // nblk[k]: block partials written by step (k = 0), step2 (1), step3 (2)
     int run_chunked(Level &L, int niter, int nb, const StepFn &step, int &final_buf,
                     const StepFn2 &step2 = nullptr, const StepFn3 &step3 = nullptr,
-                    const int *nblk = nullptr);
+                    const int *nblk = nullptr, const StepFn3M &step3m = nullptr);
     void ensure_device();
     void estimate_level(int s);
     int loop_hs(Level &L, int niter, float alpha, int &final_buf);
@@ -186,12 +189,15 @@ class Registration {
     // enqueue the exact norms of one Logger update into d_seq_[2t], [2t + 1]
     // (synchronous loops: Elastic, Fluid; workspace 0, on st_)
     void seqnorm(const Level &L, const float2 *cur, const float2 *prev, int t);
-    // run_chunked with the reference's float norms: single steps into a ring
-    // of four buffers; each iteration's tables on sn_st_ and walk on wk_st_,
+    // run_chunked with the reference's float norms: every iterate in memory
+    // (single steps into a ring of four buffers, or with step3m triples into a
+    // ring of eight); each iteration's tables on sn_st_ and walk on wk_st_,
     // alternating between two workspaces
-    int run_chunked_exact(Level &L, int niter, int nb, const StepFn &step, int &final_buf);
+    int run_chunked_exact(Level &L, int niter, int nb, const StepFn &step, int &final_buf,
+                          const StepFn3M &step3m = nullptr);
     hipStream_t sn_st_ = nullptr, wk_st_ = nullptr;
-    hipEvent_t ev_step_[4] = {}, ev_fix_[4] = {}, ev_walk_[4] = {};
+    static constexpr int kExactEv = 16;  // event ring (> ring buffers + 3)
+    hipEvent_t ev_step_[kExactEv] = {}, ev_fix_[kExactEv] = {}, ev_walk_[kExactEv] = {};
     DevArray<unsigned char> d_seqws_[2];  // seqnorm workspaces (level 0 size)
     DevArray<float> d_seq_;               // per-iteration exact sums of a chunk
     int seq_dx_[2] = {0, 0}, seq_dy_[2] = {0, 0};  // grid of each workspace's last call

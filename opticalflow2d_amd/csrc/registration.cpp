@@ -150,7 +150,7 @@ Registration::~Registration() {
     if (ev_join_) (void)hipEventDestroy(ev_join_);
     if (sn_st_) (void)hipStreamDestroy(sn_st_);
     if (wk_st_) (void)hipStreamDestroy(wk_st_);
-    for (int k = 0; k < 4; k++) {
+    for (int k = 0; k < kExactEv; k++) {
         if (ev_step_[k]) (void)hipEventDestroy(ev_step_[k]);
         if (ev_fix_[k]) (void)hipEventDestroy(ev_fix_[k]);
         if (ev_walk_[k]) (void)hipEventDestroy(ev_walk_[k]);
@@ -188,7 +188,7 @@ void Registration::ensure_device() {
     OF2D_HIP(hipStreamCreateWithFlags(&st_, hipStreamNonBlocking));
     OF2D_HIP(hipStreamCreateWithFlags(&sn_st_, hipStreamNonBlocking));
     OF2D_HIP(hipStreamCreateWithFlags(&wk_st_, hipStreamNonBlocking));
-    for (int k = 0; k < 4; k++) {
+    for (int k = 0; k < kExactEv; k++) {
         OF2D_HIP(hipEventCreateWithFlags(&ev_step_[k], hipEventDisableTiming));
         OF2D_HIP(hipEventCreateWithFlags(&ev_fix_[k], hipEventDisableTiming));
         OF2D_HIP(hipEventCreateWithFlags(&ev_walk_[k], hipEventDisableTiming));
@@ -209,7 +209,7 @@ void Registration::ensure_device() {
         L.motion[0].alloc(L.dx, L.dy);
         L.motion[1].alloc(L.dx, L.dy);
         L.dI.alloc(L.dx, L.dy);
-        for (auto &e : L.est) e.alloc(L.dx, L.dy);
+        for (int b = 0; b < 3; b++) L.est[b].alloc(L.dx, L.dy);  // [3..]: exact-norm ring
         solvers::alloc_level(L, reg_);
         maxnb = std::max(maxnb, (size_t)solvers::max_partial_blocks(L, reg_));
     }
@@ -322,51 +322,64 @@ void Registration::seqnorm(const Level &L, const float2 *cur, const float2 *prev
 }
 
 // The chunked loop of run_chunked with the reference's float norms.  Every
-// iterate must be in memory for its norms, so the iterations run as single
-// steps into a ring of the four buffers other than the chunk's start buffer a
-// (kept for a replay).  The norms of iteration t run behind step t on two
-// streams: the bandwidth passes (seqnorm tables, sn_st_) and the
-// latency-bound walk (wk_st_), on workspace t mod 2, whose last walk (t - 2)
-// also predicts them (its profile).  Step t + 4 reuses t's buffer and waits
-// for the walk of t + 1, the last reader of t's iterate.
+// iterate must be in memory for its norms: single steps write a ring of the
+// four buffers other than the chunk's start buffer a (kept for a replay), or,
+// with step3m (HS), triples write all three of their iterates into a ring of
+// eight.  The norms of iteration t run behind its step on two streams: the
+// bandwidth passes (seqnorm tables, sn_st_) and the latency-bound walk
+// (wk_st_), on workspace t mod 2, whose last walk (t - 2) also predicts them
+// (its profile).  Iterate t's buffer is next written by iterate t + R (R the
+// ring size), after the walk of t + 1, its last reader.
 int Registration::run_chunked_exact(Level &L, int niter, int nb, const StepFn &step,
-                                    int &final_buf) {
+                                    int &final_buf, const StepFn3M &step3m) {
     const double npx = (double)L.dx * L.dy;
     last_err_.clear();
-    for (int b = 3; b < 5; b++)
+    const int R = step3m ? 8 : 4;
+    for (int b = 3; b <= R; b++)
         if (!L.est[b].p) L.est[b].alloc(L.dx, L.dy);
-    auto ring = [](int a, int t) {  // the (t mod 4)-th buffer other than a
-        const int i = t & 3;
+    auto ring = [&](int a, int t) {  // the (t mod R)-th buffer other than a
+        const int i = t % R;
         return i < a ? i : i + 1;
     };
     auto src_of = [&](int a, int t) { return t == 0 ? a : ring(a, t - 1); };
+    auto ev = [](hipEvent_t *e, int t) { return e[t % kExactEv]; };
     // a new loop: its first two calls per workspace start from a fresh state
     bool walked[2] = {false, false};
     int a = 0, k0 = 0;
     while (k0 < niter) {
         const int C = std::min(chunk_, niter - k0);
-        for (int t = 0; t < C; t++) {
-            const int src = src_of(a, t), dst = ring(a, t), w = (k0 + t) & 1;
-            if (t >= 4) OF2D_HIP(hipStreamWaitEvent(st_, ev_walk_[(t - 3) & 3], 0));
-            step(L.est[src].p, L.est[dst].p, d_partial_ + (size_t)t * nb * 2);
-            OF2D_HIP(hipEventRecord(ev_step_[t & 3], st_));
-            OF2D_HIP(hipStreamWaitEvent(sn_st_, ev_step_[t & 3], 0));
-            // workspace w: the walk two iterations back has read it and left
-            // its profile (wk_st_ runs the walks in order)
-            if (t >= 2) OF2D_HIP(hipStreamWaitEvent(sn_st_, ev_walk_[(t - 2) & 3], 0));
-            const bool use_prof = walked[w] && seq_dx_[w] == L.dx && seq_dy_[w] == L.dy;
-            seq_dx_[w] = L.dx;
-            seq_dy_[w] = L.dy;
-            walked[w] = true;
-            launch_seqnorm_tables(L.est[dst].p, L.est[src].p, L.dx, L.dy, L.P, d_seqws_[w].p,
-                                  use_prof, sn_st_);
-            OF2D_HIP(hipEventRecord(ev_fix_[t & 3], sn_st_));
-            OF2D_HIP(hipStreamWaitEvent(wk_st_, ev_fix_[t & 3], 0));
-            launch_seqnorm_walk(L.est[dst].p, L.est[src].p, L.dx, L.dy, L.P, d_seqws_[w].p,
-                                nullptr, d_seq_.p + 2 * (size_t)t, nullptr, wk_st_);
-            OF2D_HIP(hipEventRecord(ev_walk_[t & 3], wk_st_));
+        for (int t = 0; t < C;) {
+            const int k = (step3m && C - t >= 3) ? 3 : 1;
+            // the buffers of iterates t .. t + k - 1 held iterates t - R ..,
+            // last read by the walks up to t + k - R (walks run in order)
+            if (t + k - R >= 0) OF2D_HIP(hipStreamWaitEvent(st_, ev(ev_walk_, t + k - R), 0));
+            if (k == 3)
+                step3m(L.est[src_of(a, t)].p, L.est[ring(a, t)].p, L.est[ring(a, t + 1)].p,
+                       L.est[ring(a, t + 2)].p);
+            else
+                step(L.est[src_of(a, t)].p, L.est[ring(a, t)].p, d_partial_ + (size_t)t * nb * 2);
+            OF2D_HIP(hipEventRecord(ev(ev_step_, t), st_));
+            for (int m = t; m < t + k; m++) {
+                const int src = src_of(a, m), dst = ring(a, m), w = (k0 + m) & 1;
+                if (m == t) OF2D_HIP(hipStreamWaitEvent(sn_st_, ev(ev_step_, t), 0));
+                // workspace w: the walk two iterations back has read it and left
+                // its profile (wk_st_ runs the walks in order)
+                if (m >= 2) OF2D_HIP(hipStreamWaitEvent(sn_st_, ev(ev_walk_, m - 2), 0));
+                const bool use_prof = walked[w] && seq_dx_[w] == L.dx && seq_dy_[w] == L.dy;
+                seq_dx_[w] = L.dx;
+                seq_dy_[w] = L.dy;
+                walked[w] = true;
+                launch_seqnorm_tables(L.est[dst].p, L.est[src].p, L.dx, L.dy, L.P,
+                                      d_seqws_[w].p, use_prof, sn_st_);
+                OF2D_HIP(hipEventRecord(ev(ev_fix_, m), sn_st_));
+                OF2D_HIP(hipStreamWaitEvent(wk_st_, ev(ev_fix_, m), 0));
+                launch_seqnorm_walk(L.est[dst].p, L.est[src].p, L.dx, L.dy, L.P, d_seqws_[w].p,
+                                    nullptr, d_seq_.p + 2 * (size_t)m, nullptr, wk_st_);
+                OF2D_HIP(hipEventRecord(ev(ev_walk_, m), wk_st_));
+            }
+            t += k;
         }
-        OF2D_HIP(hipStreamWaitEvent(st_, ev_walk_[(C - 1) & 3], 0));
+        OF2D_HIP(hipStreamWaitEvent(st_, ev(ev_walk_, C - 1), 0));
         OF2D_HIP(hipMemcpyAsync(hs_.flt, d_seq_.p, sizeof(float) * 2 * C, hipMemcpyDeviceToHost,
                                 st_));
         check_status();  // synchronises st_ (and with it every norm of the chunk)
@@ -376,8 +389,8 @@ int Registration::run_chunked_exact(Level &L, int niter, int nb, const StepFn &s
             last_err_.push_back(err);
             if (verbose_) print("Iteration: %d\tError:%.4f\n", k, (double)err);
             if (err < 0.001f && k > 1) {  // ImageRegistrationOpticalFlow.cpp:131-134
-                // iteration t's buffer was reused by iteration t + 4: replay
-                if (t + 4 <= C - 1)
+                // iteration t's buffer was reused by iteration t + R: replay
+                if (t + R <= C - 1)
                     for (int r = 0; r <= t; r++)
                         step(L.est[src_of(a, r)].p, L.est[ring(a, r)].p, d_partial_);
                 final_buf = ring(a, t);
@@ -401,8 +414,9 @@ int Registration::run_chunked_exact(Level &L, int niter, int nb, const StepFn &s
 // iteration t is replayed from it with single steps (iteration t reads
 // src_of(a, t) and writes dst_of(a, t)).
 int Registration::run_chunked(Level &L, int niter, int nb, const StepFn &step, int &final_buf,
-                              const StepFn2 &step2, const StepFn3 &step3, const int *nblk) {
-    if (exact_norms()) return run_chunked_exact(L, niter, nb, step, final_buf);
+                              const StepFn2 &step2, const StepFn3 &step3, const int *nblk,
+                              const StepFn3M &step3m) {
+    if (exact_norms()) return run_chunked_exact(L, niter, nb, step, final_buf, step3m);
     const double npx = (double)L.dx * L.dy;
     last_err_.clear();
     if (fixed_ && d_all_.n < 2 * (size_t)niter) {
@@ -526,7 +540,18 @@ int Registration::loop_hs(Level &L, int niter, float alpha, int &final_buf) {
                                   : nullptr);
         })
               : StepFn3(),
-        nblk);
+        nblk,
+        pairs ? StepFn3M([&](const float2 *src, float2 *d1, float2 *d2, float2 *d3) {
+            // the exact Logger's triples: every iterate stored (partials unused)
+            launch_hs_jacobi3(src, d3, L.dI.p, L.It.p, L.P, L.dx, L.dy, 0, L.dy, alphasq, -1,
+                              L.dy + 1, d_partial_, d_partial_ + (size_t)nb * 2,
+                              d_partial_ + (size_t)nb * 4, d_status_, range_flag, st_, -1, -1,
+                              (gi_ < 0 ? hs3_gradients_from_image(L.dx, L.dy) : gi_ != 0)
+                                  ? L.Iaux.p
+                                  : nullptr,
+                              d1, d2);
+        })
+              : StepFn3M());
 }
 
 // WrapperOpticalFlow2d.cpp:105-117 -> Motion::copy_motion_to_input

@@ -394,12 +394,48 @@ __global__ __launch_bounds__(kSnThreads) void seqnorm_tables(const float2 *__res
 __global__ __launch_bounds__(kSnScan) void seqnorm_check(unsigned nt, SnWs ws, int use_prof,
                                                          const double *__restrict__ p_off) {
     const unsigned chunk = (nt + kSnScan - 1) / kSnScan;
-    const unsigned b0 = threadIdx.x * chunk;
+    const unsigned b0 = min(nt, threadIdx.x * chunk);
     const unsigned b1 = min(nt, b0 + chunk);
+    // up to kCk tiles per thread (grids up to 4 * 1024 tiles, 4096^2): every
+    // global read of the thread is issued before the first is used and the
+    // tile values stay in registers; longer chunks loop over global memory
+    constexpr int kCk = 4;
+    const bool inreg = chunk <= (unsigned)kCk;
+    const int src[2] = {prof_src(ws, 0), prof_src(ws, 1)};
+    auto drift_at = [&](int sn, unsigned b) {
+        if (!use_prof) return 1.0;
+        const double f = ws.prof[(size_t)sn * (nt + 1) + b], q = ws.Pp[(size_t)sn * (nt + 1) + b];
+        return (q > 0.0 && f > 0.0 && f < INFINITY) ? f / q : 1.0;
+    };
+    double av[2][kCk];
+    float dv[2][kCk + 1];  // a prediction factor: float is plenty
+    unsigned hv[2][kCk];
+    if (inreg) {
+#pragma unroll
+        for (int k = 0; k < kCk; k++)
+#pragma unroll
+            for (int n = 0; n < 2; n++) {
+                const bool in = b0 + k < b1;
+                av[n][k] = in ? ws.A[2 * (size_t)(b0 + k) + n] : 0.0;
+                hv[n][k] = in ? ws.H[2 * (size_t)(b0 + k) + n] : 0u;
+            }
+        // drift at b0 .. b1 (b1: the next thread's first tile; prof / Pp hold
+        // nt + 1 entries)
+#pragma unroll
+        for (int k = 0; k <= kCk; k++)
+#pragma unroll
+            for (int n = 0; n < 2; n++)
+                dv[n][k] = (b0 < b1 && b0 + k <= b1) ? (float)drift_at(src[n], b0 + k) : 1.0f;
+    }
     __shared__ double sh[2][kSnScan];
     for (int n = 0; n < 2; n++) {
         double s = 0.0;
-        for (unsigned b = b0; b < b1; b++) s += ws.A[2 * (size_t)b + n];
+        if (inreg) {
+#pragma unroll
+            for (int k = 0; k < kCk; k++) s += av[n][k];
+        } else {
+            for (unsigned b = b0; b < b1; b++) s += ws.A[2 * (size_t)b + n];
+        }
         sh[n][threadIdx.x] = s;
     }
     __syncthreads();
@@ -415,35 +451,25 @@ __global__ __launch_bounds__(kSnScan) void seqnorm_check(unsigned nt, SnWs ws, i
         __syncthreads();
     }
     const double del = use_prof ? 1.0 / 64 : 1.0 / 16;
-    int src[2];
     double Pb[2], drift[2], dend[2];
-    auto drift_at = [&](int s, unsigned b) {
-        if (!use_prof) return 1.0;
-        const double f = ws.prof[(size_t)s * (nt + 1) + b], q = ws.Pp[(size_t)s * (nt + 1) + b];
-        return (q > 0.0 && f > 0.0 && f < INFINITY) ? f / q : 1.0;
-    };
-    // threads past the last tile (nt < kSnScan) read nothing: prof / Pp hold
-    // nt + 1 entries
+    // threads past the last tile (nt < kSnScan) read nothing
     const bool active = b0 < b1;
     for (int n = 0; n < 2; n++) {
-        src[n] = prof_src(ws, n);
         // p_off: the fp64 sum of the terms before this grid (a row slab's
         // predecessors), so that the prediction is of the global running sum
         Pb[n] = (threadIdx.x ? sh[n][threadIdx.x - 1] : 0.0) + (p_off ? p_off[n] : 0.0);
-        drift[n] = active ? drift_at(src[n], b0) : 1.0;
-        dend[n] = active ? drift_at(src[n], b1) : 1.0;  // the next thread's first tile
+        drift[n] = !active ? 1.0 : inreg ? dv[n][0] : drift_at(src[n], b0);
+        dend[n] = !active ? 1.0 : inreg ? dv[n][0] : drift_at(src[n], b1);  // (inreg: unused)
     }
     __syncthreads();  // these reads of the last call's Pp before this call's writes
-    for (unsigned b = b0; b < b1; b++) {
+    // one tile: the candidate window it needs against the one it has
+    auto tile = [&](unsigned b, const double a[2], const unsigned h0[2], const double dnext[2]) {
         bool listed = false;
-        double dnext[2];
-        for (int n = 0; n < 2; n++) dnext[n] = b + 1 == b1 ? dend[n] : drift_at(src[n], b + 1);
         for (int n = 0; n < 2; n++) {
-            const double a = ws.A[2 * (size_t)b + n];
-            const unsigned h = ws.H[2 * (size_t)b + n];
-            if (!(h & (kHdrZero | kHdrNan)) && a < INFINITY && Pb[n] < INFINITY) {
+            const unsigned h = h0[n];
+            if (!(h & (kHdrZero | kHdrNan)) && a[n] < INFINITY && Pb[n] < INFINITY) {
                 const unsigned want = cand_window(Pb[n] * drift[n] * (1.0 - del),
-                                                  (Pb[n] + a) * dnext[n] * (1.0 + del));
+                                                  (Pb[n] + a[n]) * dnext[n] * (1.0 + del));
                 const int wl = hdr_elo(want), wn = hdr_nc(want), hl = hdr_elo(h), hn = hdr_nc(h);
                 unsigned hh = h;
                 if (wn > 0 && (wl < hl || wl + wn > hl + hn)) hh = want | kHdrPending;
@@ -456,7 +482,25 @@ __global__ __launch_bounds__(kSnScan) void seqnorm_check(unsigned nt, SnWs ws, i
         if (listed) ws.list[atomicAdd(&ws.cnt[0], 1u)] = b;
         for (int n = 0; n < 2; n++) {
             ws.Pp[(size_t)n * (nt + 1) + b] = Pb[n];
-            Pb[n] += ws.A[2 * (size_t)b + n];
+            Pb[n] += a[n];
+        }
+    };
+    if (inreg) {
+#pragma unroll
+        for (int k = 0; k < kCk; k++) {
+            if (b0 + k >= b1) break;
+            const double a[2] = {av[0][k], av[1][k]};
+            const unsigned h[2] = {hv[0][k], hv[1][k]};
+            const double dn[2] = {dv[0][k + 1], dv[1][k + 1]};
+            tile(b0 + k, a, h, dn);
+        }
+    } else {
+        for (unsigned b = b0; b < b1; b++) {
+            const double a[2] = {ws.A[2 * (size_t)b], ws.A[2 * (size_t)b + 1]};
+            const unsigned h[2] = {ws.H[2 * (size_t)b], ws.H[2 * (size_t)b + 1]};
+            double dn[2];
+            for (int n = 0; n < 2; n++) dn[n] = b + 1 == b1 ? dend[n] : drift_at(src[n], b + 1);
+            tile(b, a, h, dn);
         }
     }
     if (b1 == nt && b0 < b1)

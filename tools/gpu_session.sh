@@ -3,7 +3,8 @@
 #   steps: tests (all gpu tests), sntests / ranks (Logger-norm / multi-device
 #          tests), diag (tools/seqnorm_diag.py), conv (tools/time_convergence.py),
 #          convprof (rocprofv3 kernel stats of conv), smoke, bench, prof (bench
-#          under rocprofv3), cfgs (bench_configs.py)
+#          under rocprofv3), cfgs (bench_configs.py), cfg3prof / cfg4prof
+#          (rocprofv3 kernel trace of one secondary config, 50 iterations)
 # Stops at the first step that faults / aborts / times out (rc > 1).
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
@@ -32,6 +33,8 @@ for s in "$@"; do
         bench) step bench 600 python bench.py || exit $? ;;
         prof) step prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/$OUT/${tag}_prof" -o hs -- python3 "$R/bench.py" --no-cpu-baseline || exit $? ;;
         cfgs) step cfgs 900 python -u bench_configs.py || exit $? ;;
+        cfg4prof) step cfg4prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/$OUT/${tag}_cfg4prof" -o k -- python3 -u "$R/bench_configs.py" --configs 4 --no-cpu --iters 50 || exit $? ;;
+        cfg3prof) step cfg3prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/$OUT/${tag}_cfg3prof" -o k -- python3 -u "$R/bench_configs.py" --configs 3 --no-cpu --iters 50 || exit $? ;;
         *) echo "unknown step $s"; exit 2 ;;
     esac
 done
