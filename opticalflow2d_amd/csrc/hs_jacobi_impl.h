@@ -571,12 +571,6 @@ __device__ __forceinline__ void progress_prio(int done, int total) {
 // the same ghost j-lines as u (rows glo .. ghi-1 readable).  Worth it when dI
 // and It do not stay resident in the 256 MB MALL between launches (the
 // launchers' callers decide, of2d_device.h hs3_gradients_from_image).
-// u is read and u3 written non-temporally (streamed past the MALL, which keeps
-// the gradients); OF2D_HS3_NTU=0 builds the cached variant (measured A/B)
-#ifndef OF2D_HS3_NTU
-#define OF2D_HS3_NTU 1
-#endif
-constexpr bool kHs3NtU = OF2D_HS3_NTU != 0;
 // MID: the two intermediate iterates u1, u2 of the owned rows are stored too
 // (to m1, m2): the reference-exact Logger needs every iterate in memory
 // (registration.cpp run_chunked_exact), 16 B/px more per launch.
@@ -616,7 +610,7 @@ __global__ __launch_bounds__(64 * WAVES, MINB) void jacobi3_kernel(
     unsigned bad = 0;
     auto cl = [&](int j) { return min(max(j, glo), ghi - 1); };
     const int xl = xin ? x : (x < 0 ? 0 : P - 2);
-    auto ldu = [&](int j) { return load_row<2, kHs3NtU>(uo + (long)cl(j) * P, xl); };
+    auto ldu = [&](int j) { return load_row<2, true>(uo + (long)cl(j) * P, xl); };
     // one row of gradients with the denominator (alpha^2 + gx^2) + gy^2
     // (OpticalFlowDiffusion.cpp:78), which the three steps share
     struct G {
@@ -852,8 +846,8 @@ __global__ __launch_bounds__(64 * WAVES, MINB) void jacobi3_kernel(
                 bad |= b3;  // the denominator depends on dI only: one test per pixel
                 float2 *dst = un + (long)J(sp) * P + x;
                 if (x + 2 <= dimx)
-                    st4<kHs3NtU>(reinterpret_cast<float4 *>(dst),
-                                 make_float4(z.v[0].x, z.v[0].y, z.v[1].x, z.v[1].y));
+                    st4<true>(reinterpret_cast<float4 *>(dst),
+                              make_float4(z.v[0].x, z.v[0].y, z.v[1].x, z.v[1].y));
                 else
                     dst[0] = z.v[0];
             }
