@@ -574,16 +574,15 @@ __device__ __forceinline__ void progress_prio(int done, int total) {
 // MID: the two intermediate iterates u1, u2 of the owned rows are stored too
 // (to m1, m2): the reference-exact Logger needs every iterate in memory
 // (registration.cpp run_chunked_exact), 16 B/px more per launch.
-template <int ROWS, int WAVES, bool XCD = true, int MINB = 1, int UNR = 4, int PRIO = 0,
-          bool ALT = false, bool GI = false, bool MID = false>
-__global__ __launch_bounds__(64 * WAVES, MINB) void jacobi3_kernel(
+template <int ROWS, int WAVES, bool XCD, int MINB, int UNR, int PRIO, bool ALT, bool GI,
+          bool MID>
+__device__ __forceinline__ void jacobi3_body(
     const float2 *__restrict__ uo, float2 *__restrict__ un, const float2 *__restrict__ dI,
     const float *__restrict__ It, int P, int dimx, int nrows, int row0, int dimy, float alphasq,
     int glo, int ghi, double *__restrict__ partial, double *__restrict__ partial2,
     double *__restrict__ partial3, unsigned *__restrict__ status, int band0, int gx, int gy,
-    int rows = ROWS, const unsigned *__restrict__ range_flag = nullptr, int jlo = -1,
-    int jhi = -1, const float *__restrict__ Ia = nullptr, float2 *__restrict__ m1 = nullptr,
-    float2 *__restrict__ m2 = nullptr) {
+    int rows, const unsigned *__restrict__ range_flag, int jlo, int jhi,
+    const float *__restrict__ Ia, float2 *__restrict__ m1, float2 *__restrict__ m2) {
     int bx = (int)blockIdx.x, by = (int)blockIdx.y;
     if constexpr (XCD) {
         if (!xcd_block(gx, gy, bx, by)) return;
@@ -910,6 +909,34 @@ __global__ __launch_bounds__(64 * WAVES, MINB) void jacobi3_kernel(
         partial3[2 * blk] = r[4];
         partial3[2 * blk + 1] = r[5];
     }
+}
+
+template <int ROWS, int WAVES, bool XCD = true, int MINB = 1, int UNR = 4, int PRIO = 0,
+          bool ALT = false, bool GI = false>
+__global__ __launch_bounds__(64 * WAVES, MINB) void jacobi3_kernel(
+    const float2 *__restrict__ uo, float2 *__restrict__ un, const float2 *__restrict__ dI,
+    const float *__restrict__ It, int P, int dimx, int nrows, int row0, int dimy, float alphasq,
+    int glo, int ghi, double *__restrict__ partial, double *__restrict__ partial2,
+    double *__restrict__ partial3, unsigned *__restrict__ status, int band0, int gx, int gy,
+    int rows = ROWS, const unsigned *__restrict__ range_flag = nullptr, int jlo = -1,
+    int jhi = -1, const float *__restrict__ Ia = nullptr) {
+    jacobi3_body<ROWS, WAVES, XCD, MINB, UNR, PRIO, ALT, GI, false>(
+        uo, un, dI, It, P, dimx, nrows, row0, dimy, alphasq, glo, ghi, partial, partial2, partial3,
+        status, band0, gx, gy, rows, range_flag, jlo, jhi, Ia, nullptr, nullptr);
+}
+// the same storing the intermediate iterates u1, u2 to m1, m2 (MID)
+template <int ROWS, int WAVES, bool XCD = true, int MINB = 1, int UNR = 4, int PRIO = 0,
+          bool ALT = false, bool GI = false>
+__global__ __launch_bounds__(64 * WAVES, MINB) void jacobi3_mid_kernel(
+    const float2 *__restrict__ uo, float2 *__restrict__ un, const float2 *__restrict__ dI,
+    const float *__restrict__ It, int P, int dimx, int nrows, int row0, int dimy, float alphasq,
+    int glo, int ghi, double *__restrict__ partial, double *__restrict__ partial2,
+    double *__restrict__ partial3, unsigned *__restrict__ status, int band0, int gx, int gy,
+    int rows, const unsigned *__restrict__ range_flag, int jlo, int jhi,
+    const float *__restrict__ Ia, float2 *__restrict__ m1, float2 *__restrict__ m2) {
+    jacobi3_body<ROWS, WAVES, XCD, MINB, UNR, PRIO, ALT, GI, true>(
+        uo, un, dI, It, P, dimx, nrows, row0, dimy, alphasq, glo, ghi, partial, partial2, partial3,
+        status, band0, gx, gy, rows, range_flag, jlo, jhi, Ia, m1, m2);
 }
 
 template <int ROWS, int WAVES>

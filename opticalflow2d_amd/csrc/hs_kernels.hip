@@ -67,10 +67,8 @@ static const auto kHsJacobi3 = &hs::jacobi3_kernel<0, kHs3Waves, true, 4, 4, 1, 
 // the same with the gradients derived from Iaux in the kernel (GI: 24 B/px)
 static const auto kHsJacobi3I = &hs::jacobi3_kernel<0, kHs3Waves, true, 4, 4, 1, true, true>;
 // both, storing the intermediate iterates too (MID: +16 B/px)
-static const auto kHsJacobi3M =
-    &hs::jacobi3_kernel<0, kHs3Waves, true, 4, 4, 1, true, false, true>;
-static const auto kHsJacobi3IM =
-    &hs::jacobi3_kernel<0, kHs3Waves, true, 4, 4, 1, true, true, true>;
+static const auto kHsJacobi3M = &hs::jacobi3_mid_kernel<0, kHs3Waves, true, 4, 4, 1, true, false>;
+static const auto kHsJacobi3IM = &hs::jacobi3_mid_kernel<0, kHs3Waves, true, 4, 4, 1, true, true>;
 
 void launch_hs_jacobi3(const float2 *u_old, float2 *u_new, const float2 *dI, const float *It,
                        int P, int dimx, int nrows, int row0, int dimy, float alphasq, int glo,
@@ -89,11 +87,16 @@ void launch_hs_jacobi3(const float2 *u_old, float2 *u_new, const float2 *dI, con
     dim3 g = hs3_grid(dimx, nrows);
     g.y = band_hi - band_lo;
     const dim3 gl(8 * ((g.x * g.y + 7) / 8));
-    const auto kern = u1 ? (Ia ? kHsJacobi3IM : kHsJacobi3M) : (Ia ? kHsJacobi3I : kHsJacobi3);
-    hipLaunchKernelGGL(kern, gl, dim3(64 * kHs3Waves), 0, st, u_old, u_new, dI, It, P, dimx,
-                       nrows, row0, dimy, alphasq, glo, ghi, partial, partial2, partial3, status,
-                       band_lo, (int)g.x, (int)g.y, hs3_rows(dimx, nrows), range_flag, -1, -1, Ia,
-                       u1, u2);
+    if (u1)
+        hipLaunchKernelGGL(Ia ? kHsJacobi3IM : kHsJacobi3M, gl, dim3(64 * kHs3Waves), 0, st, u_old,
+                           u_new, dI, It, P, dimx, nrows, row0, dimy, alphasq, glo, ghi, partial,
+                           partial2, partial3, status, band_lo, (int)g.x, (int)g.y,
+                           hs3_rows(dimx, nrows), range_flag, -1, -1, Ia, u1, u2);
+    else
+        hipLaunchKernelGGL(Ia ? kHsJacobi3I : kHsJacobi3, gl, dim3(64 * kHs3Waves), 0, st, u_old,
+                           u_new, dI, It, P, dimx, nrows, row0, dimy, alphasq, glo, ghi, partial,
+                           partial2, partial3, status, band_lo, (int)g.x, (int)g.y,
+                           hs3_rows(dimx, nrows), range_flag, -1, -1, Ia);
     OF2D_HIP(hipGetLastError());
 }
 
@@ -114,7 +117,7 @@ int launch_hs_jacobi3_window(const float2 *u_old, float2 *u_new, const float2 *d
     hipLaunchKernelGGL(Ia ? kHsJacobi3I : kHsJacobi3, gl, dim3(64 * kHs3Waves), 0, st, u_old,
                        u_new, dI, It, P, dimx, nrows, row0, dimy, alphasq, glo, ghi, partial,
                        partial2, partial3, status, slot_band0, gx, gy, rows_per_wave, range_flag,
-                       jlo, jhi, Ia, nullptr, nullptr);
+                       jlo, jhi, Ia);
     OF2D_HIP(hipGetLastError());
     return gy;
 }

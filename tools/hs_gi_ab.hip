@@ -134,8 +134,7 @@ int main(int argc, char **argv) {
         const int nb = gx * gy;
         hipLaunchKernelGGL(v.k, dim3(8 * ((nb + 7) / 8)), dim3(256), 0, st, in, out, pdI, pIt, P,
                            n, ny, 0, ny, alphasq, -1, ny + 1, part, part + 2 * nb, part + 4 * nb,
-                           status, 0, gx, gy, rows, rflag, -1, -1, v.gi ? pIa : nullptr, nullptr,
-                           nullptr);
+                           status, 0, gx, gy, rows, rflag, -1, -1, v.gi ? pIa : nullptr);
     };
     // probes over the pitched rows (P * ny px, 2 px per thread)
     const long n2 = (long)P * ny / 2;
