@@ -142,12 +142,13 @@ __device__ __forceinline__ float wide_min(float m) {
 }
 }  // namespace
 
-// The sweep works on a packed array vb = {v.x, v.y, b.x, b.y}: the field being
-// relaxed and its right-hand side, stored SKEWED along the wavefront: pixel
-// (i, j) lives at row t = 2i + j, column i (sor_index).  Every lane of a strip
-// then works on the same row t at each step, so a step's load is one
-// contiguous 1-KB row segment and its store one 512-B half-interleaved segment
-// (row-major storage would make both 64 separate transactions).  Cells of the
+// The sweep works on the array vb of the field being relaxed (v) and its
+// right-hand side (b), stored SKEWED along the wavefront: pixel (i, j) lives at
+// row t = 2i + j, column i, a row being P float2 v then P float2 b (sor_v,
+// sor_b).  Every lane of a strip then works on the same row t at each step, so
+// a step's loads are two contiguous 512-B row segments (v and b) and its store
+// one (row-major storage would make each 64 separate transactions); the
+// passes around the sweep that write only b (the force) write whole runs.  Cells of the
 // skewed array that are no pixel (j outside [0, dimy)) are padding: a lane
 // whose wavefront row lies outside the image reads and writes back its own
 // padding cell instead of branching.
@@ -294,11 +295,21 @@ __global__ __launch_bounds__(64) void sor_strip_kernel(float4 *__restrict__ vb, 
     const int c = c0 + lane;
     const bool active = lane < kSorCols && c <= dimx - 2;
     // vb addressing: at step s every lane is on skewed row 2 c0 + s + 1; a
-    // batch rsrc points at (that row for the batch's first step, column c0)
-    const unsigned P16 = (unsigned)P * 16u;
-    const unsigned voff_ld = (unsigned)lane * 16u;  // lanes past dimx read padding cells
-    const unsigned voff_st = active ? (unsigned)lane * 16u : kOob;
-    const char *vbc0 = reinterpret_cast<const char *>(vb + c0);
+    // batch rsrc points at (that row for the batch's first step, column c0);
+    // a row is P16 bytes, its b half starts P8 bytes in
+    const unsigned P16 = (unsigned)P * 16u, P8 = (unsigned)P * 8u;
+    const unsigned voff_ld = (unsigned)lane * 8u;  // lanes past dimx read padding cells
+    const unsigned voff_st = active ? (unsigned)lane * 8u : kOob;
+    const char *vbc0 = reinterpret_cast<const char *>(vb) + (size_t)c0 * 8u;
+    // one row of the lane's column: {v.x, v.y, b.x, b.y}
+    auto ldrow = [&](__amdgpu_buffer_rsrc_t rs, int soff, auto aux) __attribute__((always_inline)) {
+        constexpr int kAux = decltype(aux)::value;
+        const v2u v = __builtin_amdgcn_raw_buffer_load_b64(rs, voff_ld, soff, kAux);
+        const v2u b = __builtin_amdgcn_raw_buffer_load_b64(rs, voff_ld, soff + (int)P8, kAux);
+        return v4u{v.x, v.y, b.x, b.y};
+    };
+    using Aux0 = std::integral_constant<int, 0>;
+    using AuxLd = std::integral_constant<int, OF2D_SOR_LD_AUX>;
     // granules: region I (ghost column of this strip), region I+1 (published)
     const char *gin = reinterpret_cast<const char *>(H + (long)I * Hstride + kSorPadRows);
     const char *gout = reinterpret_cast<const char *>(H + (long)(I + 1) * Hstride + kSorPadRows);
@@ -320,16 +331,14 @@ __global__ __launch_bounds__(64) void sor_strip_kernel(float4 *__restrict__ vb, 
     v4u W0, W1, W2, W3, X[kSorNB][kSorB], GV[kSorNB];
     {
         const auto rs = rsrc_at(vrow);
-        W0 = __builtin_amdgcn_raw_buffer_load_b128(rs, voff_ld, 0, 0);
-        W1 = __builtin_amdgcn_raw_buffer_load_b128(rs, voff_ld, (int)P16, 0);
-        W2 = __builtin_amdgcn_raw_buffer_load_b128(rs, voff_ld, 2 * (int)P16, 0);
-        W3 = __builtin_amdgcn_raw_buffer_load_b128(rs, voff_ld, 3 * (int)P16, 0);
+        W0 = ldrow(rs, 0, Aux0{});
+        W1 = ldrow(rs, (int)P16, Aux0{});
+        W2 = ldrow(rs, 2 * (int)P16, Aux0{});
+        W3 = ldrow(rs, 3 * (int)P16, Aux0{});
 #pragma unroll
         for (int b = 0; b < kSorNB; b++)
 #pragma unroll
-            for (int j = 0; j < kSorB; j++)
-                X[b][j] = __builtin_amdgcn_raw_buffer_load_b128(rs, voff_ld,
-                                                                (4 + kSorB * b + j) * (int)P16, 0);
+            for (int j = 0; j < kSorB; j++) X[b][j] = ldrow(rs, (4 + kSorB * b + j) * (int)P16, Aux0{});
         const auto gr = rsrc_at(grow);
 #pragma unroll
         for (int b = 0; b < kSorGLead; b++)
@@ -413,9 +422,7 @@ __global__ __launch_bounds__(64) void sor_strip_kernel(float4 *__restrict__ vb, 
             }
             // batch b of the next group: rows 32 further down
 #pragma unroll
-            for (int j = 0; j < kSorB; j++)
-                X[b][j] = __builtin_amdgcn_raw_buffer_load_b128(
-                    rs, voff_ld, (4 + kSorG + j) * (int)P16, OF2D_SOR_LD_AUX);
+            for (int j = 0; j < kSorB; j++) X[b][j] = ldrow(rs, (4 + kSorG + j) * (int)P16, AuxLd{});
             vrow += vstep;
             prow += kSorB * 16;
         }
@@ -500,30 +507,17 @@ __device__ __forceinline__ void skew_tile_for_each(int i0, int j0, int dimx, int
         if (skew_slot(it, i0, j0, dimx, dimy, ii, jj)) f(ii, jj);
     }
 }
-// vb.zw <- f(ii, jj) over the tile's skewed runs, keeping vb.xy: every granule
-// of the thread is loaded before the first is written back (a read-modify-
-// write per run would wait for each load in turn: the compiler cannot prove
-// the runs' addresses distinct)
+// vb's b <- f(ii, jj) over the tile's skewed runs (8-B elements, runs of 16
+// consecutive columns: whole 128-B segments, no read of v)
 template <class F>
-__device__ __forceinline__ void skew_tile_set_zw(float4 *__restrict__ vb, int i0, int j0, int dimx,
-                                                 int dimy, int P, F f) {
-    float4 o[kSkIts];
-    int ii[kSkIts], jj[kSkIts];
-    bool ok[kSkIts];
-#pragma unroll
-    for (int it = 0; it < kSkIts; it++) {
-        ok[it] = skew_slot(it, i0, j0, dimx, dimy, ii[it], jj[it]);
-        o[it] = vb[ok[it] ? sor_index(i0 + ii[it], j0 + jj[it], P) : 0];
-    }
-#pragma unroll
-    for (int it = 0; it < kSkIts; it++)
-        if (ok[it]) {
-            const float2 z = f(ii[it], jj[it]);
-            vb[sor_index(i0 + ii[it], j0 + jj[it], P)] = make_float4(o[it].x, o[it].y, z.x, z.y);
-        }
+__device__ __forceinline__ void skew_tile_set_b(float4 *__restrict__ vb, int i0, int j0, int dimx,
+                                                int dimy, int P, F f) {
+    float2 *vb2 = reinterpret_cast<float2 *>(vb);
+    skew_tile_for_each(i0, j0, dimx, dimy,
+                       [&](int ii, int jj) { vb2[sor_b(i0 + ii, j0 + jj, P)] = f(ii, jj); });
 }
 
-// vb.zw <- force(u, dI, It) (OpticalFlow.cpp:15-39); with pack_v also vb.xy <- v.
+// vb's b <- force(u, dI, It) (OpticalFlow.cpp:15-39); with pack_v also its v <- v.
 // Column 0 (never relaxed) is the ghost column of strip 0: its values go to
 // granule region 0 with this sweep's epoch.
 __global__ __launch_bounds__(256) void sor_pack_kernel(float4 *__restrict__ vb,
@@ -545,17 +539,20 @@ __global__ __launch_bounds__(256) void sor_pack_kernel(float4 *__restrict__ vb,
         float2 x = v ? v[idx] : make_float2(0.0f, 0.0f);
         tile[r][threadIdx.x] = make_float4(x.x, x.y, g.x * sc, g.y * sc);
         if (i == 0 && H) {
-            if (!v) x = reinterpret_cast<const float2 *>(vb + sor_index(0, j, P))[0];
+            if (!v) x = reinterpret_cast<const float2 *>(vb)[sor_v(0, j, P)];
             H[kSorPadRows + j] = v4u{__float_as_uint(x.x), __float_as_uint(x.y), epoch, epoch};
         }
     }
     __syncthreads();
     if (v) {
+        float2 *vb2 = reinterpret_cast<float2 *>(vb);
         skew_tile_for_each(i0, j0, dimx, dimy, [&](int ii, int jj) {
-            vb[sor_index(i0 + ii, j0 + jj, P)] = tile[jj][ii];
+            const float4 q = tile[jj][ii];
+            vb2[sor_v(i0 + ii, j0 + jj, P)] = make_float2(q.x, q.y);
+            vb2[sor_b(i0 + ii, j0 + jj, P)] = make_float2(q.z, q.w);
         });
-    } else {  // whole 16-B granules (a masked 8-B store per granule measured slower)
-        skew_tile_set_zw(vb, i0, j0, dimx, dimy, P, [&](int ii, int jj) {
+    } else {
+        skew_tile_set_b(vb, i0, j0, dimx, dimy, P, [&](int ii, int jj) {
             const float4 q = tile[jj][ii];
             return make_float2(q.z, q.w);
         });
@@ -573,7 +570,7 @@ void launch_sor_pack(float4 *vb, const float2 *u, const float2 *dI, const float 
 // After a fluid regrid (ImageRegistrationFluid.cpp:118-123): set_derivatives
 // of the new warped image (IterativeSolver.cpp:22-56, gradients.h:9-32; the
 // same taps and operations as gradients_kernel) and the next sweep's force of
-// the zeroed estimate into vb.zw (get_force with u = +0, the operations of
+// the zeroed estimate into vb's b (get_force with u = +0, the operations of
 // sor_pack_kernel), in one pass over a 64 x 32 tile.
 __global__ __launch_bounds__(256) void regrid_pack_kernel(
     const float *__restrict__ Iref, const float *__restrict__ Ia, float2 *__restrict__ dI,
@@ -617,12 +614,12 @@ __global__ __launch_bounds__(256) void regrid_pack_kernel(
         const float sc = (t + z * gx) + z * gy;
         fo[rr][threadIdx.x] = make_float2(gx * sc, gy * sc);
         if (i == 0 && H) {
-            const float2 x = reinterpret_cast<const float2 *>(vb + sor_index(0, j, P))[0];
+            const float2 x = reinterpret_cast<const float2 *>(vb)[sor_v(0, j, P)];
             H[kSorPadRows + j] = v4u{__float_as_uint(x.x), __float_as_uint(x.y), epoch, epoch};
         }
     }
     __syncthreads();
-    skew_tile_set_zw(vb, i0, j0, dimx, dimy, P, [&](int ii, int jj) { return fo[jj][ii]; });
+    skew_tile_set_b(vb, i0, j0, dimx, dimy, P, [&](int ii, int jj) { return fo[jj][ii]; });
 }
 void launch_regrid_pack(const float *Iref, const float *Iaux, float2 *dI, float *It, float4 *vb,
                         int dimx, int dimy, int P, void *H, unsigned epoch, hipStream_t st) {
@@ -662,7 +659,7 @@ __global__ __launch_bounds__(256) void increment_kernel(const float2 *__restrict
     __shared__ float2 vt[kSkJ][kSkI];  // the tile's velocities, read along skewed rows
     const int i0 = blockIdx.x * kSkI, j0 = blockIdx.y * kFieldRows;
     skew_tile_for_each(i0, j0, dimx, dimy, [&](int ii, int jj) {
-        vt[jj][ii] = reinterpret_cast<const float2 *>(vel + sor_index(i0 + ii, j0 + jj, P))[0];
+        vt[jj][ii] = reinterpret_cast<const float2 *>(vel)[sor_v(i0 + ii, j0 + jj, P)];
     });
     __syncthreads();
     const int i = i0 + threadIdx.x;
@@ -726,7 +723,7 @@ void launch_increment(const float2 *u, const float4 *vel, float2 *R, int dimx, i
 //   per-block min of the Jacobian of the new u (Image.cpp:189-218, Image::min
 //   at Image.cpp:96-104; the neighbours' new u from an LDS tile with a
 //   one-pixel halo);
-//   the next iteration's force f = dI ((It + u.x dI.x) + u.y dI.y) into vb.zw
+//   the next iteration's force f = dI ((It + u.x dI.x) + u.y dI.y) into vb's b
 //   and the region-0 granules tagged with the next sweep's epoch (sor_pack's
 //   force-only mode).  When the iteration regrids, the host discards the packed
 //   force and packs again.  One pass instead of three (integrate + Logger,
@@ -831,15 +828,15 @@ __global__ __launch_bounds__(256) void fluid_step_kernel(
         const float sc = (itk[k] + m.x * g.x) + m.y * g.y;
         fo[rr][threadIdx.x] = make_float2(g.x * sc, g.y * sc);
         if (i == 0 && H) {  // ghost column of strip 0 for the next sweep
-            const float2 x = reinterpret_cast<const float2 *>(vb + sor_index(0, j, P))[0];
+            const float2 x = reinterpret_cast<const float2 *>(vb)[sor_v(0, j, P)];
             H[kSorPadRows + j] = v4u{__float_as_uint(x.x), __float_as_uint(x.y), epoch, epoch};
         }
     }
     block_sum2(sd, sp, lpart);
     jm = block_min(jm);
     if (threadIdx.x == 0 && threadIdx.y == 0) jpart[(long)blockIdx.y * gridDim.x + blockIdx.x] = jm;
-    // 3. vb.zw <- force along the skewed rows (whole 16-B granules, as sor_pack)
-    skew_tile_set_zw(vb, i0, j0, dimx, dimy, P, [&](int ii, int jj) { return fo[jj][ii]; });
+    // 3. vb's b <- force along the skewed rows
+    skew_tile_set_b(vb, i0, j0, dimx, dimy, P, [&](int ii, int jj) { return fo[jj][ii]; });
 }
 
 void launch_fluid_step(const float2 *u, const float2 *R, float2 *uo, const float2 *prev,
@@ -905,7 +902,7 @@ void launch_fluid_report(const double *lpart, int nb, const float *jpart, float 
     OF2D_HIP(hipGetLastError());
 }
 
-// Logger only (Elastic, whose update is the in-place sweep): u <- vb.xy, partials
+// Logger only (Elastic, whose update is the in-place sweep): u <- vb's v, partials
 // of ||u - prev||, ||prev||; prev <- u
 __global__ __launch_bounds__(256) void logger_kernel(const float4 *__restrict__ vb,
                                                      float2 *__restrict__ u,
@@ -915,7 +912,7 @@ __global__ __launch_bounds__(256) void logger_kernel(const float4 *__restrict__ 
     __shared__ float2 vt[kSkJ][kSkI];  // as increment_kernel
     const int i0 = blockIdx.x * kSkI, j0 = blockIdx.y * kFieldRows;
     skew_tile_for_each(i0, j0, dimx, dimy, [&](int ii, int jj) {
-        vt[jj][ii] = reinterpret_cast<const float2 *>(vb + sor_index(i0 + ii, j0 + jj, P))[0];
+        vt[jj][ii] = reinterpret_cast<const float2 *>(vb)[sor_v(i0 + ii, j0 + jj, P)];
     });
     __syncthreads();
     const int i = i0 + threadIdx.x;

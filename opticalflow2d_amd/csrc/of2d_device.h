@@ -315,30 +315,33 @@ void launch_curv_construct(const double *Z, long plane, const float2 *u, float2 
 // ---------------------------------------------------------------- Fluid / Elastic
 int sor_nstrips(int dimx);
 // The SOR working array vb is stored skewed along the Gauss-Seidel wavefront:
-// pixel (i, j) at row 2i + j, column i, pitch P (fluid_kernels.hip).  It has
+// pixel (i, j) at row 2i + j, column i (fluid_kernels.hip).  A row is 16 P
+// bytes: P float2 values of the field being relaxed (v), then P float2
+// right-hand sides (b), so the passes that write only b (the force) or read
+// only v write / read contiguous runs of 8-B elements.  It has
 // sor_rows(dimx, dimy) rows; the last kSorPadRows are padding for lanes that
 // run past the image (as do the kSorPadRows above and below each granule region).
 constexpr int kSorPadRows = 256;
-__host__ __device__ inline long sor_index(int i, int j, int P) {
-    return (2L * i + j) * P + i;
-}
+// float2 index of v(i, j) / b(i, j) in vb
+__host__ __device__ inline long sor_v(int i, int j, int P) { return (2L * i + j) * 2L * P + i; }
+__host__ __device__ inline long sor_b(int i, int j, int P) { return sor_v(i, j, P) + P; }
 inline int sor_rows(int dimx, int dimy) { return 2 * dimx + dimy + kSorPadRows; }
 long sor_granule_stride(int dimy);
 // (nstrips + 1) regions of 16-B granules, zeroed once
 size_t sor_granule_bytes(int dimx, int dimy);
 // in-place Gauss-Seidel SOR sweep (OpticalFlowFluid.cpp:7-41), wavefront-exact,
-// on the skewed vb = {v.x, v.y, b.x, b.y} (sor_rows rows of pitch P).
+// on the skewed vb (v and b halves per row, sor_rows rows of 16 P bytes).
 // epoch: > every earlier epoch on H, the same epoch as the sor_pack before it;
 // ticket: per-H counter, a multiple of nstrips before the launch.
 void launch_sor(float4 *vb, int dimx, int dimy, int P, float mu, float lambda, float omega,
                 void *H, unsigned epoch, unsigned *ticket, unsigned *status, hipStream_t st);
-// vb.zw <- force(u, dI, It); if v != nullptr also vb.xy <- v; granule region 0
-// <- column 0 of vb.xy tagged with epoch
+// vb's b <- force(u, dI, It); if v != nullptr also vb's v <- v; granule region
+// 0 <- column 0 of v tagged with epoch
 void launch_sor_pack(float4 *vb, const float2 *u, const float2 *dI, const float *It,
                      const float2 *v, int dimx, int dimy, int P, void *H, unsigned epoch,
                      hipStream_t st);
-// after a regrid: dI, It <- gradients of Iaux (set_derivatives) and vb.zw <-
-// force of a zero estimate, granule region 0 <- column 0 of vb.xy tagged epoch
+// after a regrid: dI, It <- gradients of Iaux (set_derivatives) and vb's b <-
+// force of a zero estimate, granule region 0 <- column 0 of v tagged epoch
 void launch_regrid_pack(const float *Iref, const float *Iaux, float2 *dI, float *It, float4 *vb,
                         int dimx, int dimy, int P, void *H, unsigned epoch, hipStream_t st);
 void launch_force(const float2 *u, const float2 *dI, const float *It, float2 *f, int dimx,
@@ -349,7 +352,7 @@ void launch_increment(const float2 *u, const float4 *vel, float2 *R, int dimx, i
                       float *part, float *scal, hipStream_t st);
 // uo <- u + R dt (dt < 65) or u; Logger partials of uo against prev (against u
 // when prev is null); per-block Jacobian minima of uo into jpart (their min:
-// launch_fluid_report); vb.zw <- force(uo) and granule region 0 tagged with
+// launch_fluid_report); vb's b <- force(uo) and granule region 0 tagged with
 // `epoch` for the next sweep (fluid_kernels.hip fluid_step_kernel)
 void launch_fluid_step(const float2 *u, const float2 *R, float2 *uo, const float2 *prev,
                        const float *scal, const float2 *dI, const float *It, float4 *vb, int dimx,

@@ -30,7 +30,7 @@ void alloc_level(Level &L, int reg) {
             L.sorH.alloc(sor_granule_bytes(L.dx, L.dy) / sizeof(unsigned long long));
             L.sorTicket.alloc(1);
             L.part.alloc((size_t)increment_nblocks(L.dx, L.dy));
-            L.vb.alloc(L.dx, sor_rows(L.dx, L.dy));  // skewed; Fluid: the velocity is vb.xy
+            L.vb.alloc(L.dx, sor_rows(L.dx, L.dy));  // skewed v | b rows; Fluid: v is the velocity
             if (reg == 5) L.increment.alloc(L.dx, L.dy);
             break;
         case 1:  // OpticalFlowCurvature.cpp:36-56 (the force is fused into the rhs kernel)
@@ -165,14 +165,14 @@ int Registration::loop_fluid(Level &L, int niter) {
     // L.est[0] is the estimate; L.force receives the next one and the two swap
     // every iteration.  prev_separate: the Logger's previous motion is L.tmp,
     // not the iteration's input estimate (first iteration, after a regrid);
-    // packed: vb.zw already holds the force of the estimate, tagged with the
+    // packed: vb's b already holds the force of the estimate, tagged with the
     // next epoch (fluid_step of the previous iteration).
     bool prev_separate = true, packed = false, regridded = false;
     last_err_.clear();
     int iter;
     for (iter = 0; iter < niter; iter++) {
         float2 *est = L.est[0].p;
-        // get_force(force, motion) into vb.zw, then the SOR sweep of the velocity vb.xy
+        // get_force(force, motion) into vb's b, then the SOR sweep of the velocity (v)
         const unsigned ep = ++epoch_;
         if (!packed && regridded)  // gradients of the new warped image + force of est = 0
             launch_regrid_pack(L.Iref.p, L.Iaux.p, L.dI.p, L.It.p, L.vb.p, L.dx, L.dy, L.P,
