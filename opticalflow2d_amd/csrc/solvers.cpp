@@ -162,15 +162,15 @@ int Registration::loop_fluid(Level &L, int niter) {
     float *scal = d_scalar_ + 8;  // [0] maxabs, [1] dt, [2] min jacobian
     const int nb = increment_nblocks(L.dx, L.dy);
     const double npx = (double)L.dx * L.dy;
+    const bool exact = exact_norms();
     // L.est[0] is the estimate; L.force receives the next one and the two swap
     // every iteration.  prev_separate: the Logger's previous motion is L.tmp,
     // not the iteration's input estimate (first iteration, after a regrid);
     // packed: vb's b already holds the force of the estimate, tagged with the
     // next epoch (fluid_step of the previous iteration).
     bool prev_separate = true, packed = false, regridded = false;
-    last_err_.clear();
-    int iter;
-    for (iter = 0; iter < niter; iter++) {
+    // one iteration's device work, up to its report in host memory
+    auto enqueue = [&]() {
         float2 *est = L.est[0].p;
         // get_force(force, motion) into vb's b, then the SOR sweep of the velocity (v)
         const unsigned ep = ++epoch_;
@@ -188,7 +188,6 @@ int Registration::loop_fluid(Level &L, int niter) {
         launch_fluid_step(est, L.increment.p, L.force.p, prev_separate ? prev : nullptr, scal,
                           L.dI.p, L.It.p, L.vb.p, L.dx, L.dy, L.P, L.sorH.p, ep + 1, d_partial_,
                           L.part.p, st_);
-        const bool exact = exact_norms();
         if (exact) seqnorm(L, L.force.p, prev_separate ? prev : est, 0);
         std::swap(L.est[0], L.force);
         prev_separate = false;
@@ -199,21 +198,19 @@ int Registration::loop_fluid(Level &L, int niter) {
         if (exact)
             OF2D_HIP(hipMemcpyAsync(hs_.flt, d_seq_.p, 2 * sizeof(float), hipMemcpyDeviceToHost,
                                     st_));
+    };
+    last_err_.clear();
+    if (niter > 0) enqueue();
+    int iter;
+    for (iter = 0; iter < niter; iter++) {
         OF2D_HIP(hipStreamSynchronize(st_));
         check_reported_status(hs_.report->status);
         const float maxabs = hs_.report->maxabs, dt = hs_.report->dt, jmin = hs_.report->jmin;
-        print("Dumax: %.3f\tMaxabs increment: %.3f\t Timestep: %.3f\n", (double)0.65f,
-              (double)maxabs, (double)dt);
         const float err = exact ? logger_error(hs_.flt[0], hs_.flt[1], npx)
                                 : logger_error(hs_.report->sums[0], hs_.report->sums[1], npx);
-        last_err_.push_back(err);
-        if (verbose_) print("Iteration: %d\tError:%.4f\n", iter, (double)err);
-        if (!fixed_ && err < 0.001f && iter > 1) {
-            iter++;
-            break;
-        }
-        if (jmin < 0.5) {  // regridding (ImageRegistrationFluid.cpp:108-124)
-            print("Regridding on iteration: %d\tMin Jacobian: %.3f\n", iter, (double)jmin);
+        const bool brk = !fixed_ && err < 0.001f && iter > 1;
+        const bool regrid = !brk && jmin < 0.5;
+        if (regrid) {  // regridding (ImageRegistrationFluid.cpp:108-124)
             // the Logger keeps this iteration's motion (the buffers trade places:
             // L.tmp takes the estimate, the old Logger buffer becomes the
             // estimate, zeroed by the regrid pass); motion accumulates the
@@ -228,6 +225,18 @@ int Registration::loop_fluid(Level &L, int niter) {
             packed = false;  // the packed force was of the old estimate and gradients
             regridded = true;
         }
+        // the next iteration goes to the GPU before this one's lines are
+        // printed (the report is in host memory: the values stay)
+        if (!brk && iter + 1 < niter) enqueue();
+        print("Dumax: %.3f\tMaxabs increment: %.3f\t Timestep: %.3f\n", (double)0.65f,
+              (double)maxabs, (double)dt);
+        last_err_.push_back(err);
+        if (verbose_) print("Iteration: %d\tError:%.4f\n", iter, (double)err);
+        if (brk) {
+            iter++;
+            break;
+        }
+        if (regrid) print("Regridding on iteration: %d\tMin Jacobian: %.3f\n", iter, (double)jmin);
     }
     return iter;
 }
