@@ -31,7 +31,7 @@
 //                          (predicted from the previous update's exact
 //                          running sums, the "profile") the ulp sums of each
 //                          segment and of the tile
-//   seqnorm_check          fp64 prefix over the tiles -> the binades the float
+//   seqnorm_check(_sums, _scan)  fp64 prefix over the tiles -> the binades the float
 //                          sum can be in across each tile (the fp64 sum +-1/8);
 //                          tiles whose candidates miss one are marked pending
 //   seqnorm_tables<false>  the pending tiles again, with those binades
@@ -227,6 +227,9 @@ struct SnWs {
     unsigned *list;         // [nt] tiles seqnorm_check listed for seqnorm_fix
     unsigned *cnt;          // [4] list length
     double *tot64;          // [2] fp64 total of this call (seqnorm_total: a slab's offset)
+    double *bs;             // [2][nb] block sums, then block offsets (check)
+    float *dr;              // [2][nt + 1] the last call's drift at each tile (check, pass 1)
+    unsigned *miss;         // [2] raw segments the last walk stepped (its profile's quality)
 };
 // The profile of the last call that predicts norm n: its own, except for
 // |prev| after a call whose prev was zero (the Logger's first update), whose
@@ -397,53 +400,48 @@ __global__ __launch_bounds__(kSnThreads) void seqnorm_tables(const float2 *__res
 // drift of the float sum from it (use_prof; 1/64 either side), or the prefix
 // alone (1/16 either side).  A tile whose entries miss one is listed for new
 // tile entries (pending); a tile across which the sum may change binade is
-// listed for segment entries (the walk resolves it).
-__global__ __launch_bounds__(kSnScan) void seqnorm_check(unsigned nt, SnWs ws, int use_prof,
-                                                         const double *__restrict__ p_off) {
-    const unsigned chunk = (nt + kSnScan - 1) / kSnScan;
-    const unsigned b0 = min(nt, threadIdx.x * chunk);
-    const unsigned b1 = min(nt, b0 + chunk);
-    // up to kCk tiles per thread (grids up to 4 * 1024 tiles, 4096^2): every
-    // global read of the thread is issued before the first is used and the
-    // tile values stay in registers; longer chunks loop over global memory
-    constexpr int kCk = 4;
-    const bool inreg = chunk <= (unsigned)kCk;
-    const int src[2] = {prof_src(ws, 0), prof_src(ws, 1)};
-    auto drift_at = [&](int sn, unsigned b) {
-        if (!use_prof) return 1.0;
-        const double f = ws.prof[(size_t)sn * (nt + 1) + b], q = ws.Pp[(size_t)sn * (nt + 1) + b];
-        return (q > 0.0 && f > 0.0 && f < INFINITY) ? f / q : 1.0;
-    };
-    double av[2][kCk];
-    float dv[2][kCk + 1];  // a prediction factor: float is plenty
-    unsigned hv[2][kCk];
-    if (inreg) {
-#pragma unroll
-        for (int k = 0; k < kCk; k++)
-#pragma unroll
-            for (int n = 0; n < 2; n++) {
-                const bool in = b0 + k < b1;
-                av[n][k] = in ? ws.A[2 * (size_t)(b0 + k) + n] : 0.0;
-                hv[n][k] = in ? ws.H[2 * (size_t)(b0 + k) + n] : 0u;
-            }
-        // drift at b0 .. b1 (b1: the next thread's first tile; prof / Pp hold
-        // nt + 1 entries)
-#pragma unroll
-        for (int k = 0; k <= kCk; k++)
-#pragma unroll
-            for (int n = 0; n < 2; n++)
-                dv[n][k] = (b0 < b1 && b0 + k <= b1) ? (float)drift_at(src[n], b0 + k) : 1.0f;
+// listed for segment entries (the walk resolves it).  Three launches over
+// every tile: (1) the last call's drift at each tile (read before this call
+// rewrites Pp) and the sums of blocks of kSnChk tiles, (2) one block scans the
+// block sums, (3) each block scans its tiles from its offset and checks them.
+// (A single 1024-thread block over every tile took 22 us at 4096^2 and 120
+// us at 8192^2, 600 us when it waited for CUs behind a triple launch.)
+constexpr int kSnChk = 256;  // tiles per block of the check
+constexpr unsigned kSnMissMax = 256;  // raw segments of a walk whose profile still predicts
+__device__ __forceinline__ double sn_drift(const SnWs &ws, unsigned nt, int src, unsigned b) {
+    const double f = ws.prof[(size_t)src * (nt + 1) + b], q = ws.Pp[(size_t)src * (nt + 1) + b];
+    return (q > 0.0 && f > 0.0 && f < INFINITY) ? f / q : 1.0;
+}
+__global__ __launch_bounds__(kSnChk) void seqnorm_check_sums(unsigned nt, SnWs ws, int use_prof) {
+    const unsigned b = blockIdx.x * kSnChk + threadIdx.x;
+    __shared__ double sh[2][kSnChk / 64];
+    for (int n = 0; n < 2; n++) {
+        if (b <= nt)
+            ws.dr[(size_t)n * (nt + 1) + b] =
+                use_prof ? (float)sn_drift(ws, nt, prof_src(ws, n), b) : 1.0f;
+        const double t = wave_reduce(b < nt ? ws.A[2 * (size_t)b + n] : 0.0,
+                                     [](double p, double x) { return p + x; });
+        if ((threadIdx.x & 63) == 0) sh[n][threadIdx.x / 64] = t;
     }
+    __syncthreads();
+    if (threadIdx.x < 2) {
+        double t = 0.0;
+        for (int k = 0; k < kSnChk / 64; k++) t += sh[threadIdx.x][k];
+        ws.bs[(size_t)threadIdx.x * gridDim.x + blockIdx.x] = t;
+    }
+}
+// exclusive scan of the nb block sums (in place) plus p_off (a row slab's
+// predecessors: the prediction is of the global running sum); Pp[nt] <- the
+// total
+__global__ __launch_bounds__(kSnScan) void seqnorm_check_scan(unsigned nt, unsigned nb, SnWs ws,
+                                                              const double *__restrict__ p_off) {
+    const unsigned chunk = (nb + kSnScan - 1) / kSnScan;
+    const unsigned k0 = min(nb, threadIdx.x * chunk), k1 = min(nb, k0 + chunk);
     __shared__ double sh[2][kSnScan];
     for (int n = 0; n < 2; n++) {
-        double s = 0.0;
-        if (inreg) {
-#pragma unroll
-            for (int k = 0; k < kCk; k++) s += av[n][k];
-        } else {
-            for (unsigned b = b0; b < b1; b++) s += ws.A[2 * (size_t)b + n];
-        }
-        sh[n][threadIdx.x] = s;
+        double t = 0.0;
+        for (unsigned k = k0; k < k1; k++) t += ws.bs[(size_t)n * nb + k];
+        sh[n][threadIdx.x] = t;
     }
     __syncthreads();
     for (int o = 1; o < kSnScan; o <<= 1) {
@@ -457,61 +455,88 @@ __global__ __launch_bounds__(kSnScan) void seqnorm_check(unsigned nt, SnWs ws, i
         sh[1][threadIdx.x] += v1;
         __syncthreads();
     }
-    const double del = use_prof ? 1.0 / 64 : 1.0 / 16;
-    double Pb[2], drift[2], dend[2];
-    // threads past the last tile (nt < kSnScan) read nothing
-    const bool active = b0 < b1;
+    double total[2];
     for (int n = 0; n < 2; n++) {
-        // p_off: the fp64 sum of the terms before this grid (a row slab's
-        // predecessors), so that the prediction is of the global running sum
-        Pb[n] = (threadIdx.x ? sh[n][threadIdx.x - 1] : 0.0) + (p_off ? p_off[n] : 0.0);
-        drift[n] = !active ? 1.0 : inreg ? dv[n][0] : drift_at(src[n], b0);
-        dend[n] = !active ? 1.0 : inreg ? dv[n][0] : drift_at(src[n], b1);  // (inreg: unused)
+        double run = (threadIdx.x ? sh[n][threadIdx.x - 1] : 0.0) + (p_off ? p_off[n] : 0.0);
+        for (unsigned k = k0; k < k1; k++) {
+            const double t = ws.bs[(size_t)n * nb + k];
+            ws.bs[(size_t)n * nb + k] = run;
+            run += t;
+        }
+        total[n] = run;
     }
-    __syncthreads();  // these reads of the last call's Pp before this call's writes
-    // one tile: the candidate window it needs against the one it has
-    auto tile = [&](unsigned b, const double a[2], const unsigned h0[2], const double dnext[2]) {
-        bool listed = false;
+    if (threadIdx.x == kSnScan - 1) {
+        // the profile predicts the drift of the float sum from the fp64 one
+        // only while the sums stay alike: the drift comes mostly from terms
+        // that vanish below half an ulp of the running sum, which moves with
+        // the terms' size (ws.cnt[1 + n]: the profile of norm n is usable)
+        // and while they predicted it: a walk that stepped many raw segments
+        // (binades its tiles' candidates missed) leaves a profile whose drift
+        // has moved on, and the next call on the workspace takes the wide window
         for (int n = 0; n < 2; n++) {
-            const unsigned h = h0[n];
-            if (!(h & (kHdrZero | kHdrNan)) && a[n] < INFINITY && Pb[n] < INFINITY) {
-                const unsigned want = cand_window(Pb[n] * drift[n] * (1.0 - del),
-                                                  (Pb[n] + a[n]) * dnext[n] * (1.0 + del));
-                const int wl = hdr_elo(want), wn = hdr_nc(want), hl = hdr_elo(h), hn = hdr_nc(h);
-                unsigned hh = h;
-                if (wn > 0 && (wl < hl || wl + wn > hl + hn)) hh = want | kHdrPending;
-                if (wn > 1 || b == 0) hh |= kHdrSegReq;
-                if (hh != h) ws.H[2 * (size_t)b + n] = hh;
-                listed |= (hh & (kHdrPending | kHdrSegReq)) != 0;
-            }
-            drift[n] = dnext[n];
+            const int src = prof_src(ws, n);
+            const double old = ws.Pp[(size_t)src * (nt + 1) + nt];
+            ws.cnt[1 + n] = (old > 0.0 && total[n] > 0.0 && total[n] < 1.25 * old &&
+                             total[n] > 0.8 * old && ws.miss[src] <= kSnMissMax)
+                                ? 1u
+                                : 0u;
         }
-        if (listed) ws.list[atomicAdd(&ws.cnt[0], 1u)] = b;
-        for (int n = 0; n < 2; n++) {
-            ws.Pp[(size_t)n * (nt + 1) + b] = Pb[n];
-            Pb[n] += a[n];
-        }
-    };
-    if (inreg) {
+        for (int n = 0; n < 2; n++) ws.Pp[(size_t)n * (nt + 1) + nt] = total[n];
+    }
+}
+__global__ __launch_bounds__(kSnChk) void seqnorm_check(unsigned nt, SnWs ws, int use_prof) {
+    const unsigned b = blockIdx.x * kSnChk + threadIdx.x;
+    const bool active = b < nt;
+    const int lane = threadIdx.x & 63, w = threadIdx.x / 64;
+    double a[2], Pb[2];
+    unsigned h[2];
+    float d0[2], d1[2];
+    __shared__ double sw[2][kSnChk / 64];
+    for (int n = 0; n < 2; n++) {
+        a[n] = active ? ws.A[2 * (size_t)b + n] : 0.0;
+        h[n] = active ? ws.H[2 * (size_t)b + n] : 0u;
+        d0[n] = active ? ws.dr[(size_t)n * (nt + 1) + b] : 1.0f;
+        d1[n] = active ? ws.dr[(size_t)n * (nt + 1) + b + 1] : 1.0f;
+        // the block's exclusive prefix: a wave scan, then the waves before
+        double x = a[n];
 #pragma unroll
-        for (int k = 0; k < kCk; k++) {
-            if (b0 + k >= b1) break;
-            const double a[2] = {av[0][k], av[1][k]};
-            const unsigned h[2] = {hv[0][k], hv[1][k]};
-            const double dn[2] = {dv[0][k + 1], dv[1][k + 1]};
-            tile(b0 + k, a, h, dn);
+        for (int o = 1; o < 64; o <<= 1) {
+            const double y = __shfl_up(x, o, 64);
+            if (lane >= o) x += y;
         }
-    } else {
-        for (unsigned b = b0; b < b1; b++) {
-            const double a[2] = {ws.A[2 * (size_t)b], ws.A[2 * (size_t)b + 1]};
-            const unsigned h[2] = {ws.H[2 * (size_t)b], ws.H[2 * (size_t)b + 1]};
-            double dn[2];
-            for (int n = 0; n < 2; n++) dn[n] = b + 1 == b1 ? dend[n] : drift_at(src[n], b + 1);
-            tile(b, a, h, dn);
-        }
+        if (lane == 63) sw[n][w] = x;
+        Pb[n] = x - a[n];
     }
-    if (b1 == nt && b0 < b1)
-        for (int n = 0; n < 2; n++) ws.Pp[(size_t)n * (nt + 1) + nt] = Pb[n];
+    __syncthreads();
+    for (int n = 0; n < 2; n++) {
+        double off = ws.bs[(size_t)n * gridDim.x + blockIdx.x];
+        for (int k = 0; k < w; k++) off += sw[n][k];
+        Pb[n] += off;
+    }
+    if (!active) return;
+    bool listed = false;
+    for (int n = 0; n < 2; n++) {
+        if (!(h[n] & (kHdrZero | kHdrNan)) && a[n] < INFINITY && Pb[n] < INFINITY) {
+            // with a usable profile: the prefix times its drift, 1/64 either
+            // side; without: the float sum below the fp64 prefix by up to a
+            // factor 16 (the kSnCand binades below 1/16 above it: past 2^24
+            // terms most small terms vanish below half an ulp and the float
+            // sum falls well behind; a miss costs the walk term-level steps)
+            const bool prof = use_prof && ws.cnt[1 + n] != 0;
+            const unsigned want =
+                prof ? cand_window(Pb[n] * d0[n] * (1.0 - 1.0 / 64),
+                                   (Pb[n] + a[n]) * d1[n] * (1.0 + 1.0 / 64))
+                     : cand_window(Pb[n] * (1.0 / 16), (Pb[n] + a[n]) * (1.0 + 1.0 / 16));
+            const int wl = hdr_elo(want), wn = hdr_nc(want), hl = hdr_elo(h[n]), hn = hdr_nc(h[n]);
+            unsigned hh = h[n];
+            if (wn > 0 && (wl < hl || wl + wn > hl + hn)) hh = want | kHdrPending;
+            if (wn > 1 || b == 0) hh |= kHdrSegReq;
+            if (hh != h[n]) ws.H[2 * (size_t)b + n] = hh;
+            listed |= (hh & (kHdrPending | kHdrSegReq)) != 0;
+        }
+        ws.Pp[(size_t)n * (nt + 1) + b] = Pb[n];
+    }
+    if (listed) ws.list[atomicAdd(&ws.cnt[0], 1u)] = b;
 }
 
 // fp64 total of the tile sums (a slab's contribution to its successors' p_off)
@@ -787,6 +812,7 @@ __global__ __launch_bounds__(64) void seqnorm_walk(const float2 *__restrict__ cu
         prof[nt] = S;
         ws.tot[2 * n + 1] = ws.tot[2 * n];
         ws.tot[2 * n] = S;
+        ws.miss[n] = (unsigned)raw;
         out[n] = S;
         if (dbg) {
             dbg[n] = resolves;
@@ -808,7 +834,9 @@ size_t seqnorm_workspace_bytes(int dimx, int dimy) {
                  2 * kSnCand * sizeof(unsigned) + 2 * kSnCand * kSnSegs * sizeof(unsigned) +
                  sizeof(unsigned)) +
            2 * (nt + 1) * (sizeof(double) + sizeof(float)) + 4 * sizeof(float) +
-           4 * sizeof(unsigned) + 2 * sizeof(double) + 256;
+           4 * sizeof(unsigned) + 2 * sizeof(double) +
+           2 * ((nt + 1 + kSnChk - 1) / kSnChk) * sizeof(double) + 2 * (nt + 1) * sizeof(float) +
+           2 * sizeof(unsigned) + 256;
 }
 
 namespace {
@@ -826,6 +854,9 @@ SnWs carve(void *ws, unsigned nt) {
     w.cnt = w.list + nt;
     w.tot64 = reinterpret_cast<double *>(
         (reinterpret_cast<uintptr_t>(w.cnt + 4) + 7) & ~static_cast<uintptr_t>(7));
+    w.bs = w.tot64 + 2;
+    w.dr = reinterpret_cast<float *>(w.bs + 2 * (size_t)((nt + 1 + kSnChk - 1) / kSnChk));
+    w.miss = reinterpret_cast<unsigned *>(w.dr + 2 * (size_t)(nt + 1));
     return w;
 }
 unsigned check_geometry(int dimx, int dimy, int P) {
@@ -867,8 +898,11 @@ void launch_seqnorm_refine(const float2 *cur, const float2 *prev, int dimx, int 
     const unsigned nt = check_geometry(dimx, dimy, P);
     const unsigned N = (unsigned)((size_t)dimx * dimy);
     const SnWs w = carve(ws, nt);
-    hipLaunchKernelGGL(seqnorm_check, dim3(1), dim3(kSnScan), 0, st, nt, w, use_profile ? 1 : 0,
-                       p_off);
+    const unsigned nb = (nt + 1 + kSnChk - 1) / kSnChk;  // blocks over tiles 0 .. nt
+    hipLaunchKernelGGL(seqnorm_check_sums, dim3(nb), dim3(kSnChk), 0, st, nt, w,
+                       use_profile ? 1 : 0);
+    hipLaunchKernelGGL(seqnorm_check_scan, dim3(1), dim3(kSnScan), 0, st, nt, nb, w, p_off);
+    hipLaunchKernelGGL(seqnorm_check, dim3(nb), dim3(kSnChk), 0, st, nt, w, use_profile ? 1 : 0);
     OF2D_HIP(hipGetLastError());
     hipLaunchKernelGGL(seqnorm_fix, dim3(std::min(nt, 1024u)), dim3(kSnThreads), 0, st, cur,
                        prev, N, dimx, P, nt, w);
