@@ -169,18 +169,21 @@ int of2d_motion_norms(const float *cur, const float *prev, int dimx, int dimy, i
         ws.alloc(of2d::seqnorm_workspace_bytes(dimx, dimy));
         of2d::DevArray<float> out;
         out.alloc(2 * (size_t)npairs);
+        // the walk's counters: the 8 of the ABI, then 2 more (tools)
+        constexpr int kSnDbg = 10;
         of2d::DevArray<int> dbg;
-        dbg.alloc(8 * (size_t)npairs);
+        dbg.alloc(kSnDbg * (size_t)npairs);
         for (int k = 0; k < npairs; k++) {
             // one workspace: each pair's walk predicts the next (its profile)
             OF2D_HIP(hipMemcpy2D(c.p, pitch, cur + k * n, row, row, dimy, hipMemcpyHostToDevice));
             OF2D_HIP(hipMemcpy2D(p.p, pitch, prev + k * n, row, row, dimy, hipMemcpyHostToDevice));
             of2d::launch_seqnorm(c.p, p.p, dimx, dimy, c.P, ws.p, k > 0, out.p + 2 * k,
-                                 dbg.p + 8 * k, nullptr);
+                                 dbg.p + kSnDbg * k, nullptr);
         }
         OF2D_HIP(hipMemcpy(sums, out.p, 2 * sizeof(float) * npairs, hipMemcpyDeviceToHost));
         if (stats)
-            OF2D_HIP(hipMemcpy(stats, dbg.p, 8 * sizeof(int) * npairs, hipMemcpyDeviceToHost));
+            OF2D_HIP(hipMemcpy2D(stats, 8 * sizeof(int), dbg.p, kSnDbg * sizeof(int),
+                                 8 * sizeof(int), npairs, hipMemcpyDeviceToHost));
     });
     if (rc != OF2D_OK) g_gateway_err = err;
     return rc;

@@ -213,8 +213,9 @@ struct PartialRuns {
 // holds the sums, not yet divided by N.  ws: seqnorm_workspace_bytes; it also
 // keeps each call's running-sum profile, which the next call on the same grid
 // uses as its prediction when use_profile is set (the result is exact either
-// way; a poor prediction costs time).  dbg (optional): tiles the walk had to
-// resolve below tile level, per norm.
+// way; a poor prediction costs time).  dbg (optional, int[10]): the walk's
+// cost counters (resolves, raw segments, listed tiles, clocks, tiles given
+// its own segment entries).
 constexpr int kSnTile = 4096;  // consecutive terms per tile
 size_t seqnorm_workspace_bytes(int dimx, int dimy);
 void launch_seqnorm(const float2 *cur, const float2 *prev, int dimx, int dimy, int P, void *ws,

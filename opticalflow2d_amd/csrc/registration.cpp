@@ -347,8 +347,9 @@ int Registration::run_chunked_exact(Level &L, int niter, int nb, const StepFn &s
     // OF2D_SN_DEBUG: the walks' cost counters per iteration to stderr
     // (resolves, raw segments, listed tiles, walk clocks; tools/ diagnostics)
     static const bool sn_debug = std::getenv("OF2D_SN_DEBUG") != nullptr;
+    constexpr int kDbg = 10;
     DevArray<int> dbg;
-    if (sn_debug) dbg.alloc(8 * (size_t)chunk_);
+    if (sn_debug) dbg.alloc(kDbg * (size_t)chunk_);
     // a new loop: its first two calls per workspace start from a fresh state
     bool walked[2] = {false, false};
     int a = 0, k0 = 0;
@@ -381,7 +382,7 @@ int Registration::run_chunked_exact(Level &L, int niter, int nb, const StepFn &s
                 OF2D_HIP(hipStreamWaitEvent(wk_st_, ev(ev_fix_, m), 0));
                 launch_seqnorm_walk(L.est[dst].p, L.est[src].p, L.dx, L.dy, L.P, d_seqws_[w].p,
                                     nullptr, d_seq_.p + 2 * (size_t)m,
-                                    sn_debug ? dbg.p + 8 * (size_t)m : nullptr, wk_st_);
+                                    sn_debug ? dbg.p + kDbg * (size_t)m : nullptr, wk_st_);
                 OF2D_HIP(hipEventRecord(ev(ev_walk_, m), wk_st_));
             }
             t += k;
@@ -391,14 +392,15 @@ int Registration::run_chunked_exact(Level &L, int niter, int nb, const StepFn &s
                                 st_));
         check_status();  // synchronises st_ (and with it every norm of the chunk)
         if (sn_debug) {
-            std::vector<int> h(8 * (size_t)C);
+            std::vector<int> h(kDbg * (size_t)C);
             OF2D_HIP(hipMemcpy(h.data(), dbg.p, h.size() * sizeof(int), hipMemcpyDeviceToHost));
             for (int t = 0; t < C; t++)
                 std::fprintf(stderr,
                              "seqnorm %dx%d it %d: resolves %d %d raw %d %d listed %d walk %d %d "
-                             "res %d\n",
-                             L.dx, L.dy, k0 + t, h[8 * t], h[8 * t + 1], h[8 * t + 2],
-                             h[8 * t + 3], h[8 * t + 4], h[8 * t + 5], h[8 * t + 6], h[8 * t + 7]);
+                             "res %d made %d %d\n",
+                             L.dx, L.dy, k0 + t, h[kDbg * t], h[kDbg * t + 1], h[kDbg * t + 2],
+                             h[kDbg * t + 3], h[kDbg * t + 4], h[kDbg * t + 5], h[kDbg * t + 6],
+                             h[kDbg * t + 7], h[kDbg * t + 8], h[kDbg * t + 9]);
         }
         for (int t = 0; t < C; t++) {
             const int k = k0 + t;

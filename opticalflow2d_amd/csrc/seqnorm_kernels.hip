@@ -669,12 +669,59 @@ __device__ float sn_raw_segment(const float2 *__restrict__ cur, const float2 *__
     return S;
 }
 
+// The segment entries of tile b for binade e, made by the walk's wave when
+// the tables hold none for it (a missed binade): lane s receives segment s's,
+// for the segments from sfrom (rounded down to 8) on.  Coalesced segments,
+// kSnNowBatch of them in flight: ~18 us for a whole tile.
+constexpr int kSnNowBatch = 32;
+__device__ unsigned sn_segments_now(const float2 *__restrict__ cur, const float2 *__restrict__ prev,
+                                    int which, unsigned b, int sfrom, int e, unsigned N, int dimx,
+                                    int P) {
+    const int lane = threadIdx.x & 63;
+    const double scale = sn_scale(e);
+    unsigned mine = 0;
+    const int sb = sfrom & ~7;
+    unsigned L = b * (unsigned)kSnTile + 64u * sb + lane;
+    unsigned j = L / (unsigned)dimx, i = L - j * (unsigned)dimx;
+    for (int s0 = sb; s0 < kSnSegs; s0 += kSnNowBatch) {
+        float2 cv[kSnNowBatch], pv[kSnNowBatch];
+#pragma unroll
+        for (int k = 0; k < kSnNowBatch; k++) {
+            cv[k] = pv[k] = make_float2(0.0f, 0.0f);
+            if (s0 + k < kSnSegs && L < N) {
+                const size_t off = (size_t)j * (size_t)P + i;
+                if (!which) cv[k] = cur[off];
+                pv[k] = prev[off];
+            }
+            L += 64u;
+            i += 64u;
+            while (i >= (unsigned)dimx) {
+                i -= (unsigned)dimx;
+                j++;
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < kSnNowBatch; k++) {
+            if (s0 + k >= kSnSegs) break;
+            // Field::operator- (Field.tpp:305-334) for |cur - prev|
+            const double d = which ? sn_mag(pv[k].x, pv[k].y)
+                                   : sn_mag(cv[k].x - pv[k].x, cv[k].y - pv[k].y);
+            bool bad = false;
+            const unsigned t = wave_sum(sn_incr(d, scale, bad));
+            const unsigned g = (t < kSnSat ? t : kSnSat) | (__ballot(bad) ? kSnBad : 0u);
+            if (lane == s0 + k) mine = g;
+        }
+    }
+    return mine;
+}
+
 // Tile b from the exact running sum S: its segment entries where one covers
-// the binade, raw segments where none does (a crossing, a tie, a missed
-// binade, the low sum).
+// the binade (the tables' or, where those miss it with more than a few
+// segments left, the walk's own), raw segments otherwise (a crossing, a tie,
+// the low sum).
 __device__ float sn_resolve(const float2 *__restrict__ cur, const float2 *__restrict__ prev,
                             int which, unsigned b, unsigned N, int dimx, int P, float S,
-                            unsigned h, const SnWs &ws, int &raw) {
+                            unsigned h, const SnWs &ws, int &raw, int &made) {
     const int lane = threadIdx.x & 63;
     const int nc = (h & kHdrSeg) ? hdr_nc(h) : 0, elo = hdr_elo(h);
     const unsigned long long zm = ws.Z[2 * (size_t)b + which];
@@ -682,14 +729,26 @@ __device__ float sn_resolve(const float2 *__restrict__ cur, const float2 *__rest
 #pragma unroll
     for (int c = 0; c < kSnCand; c++) g[c] = c < nc ? ws.G[g_index(b, which, c, lane)] : 0u;
     int s0 = 0;
+    int enow = kSnLow;  // the binade of gnow
+    int rawhere = 0;
+    unsigned gnow = 0;
     while (s0 < kSnSegs) {
         const int e = sn_region(S);
         const int c = e - elo;
-        if (e != kSnLow && e != kSnNonfinite && c >= 0 && c < nc) {
-            unsigned gc = g[0];
+        const bool table = c >= 0 && c < nc;
+        // the tile's own entries once raw steps have not brought S back into
+        // the tables' binades (~0.3 us per segment against ~1.1 us per raw one)
+        if (e != kSnLow && e != kSnNonfinite && !table && e != enow && rawhere >= 6 &&
+            kSnSegs - s0 > 16) {
+            gnow = sn_segments_now(cur, prev, which, b, s0, e, N, dimx, P);
+            enow = e;
+            made++;
+        }
+        if (e != kSnLow && e != kSnNonfinite && (table || e == enow)) {
+            unsigned gc = table ? g[0] : gnow;
 #pragma unroll
             for (int k = 1; k < kSnCand; k++)
-                if (c == k) gc = g[k];
+                if (table && c == k) gc = g[k];
             const unsigned M = sn_mant(S);
             const unsigned v = lane >= s0 ? (gc & ~kSnBad) : 0u;
             const unsigned incl = wave_incl_sat(v);
@@ -707,6 +766,7 @@ __device__ float sn_resolve(const float2 *__restrict__ cur, const float2 *__rest
         }
         S = sn_raw_segment(cur, prev, which, b, s0, N, dimx, P, S);
         raw++;
+        rawhere++;
         s0++;
     }
     return S;
@@ -717,7 +777,8 @@ constexpr int kSnAhead = 8;  // windows loaded per step: the next step's loads h
 // One wave per norm walks the tiles in windows of 64 (lane = tile): the
 // saturating scan of the entries for S's binade, a resolve at each tile whose
 // entry does not apply.  Writes every tile's start sum into the profile.
-// dbg: resolves (per norm), raw segments (per norm), listed tiles.
+// dbg: resolves (per norm), raw segments (per norm), listed tiles, walk and
+// resolve clocks, tiles given the walk's own segment entries (per norm).
 __global__ __launch_bounds__(64) void seqnorm_walk(const float2 *__restrict__ cur,
                                                    const float2 *__restrict__ prev, unsigned N,
                                                    int dimx, int P, unsigned nt, SnWs ws,
@@ -748,7 +809,7 @@ __global__ __launch_bounds__(64) void seqnorm_walk(const float2 *__restrict__ cu
     // slab's result), 0 without one
     float S = s_in ? s_in[n] : 0.0f;
     int resolves = 0;
-    int raw = 0;
+    int raw = 0, made = 0;
     bool nan = false;  // non-finite sum: a NaN magnitude after it
     const long long c0 = wall_clock64();
     long long cres = 0;
@@ -800,7 +861,7 @@ __global__ __launch_bounds__(64) void seqnorm_walk(const float2 *__restrict__ cu
                 }
                 if (!low) S = sn_make(e, M + lane_at(excl, q));
                 const long long r0 = wall_clock64();
-                S = sn_resolve(cur, prev, n, b0 + q, N, dimx, P, S, lane_at(h, q), ws, raw);
+                S = sn_resolve(cur, prev, n, b0 + q, N, dimx, P, S, lane_at(h, q), ws, raw, made);
                 cres += wall_clock64() - r0;
                 resolves++;
                 start = q + 1;
@@ -812,7 +873,7 @@ __global__ __launch_bounds__(64) void seqnorm_walk(const float2 *__restrict__ cu
         prof[nt] = S;
         ws.tot[2 * n + 1] = ws.tot[2 * n];
         ws.tot[2 * n] = S;
-        ws.miss[n] = (unsigned)raw;
+        ws.miss[n] = (unsigned)(raw + 32 * made);  // as raw segments
         out[n] = S;
         if (dbg) {
             dbg[n] = resolves;
@@ -821,6 +882,7 @@ __global__ __launch_bounds__(64) void seqnorm_walk(const float2 *__restrict__ cu
             // wall-clock ticks (100 MHz) of the whole walk and of its resolves
             dbg[5 + n] = (int)(wall_clock64() - c0);
             if (n == 0) dbg[7] = (int)cres;
+            dbg[8 + n] = made;
         }
     }
 }

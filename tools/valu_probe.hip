@@ -1,7 +1,7 @@
 // valu_probe.hip — issue cost of packed vs scalar fp32 VALU on gfx950 for one
 // wave alone and for four waves on one SIMD (not part of the product): loops
 // of independent and dependent v_add_f32 / v_pk_add_f32 / v_pk_mul_f32 /
-// v_mov_b32_dpp in inline asm, cycles from s_memtime per instruction.
+// v_mov_b32_dpp and fp64 add / mul / rsq / rndne in inline asm, cycles from s_memtime per instruction.
 //   hipcc --offload-arch=gfx950 -O3 tools/valu_probe.hip -o tools/valu_probe
 #include <hip/hip_runtime.h>
 
@@ -46,6 +46,16 @@ __global__ void probe(float *out, long long *cyc, int iters) {
             REP8(asm volatile("v_add_f32_dpp %0, %8, %0 wave_shr:1 row_mask:0xf bank_mask:0xf\n v_add_f32_dpp %1, %8, %1 wave_shr:1 row_mask:0xf bank_mask:0xf\n v_add_f32_dpp %2, %8, %2 wave_shr:1 row_mask:0xf bank_mask:0xf\n v_add_f32_dpp %3, %8, %3 wave_shr:1 row_mask:0xf bank_mask:0xf\n v_add_f32_dpp %4, %8, %4 wave_shr:1 row_mask:0xf bank_mask:0xf\n v_add_f32_dpp %5, %8, %5 wave_shr:1 row_mask:0xf bank_mask:0xf\n v_add_f32_dpp %6, %8, %6 wave_shr:1 row_mask:0xf bank_mask:0xf\n v_add_f32_dpp %7, %8, %7 wave_shr:1 row_mask:0xf bank_mask:0xf"
                          : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7)
                          : "v"(kk));)
+        } else if constexpr (MODE >= 7) {  // fp64: 8 independent ops x 8
+            double d0 = a0, d1 = a1, d2 = a2, d3 = a3;
+            const double dk = 1e-9;
+#define F64X8(op) REP8(asm volatile(op " %0, %0, %4\n " op " %1, %1, %4\n " op " %2, %2, %4\n " op " %3, %3, %4\n " op " %0, %0, %4\n " op " %1, %1, %4\n " op " %2, %2, %4\n " op " %3, %3, %4" : "+v"(d0), "+v"(d1), "+v"(d2), "+v"(d3) : "v"(dk));)
+#define F64U8(op) REP8(asm volatile(op " %0, %0\n " op " %1, %1\n " op " %2, %2\n " op " %3, %3\n " op " %0, %0\n " op " %1, %1\n " op " %2, %2\n " op " %3, %3" : "+v"(d0), "+v"(d1), "+v"(d2), "+v"(d3));)
+            if constexpr (MODE == 7) { F64X8("v_add_f64") }
+            else if constexpr (MODE == 8) { F64X8("v_mul_f64") }
+            else if constexpr (MODE == 9) { F64U8("v_rsq_f64") }
+            else if constexpr (MODE == 10) { F64U8("v_rndne_f64") }
+            a0 += (float)(d0 + d1 + d2 + d3);
         }
     }
     const long long t1 = __builtin_amdgcn_s_memtime();
@@ -82,6 +92,10 @@ int main() {
         run<3>("v_pk_add_f32 dependent chain", w, out, cyc);
         run<5>("v_mov_b32_dpp wave_shr independent", w, out, cyc);
         run<6>("v_add_f32_dpp wave_shr (folded) independent", w, out, cyc);
+        run<7>("v_add_f64 independent", w, out, cyc);
+        run<8>("v_mul_f64 independent", w, out, cyc);
+        run<9>("v_rsq_f64 independent", w, out, cyc);
+        run<10>("v_rndne_f64 independent", w, out, cyc);
     }
     return 0;
 }
