@@ -33,6 +33,9 @@
 //     word.
 #include "of2d_device.h"
 
+#include <algorithm>
+#include <cstdlib>
+
 namespace of2d {
 
 namespace {
@@ -272,20 +275,194 @@ template <bool B>
 struct Flag {
     static constexpr bool value = B;
 };
+
+// ---------------------------------------------------------------- increment
+// behind the sweep.  The Fluid sweep's grid carries `nc` more workgroups
+// (tickets nstrips .. nstrips + nc - 1, so every strip is running before any
+// of them waits) that compute the increment R = v - dudx v.x - dudy v.y and
+// the per-tile maxima of increment_kernel (same tiles, same operations, same
+// partial slots) on the 64 x 32 tiles whose strips have finished, while later
+// strips still relax: the sweep keeps one wave on ~130 of 1024 SIMDs busy, the
+// rest of the chip is idle.  Hand-off (MI355X guide G16, the plain-store
+// form): each strip stores v as before (plain), and at its end drains
+// (s_waitcnt vmcnt(0)), releases (fence release agent: L2 write-back) and one
+// lane stores done[strip] = epoch (sc1); a worker polls done[] with sc1 loads,
+// then one agent acquire and plain loads.  (sc1 write-through v stores with
+// no release: +27 % per 8192^2 sweep, the in-order vmcnt makes the row loads
+// wait for stores that now go to HBM; no change at 2048^2, where the array
+// sits in the MALL; profiles/r03bc_*.)  Tiles are taken in column-band order from a
+// 64-bit counter (each launch adds exactly ntiles + nc, so a launch's grabs
+// are that count modulo ntiles + nc); every wait is bounded in time.
+struct SorInc {
+    const float2 *u;           // the estimate (not written in the launch)
+    float2 *R;                 // increment, row-major
+    float *part;               // per-tile max of (float)(2 R.y^2), increment_kernel's slots
+    unsigned *done;            // per strip: epoch of its last finished sweep
+    unsigned long long *ctr;   // [0] role ticket, [1] tile counter
+    int nwg, ntiles, nby;      // worker workgroups (4 waves each), tiles, tile rows
+};
+constexpr unsigned long long kIncWaitTicks = 200000000ull;  // 2 s of s_memrealtime (100 MHz)
+
+__device__ __forceinline__ unsigned ld_sc1_u32(const unsigned *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// one worker wave: tiles until the counter runs out.  Out of line: inlined, its
+// registers raised the strips' SGPR spills from 9 to 156 (v_readlane in the
+// sweep's loop)
+__device__ __attribute__((noinline)) void sor_increment_worker(const float4 *__restrict__ vb, int dimx, int dimy, int P,
+                                     int nstrips, unsigned epoch, const SorInc &w,
+                                     unsigned *__restrict__ status) {
+    // the tile's velocities (kSkJ x kSkI, as increment_kernel), one per wave:
+    // the waves of a worker workgroup run independent tile loops, so they
+    // synchronise only within themselves (LDS ops of one wave run in order)
+    __shared__ float2 vts[4][32][64];
+    const int lane = threadIdx.x & 63;
+    float2 (*vt)[64] = vts[threadIdx.x >> 6];
+    const unsigned long long M = (unsigned long long)w.ntiles + 4ull * (unsigned long long)w.nwg;
+    const float2 *__restrict__ vb2 = reinterpret_cast<const float2 *>(vb);
+    for (;;) {
+        int k0 = 0;
+        if (lane == 0) k0 = (int)(atomicAdd(&w.ctr[1], 1ull) % M);
+        const int k = __builtin_amdgcn_readfirstlane(k0);
+        if (k >= w.ntiles) break;
+        const int bx = k / w.nby, by = k - bx * w.nby;
+        const int i0 = bx * 64, j0 = by * 32;
+        // the estimate around the tile (not written in this launch: plain
+        // loads), issued before the wait: rows j0-1 .. j0+32 of the lane's
+        // column and the side columns of rows j0 .. j0+31, indices clamped
+        // into the image (a clamped value is never used, gradients.h's
+        // one-sided border taps take the others)
+        float2 uc[34], ul[32], ur[32];
+        {
+            const int ic = min(i0 + lane, dimx - 1);
+            const int il = max(ic - 1, 0), ir = min(ic + 1, dimx - 1);
+#pragma unroll
+            for (int r = 0; r < 34; r++) {
+                const long row = (long)min(max(j0 - 1 + r, 0), dimy - 1) * P;
+                uc[r] = w.u[row + ic];
+                if (r >= 1 && r <= 32) {
+                    ul[r - 1] = w.u[row + il];
+                    ur[r - 1] = w.u[row + ir];
+                }
+            }
+        }
+        // strips over the tile's relaxed columns [max(i0, 1), min(i0 + 63, dimx - 2)]
+        const int ca = max(i0, 1), cb = min(i0 + 63, dimx - 2);
+        if (ca <= cb) {
+            const int Ia = (ca - 1) / 63, Ib = min((cb - 1) / 63, nstrips - 1);
+            const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+            bool ok = true;
+            for (int I = Ib; I >= Ia; I--) {  // the last strip finishes last
+                while (ld_sc1_u32(&w.done[I]) != epoch) {
+                    if (__builtin_amdgcn_s_memrealtime() - t0 > kIncWaitTicks) {
+                        ok = false;
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(64);
+                }
+                if (!ok) break;
+            }
+            if (!ok && lane == 0) atomicOr(status, kStatusSpinTimeout);
+        }
+        // one agent acquire after the poll (this CU's L1 may hold lines of v
+        // from before the strips' release), then plain loads
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        // v of the tile along its skewed runs (increment_kernel's skew_tile_for_each,
+        // the four thread rows in turn)
+        {
+            const int q = lane >> 4, kk = lane & 15;
+            float2 x[4 * 10];
+            int slot[4 * 10];
+#pragma unroll
+            for (int y = 0; y < 4; y++)
+#pragma unroll
+                for (int it = 0; it < 10; it++) {
+                    const int s = 16 * it + 4 * y + q;
+                    const int ii = max(0, (s - 30) >> 1) + kk, jj = s - 2 * ii;
+                    const bool in = s < 2 * 63 + 32 && ii < 64 && jj >= 0 && jj < 32 &&
+                                    i0 + ii < dimx && j0 + jj < dimy;
+                    slot[10 * y + it] = in ? jj * 64 + ii : -1;
+                    x[10 * y + it] = in ? vb2[sor_v(i0 + ii, j0 + jj, P)] : make_float2(0.0f, 0.0f);
+                }
+#pragma unroll
+            for (int n = 0; n < 40; n++)
+                if (slot[n] >= 0) (&vt[0][0])[slot[n]] = x[n];
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const int i = i0 + lane;
+        float m = 0.0f;
+#pragma unroll
+        for (int rr = 0; rr < 32; rr++) {
+            const int j = j0 + rr;
+            if (i < dimx && j < dimy) {
+                const long idx = (long)j * P + i;
+                const float2 v = vt[rr][lane];
+                // motion_gradients (gradients.h:9-32) from the rows loaded up front
+                const float2 c = uc[rr + 1];
+                float2 dx, dy;
+                if (i == 0)
+                    dx = make_float2(ur[rr].x - c.x, ur[rr].y - c.y);
+                else if (i == dimx - 1)
+                    dx = make_float2(c.x - ul[rr].x, c.y - ul[rr].y);
+                else
+                    dx = make_float2((ur[rr].x - ul[rr].x) / 2.0f, (ur[rr].y - ul[rr].y) / 2.0f);
+                if (j == 0)
+                    dy = make_float2(uc[rr + 2].x - c.x, uc[rr + 2].y - c.y);
+                else if (j == dimy - 1)
+                    dy = make_float2(c.x - uc[rr].x, c.y - uc[rr].y);
+                else
+                    dy = make_float2((uc[rr + 2].x - uc[rr].x) / 2.0f,
+                                     (uc[rr + 2].y - uc[rr].y) / 2.0f);
+                // (v - dudx*v.x) - dudy*v.y (OpticalFlowFluid.cpp:84), as increment_kernel
+                const float2 r = make_float2((v.x - dx.x * v.x) - dy.x * v.y,
+                                             (v.y - dx.y * v.x) - dy.y * v.y);
+                w.R[idx] = r;
+                const double yy = (double)r.y;
+                const float qq = (float)(yy * yy + yy * yy);
+                m = (m < qq) ? qq : m;
+            }
+        }
+        for (int off = 32; off > 0; off >>= 1) {
+            const float o = __shfl_down(m, off);
+            m = (m < o) ? o : m;
+        }
+        if (lane == 0) w.part[(long)by * ((dimx + 63) / 64) + bx] = m;
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");  // vt is rewritten by the next tile
+    }
+}
 }  // namespace
 
-__global__ __launch_bounds__(64) void sor_strip_kernel(float4 *__restrict__ vb, int dimx, int dimy,
+template <bool kInc>
+__global__ __launch_bounds__(kInc ? 256 : 64) void sor_strip_kernel(float4 *__restrict__ vb, int dimx, int dimy,
                                                        int P, float A, float B, float M, float ML,
                                                        v4u *__restrict__ H, long Hstride,
                                                        unsigned epoch,
                                                        unsigned *__restrict__ ticket, int nstrips,
                                                        unsigned *__restrict__ status,
-                                                       unsigned long long *__restrict__ trace) {
+                                                       unsigned long long *__restrict__ trace,
+                                                       SorInc inc) {
     const int lane = threadIdx.x;
     __shared__ int s_strip;
-    if (lane == 0) s_strip = (int)(atomicAdd(ticket, 1u) % (unsigned)nstrips);
+    if (lane == 0) {
+        if constexpr (kInc)
+            s_strip = (int)(atomicAdd(&inc.ctr[0], 1ull) %
+                            (unsigned long long)(nstrips + inc.nwg));
+        else
+            s_strip = (int)(atomicAdd(ticket, 1u) % (unsigned)nstrips);
+    }
     __syncthreads();
     const int I = __builtin_amdgcn_readfirstlane(s_strip);
+    if constexpr (kInc) {
+        if (I >= nstrips) {
+            sor_increment_worker(vb, dimx, dimy, P, nstrips, epoch, inc, status);
+            return;
+        }
+        if (threadIdx.x >= 64) return;  // a strip is one wave; its CU stays to itself
+    }
     // optional timeline (tools/sor_harness.hip): start, end, polled batches,
     // shader cycles
     const unsigned long long t_start = trace ? __builtin_amdgcn_s_memrealtime() : 0;
@@ -451,6 +628,13 @@ __global__ __launch_bounds__(64) void sor_strip_kernel(float4 *__restrict__ vb, 
         trace[4 * I + 2] = npoll;
         trace[4 * I + 3] = __builtin_amdgcn_s_memtime() - c_start;
     }
+    if constexpr (kInc) {  // the strip's v stores drained and released, then its flag
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (lane == 0)
+            __hip_atomic_store(&inc.done[I], epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
 }
 
 int sor_nstrips(int dimx) { return dimx < 3 ? 0 : (dimx - 2 + kSorCols - 1) / kSorCols; }
@@ -468,8 +652,9 @@ void launch_sor_traced(float4 *vb, int dimx, int dimy, int P, float mu, float la
     const float A = 1.0f - omega;
     const float B = omega / (-6 * mu - 2 * lambda);
     const float ML = mu + lambda;
-    hipLaunchKernelGGL(sor_strip_kernel, dim3(ns), dim3(64), 0, st, vb, dimx, dimy, P, A, B, mu,
-                       ML, (v4u *)H, sor_granule_stride(dimy), epoch, ticket, ns, status, trace);
+    hipLaunchKernelGGL(sor_strip_kernel<false>, dim3(ns), dim3(64), 0, st, vb, dimx, dimy, P, A,
+                       B, mu, ML, (v4u *)H, sor_granule_stride(dimy), epoch, ticket, ns, status,
+                       trace, SorInc{});
     OF2D_HIP(hipGetLastError());
 }
 void launch_sor(float4 *vb, int dimx, int dimy, int P, float mu, float lambda, float omega,
@@ -709,6 +894,50 @@ void launch_increment(const float2 *u, const float4 *vel, float2 *R, int dimx, i
     const dim3 g = field_grid(dimx, dimy);
     hipLaunchKernelGGL(increment_kernel, g, dim3(64, 4), 0, st, u, vel, R, dimx, dimy, P, part);
     hipLaunchKernelGGL(timestep_kernel, dim3(1), dim3(1024), 0, st, part, (int)(g.x * g.y), scal);
+    OF2D_HIP(hipGetLastError());
+}
+
+int sor_increment_workers() {
+    static const int nc = [] {
+        // A/B knob: worker workgroups (-1: every CU the strips leave; 0: separate
+        // increment pass)
+        const char *e = std::getenv("OF2D_SOR_NCONS");
+        return e ? std::atoi(e) : -1;
+    }();
+    return nc;
+}
+
+void launch_sor_increment(float4 *vb, int dimx, int dimy, int P, float mu, float lambda,
+                          float omega, void *H, unsigned epoch, unsigned *ticket,
+                          unsigned long long *ctr, const float2 *u, float2 *R, float *part,
+                          float *scal, unsigned *status, hipStream_t st) {
+    const int ns = sor_nstrips(dimx);
+    const dim3 g = field_grid(dimx, dimy);
+    const int ntiles = (int)(g.x * g.y);
+    // one 256-thread workgroup per CU (a strip's or a worker's; registers
+    // allow one wave per SIMD): no strip shares its CU's load path
+    int dev = 0, ncu = 0;
+    OF2D_HIP(hipGetDevice(&dev));
+    OF2D_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+    int nwg = sor_increment_workers();
+    if (nwg < 0) nwg = ncu - ns;
+    nwg = std::min(nwg, (ntiles + 3) / 4);
+    if (ns == 0 || dimx < 3 || dimy < 3 || nwg < 8) {  // no sweep (OpticalFlowFluid.cpp:23-24)
+        launch_sor(vb, dimx, dimy, P, mu, lambda, omega, H, epoch, ticket, status, st);
+        launch_increment(u, vb, R, dimx, dimy, P, part, scal, st);
+        return;
+    }
+    const float A = 1.0f - omega;
+    const float B = omega / (-6 * mu - 2 * lambda);
+    const float ML = mu + lambda;
+    // OF2D_SOR_INC_SKIP=1 (A/B timing only, wrong results): the workers take
+    // no tile, which leaves the sweep's own cost with the workers' code in it
+    static const bool skip = std::getenv("OF2D_SOR_INC_SKIP") != nullptr;
+    const SorInc inc{u, R, part, ticket + 1, ctr, nwg, skip ? 0 : ntiles, (int)g.y};
+    hipLaunchKernelGGL(sor_strip_kernel<true>, dim3(ns + nwg), dim3(256), 0, st, vb, dimx, dimy,
+                       P, A, B, mu, ML, (v4u *)H, sor_granule_stride(dimy), epoch, nullptr, ns,
+                       status, nullptr, inc);
+    hipLaunchKernelGGL(timestep_kernel, dim3(1), dim3(1024), 0, st, part, ntiles, scal);
     OF2D_HIP(hipGetLastError());
 }
 

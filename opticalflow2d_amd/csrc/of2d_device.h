@@ -348,6 +348,18 @@ void launch_regrid_pack(const float *Iref, const float *Iaux, float2 *dI, float 
 void launch_force(const float2 *u, const float2 *dI, const float *It, float2 *f, int dimx,
                   int dimy, int P, hipStream_t st);
 int increment_nblocks(int dimx, int dimy);
+// the Fluid sweep with the increment behind it (fluid_kernels.hip SorInc): the
+// sweep of launch_sor plus launch_increment's R, partials and scal in one
+// launch (+ the timestep reduction).  ticket: 1 + nstrips words of the level
+// (the sweep ticket, then per strip its last finished epoch), zero at
+// allocation; ctr: 2 counters, zero at allocation.  Falls back to launch_sor
+// + launch_increment where too few CUs are left for workers; with
+// sor_increment_workers() == 0 (OF2D_SOR_NCONS=0) the caller runs those.
+int sor_increment_workers();
+void launch_sor_increment(float4 *vb, int dimx, int dimy, int P, float mu, float lambda,
+                          float omega, void *H, unsigned epoch, unsigned *ticket,
+                          unsigned long long *ctr, const float2 *u, float2 *R, float *part,
+                          float *scal, unsigned *status, hipStream_t st);
 // R and scal[0] = maxabs(R), scal[1] = 0.65f / maxabs
 void launch_increment(const float2 *u, const float4 *vel, float2 *R, int dimx, int dimy, int P,
                       float *part, float *scal, hipStream_t st);

@@ -124,7 +124,9 @@ struct Level {
     DevArray<double> cE;                    // Curvature: eigenvalues (pitch P)
     Field<float4> vb;                   // SOR working array {v, b} (Fluid: persistent velocity)
     DevArray<unsigned long long> sorH;  // SOR strip hand-off granules
-    DevArray<unsigned> sorTicket;       // SOR strip ticket (multiple of nstrips between sweeps)
+    DevArray<unsigned> sorTicket;       // SOR strip ticket (multiple of nstrips between sweeps);
+                                        // Fluid: then per strip its last finished epoch
+    DevArray<unsigned long long> sorCtr;  // Fluid sweep + increment: role ticket, tile counter
     DevArray<float> part;               // per-block float partials (max / min reductions)
     float2 *cur_motion() { return motion[mcur].p; }
 };

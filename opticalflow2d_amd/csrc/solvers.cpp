@@ -28,7 +28,8 @@ void alloc_level(Level &L, int reg) {
             L.force.alloc(L.dx, L.dy);
             L.tmp.alloc(L.dx, L.dy);
             L.sorH.alloc(sor_granule_bytes(L.dx, L.dy) / sizeof(unsigned long long));
-            L.sorTicket.alloc(1);
+            L.sorTicket.alloc(reg == 5 ? 1 + (size_t)sor_nstrips(L.dx) : 1);
+            if (reg == 5) L.sorCtr.alloc(2);
             L.part.alloc((size_t)increment_nblocks(L.dx, L.dy));
             L.vb.alloc(L.dx, sor_rows(L.dx, L.dy));  // skewed v | b rows; Fluid: v is the velocity
             if (reg == 5) L.increment.alloc(L.dx, L.dy);
@@ -181,9 +182,15 @@ int Registration::loop_fluid(Level &L, int niter) {
             launch_sor_pack(L.vb.p, est, L.dI.p, L.It.p, nullptr, L.dx, L.dy, L.P, L.sorH.p, ep,
                             st_);
         regridded = false;
-        launch_sor(L.vb.p, L.dx, L.dy, L.P, mu, lambda, omega, L.sorH.p, ep, L.sorTicket.p,
-                   d_status_, st_);
-        launch_increment(est, L.vb.p, L.increment.p, L.dx, L.dy, L.P, L.part.p, scal, st_);
+        if (sor_increment_workers() != 0) {  // the increment rides behind the sweep
+            launch_sor_increment(L.vb.p, L.dx, L.dy, L.P, mu, lambda, omega, L.sorH.p, ep,
+                                 L.sorTicket.p, L.sorCtr.p, est, L.increment.p, L.part.p, scal,
+                                 d_status_, st_);
+        } else {
+            launch_sor(L.vb.p, L.dx, L.dy, L.P, mu, lambda, omega, L.sorH.p, ep, L.sorTicket.p,
+                       d_status_, st_);
+            launch_increment(est, L.vb.p, L.increment.p, L.dx, L.dy, L.P, L.part.p, scal, st_);
+        }
         // integrate, Logger, Jacobian and the next iteration's force in one pass
         launch_fluid_step(est, L.increment.p, L.force.p, prev_separate ? prev : nullptr, scal,
                           L.dI.p, L.It.p, L.vb.p, L.dx, L.dy, L.P, L.sorH.p, ep + 1, d_partial_,

@@ -81,6 +81,20 @@ def test_fluid_many_strips_512(gpu, oracle):
     assert body(gt) == body(ot)
 
 
+def test_fluid_increment_workers_ragged(gpu, oracle):
+    """Levels whose sweep carries the increment workers (fluid_kernels.hip SorInc:
+    1000 x 777 -> 16 strips, 400 tiles; 500 x 388 -> 8 strips, 104 tiles): ragged
+    last strip and tiles, regridding, two pyramid levels, printed lines."""
+    ref, mov = S.shifted_disk(1000, shift=(30, 18))
+    ref, mov = ref[:, :777], mov[:, :777]
+    g, w, gt, ot = run_both(gpu, oracle, (1000, 777), [14, 10], 1, 5, [0.25, 0.0, 0.9], 1,
+                            ref, mov)
+    assert g["iters"] == w["iters"]
+    assert np.array_equal(g["motion"], w["motion"])
+    assert body(gt) == body(ot)
+    assert any(l.startswith("Regridding") for l in body(gt))
+
+
 @pytest.mark.parametrize("chunk", [1, 5, 32])
 def test_elastic_chunked_with_break(gpu, oracle, chunk):
     ref, mov = S.texture_pair(90, seed=12, ny=77)
