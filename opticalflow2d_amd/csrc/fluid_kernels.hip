@@ -34,6 +34,7 @@
 #include "of2d_device.h"
 
 #include <algorithm>
+#include <atomic>
 #include <cstdlib>
 
 namespace of2d {
@@ -916,9 +917,15 @@ void launch_sor_increment(float4 *vb, int dimx, int dimy, int P, float mu, float
     const int ntiles = (int)(g.x * g.y);
     // one 256-thread workgroup per CU (a strip's or a worker's; registers
     // allow one wave per SIMD): no strip shares its CU's load path
-    int dev = 0, ncu = 0;
+    int dev = 0;
     OF2D_HIP(hipGetDevice(&dev));
-    OF2D_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+    // per device, queried once (the launch is on the host's critical path)
+    static std::atomic<int> cus[64];
+    int ncu = cus[dev & 63].load(std::memory_order_relaxed);
+    if (ncu == 0) {
+        OF2D_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+        cus[dev & 63].store(ncu, std::memory_order_relaxed);
+    }
     int nwg = sor_increment_workers();
     if (nwg < 0) nwg = ncu - ns;
     nwg = std::min(nwg, (ntiles + 3) / 4);
