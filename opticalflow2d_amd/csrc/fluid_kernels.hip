@@ -937,10 +937,7 @@ void launch_sor_increment(float4 *vb, int dimx, int dimy, int P, float mu, float
     const float A = 1.0f - omega;
     const float B = omega / (-6 * mu - 2 * lambda);
     const float ML = mu + lambda;
-    // OF2D_SOR_INC_SKIP=1 (A/B timing only, wrong results): the workers take
-    // no tile, which leaves the sweep's own cost with the workers' code in it
-    static const bool skip = std::getenv("OF2D_SOR_INC_SKIP") != nullptr;
-    const SorInc inc{u, R, part, ticket + 1, ctr, nwg, skip ? 0 : ntiles, (int)g.y};
+    const SorInc inc{u, R, part, ticket + 1, ctr, nwg, ntiles, (int)g.y};
     hipLaunchKernelGGL(sor_strip_kernel<true>, dim3(ns + nwg), dim3(256), 0, st, vb, dimx, dimy,
                        P, A, B, mu, ML, (v4u *)H, sor_granule_stride(dimy), epoch, nullptr, ns,
                        status, nullptr, inc);

@@ -2,8 +2,8 @@
 # Fluid sweep with the increment behind it (SorInc): fluid GPU tests, then
 # config 4 under environment settings (interleaved), then kernel traces.
 #   tools/sor_inc_ab.sh <tag> [setting ...]   setting: VAR=value[,VAR=value]
-#   (OF2D_SOR_NCONS=0: separate increment pass; OF2D_SOR_INC_SKIP=1: workers
-#    take no tile, timing only)
+#   (OF2D_SOR_NCONS=0: separate increment pass; N: N worker workgroups; the
+#    timing-only OF2D_SOR_INC_SKIP of profiles/r03bf_* lived at commit 246f03d)
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 OUT=gpurun_out
