@@ -731,17 +731,26 @@ __device__ float sn_resolve(const float2 *__restrict__ cur, const float2 *__rest
     int s0 = 0;
     int enow = kSnLow;  // the binade of gnow
     int rawhere = 0;
+    int made_at = -kSnSegs;  // segment at which gnow was made
+    bool no_more = false;    // a made set of entries served < 16 segments: step raw
     unsigned gnow = 0;
     while (s0 < kSnSegs) {
         const int e = sn_region(S);
         const int c = e - elo;
         const bool table = c >= 0 && c < nc;
         // the tile's own entries once raw steps have not brought S back into
-        // the tables' binades (~0.3 us per segment against ~1.1 us per raw one)
+        // the tables' binades (~0.3 us per segment against ~1.1 us per raw one,
+        // ~18 us to make them: worth it only while S stays in the binade, so
+        // not again in a tile where S left made entries within 16 segments,
+        // e.g. a sum still growing through many binades; 256^2 config 1)
+        if (e != kSnLow && e != kSnNonfinite && !table && e != enow && enow != kSnLow &&
+            s0 - made_at < 16)
+            no_more = true;
         if (e != kSnLow && e != kSnNonfinite && !table && e != enow && rawhere >= 6 &&
-            kSnSegs - s0 > 16) {
+            kSnSegs - s0 > 16 && !no_more) {
             gnow = sn_segments_now(cur, prev, which, b, s0, e, N, dimx, P);
             enow = e;
+            made_at = s0;
             made++;
         }
         if (e != kSnLow && e != kSnNonfinite && (table || e == enow)) {
