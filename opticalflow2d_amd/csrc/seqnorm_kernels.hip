@@ -183,19 +183,6 @@ __device__ __forceinline__ unsigned cand_window(double lo, double hi) {
     return hdr_pack(elo, ehi - elo + 1);
 }
 
-// The magnitudes of term L: 0 past the grid
-__device__ __forceinline__ void sn_terms(const float2 *__restrict__ cur,
-                                         const float2 *__restrict__ prev, unsigned L, unsigned N,
-                                         unsigned i, unsigned j, int P, double &dd, double &dp) {
-    dd = dp = 0.0;
-    if (L < N) {
-        const size_t off = (size_t)j * (size_t)P + i;
-        const float2 c = cur[off], p = prev[off];
-        dd = sn_mag(c.x - p.x, c.y - p.y);  // Field::operator- (Field.tpp:305-334)
-        dp = sn_mag(p.x, p.y);
-    }
-}
-
 template <class T, class Op>
 __device__ __forceinline__ T wave_reduce(T v, Op op) {
 #pragma unroll
@@ -620,17 +607,32 @@ __device__ __forceinline__ unsigned long long lanes_from(int k) {
     return k >= 64 ? 0ull : (~0ull << k);
 }
 
-// The 64 terms of segment `seg` of tile `b` (lane = term) from the exact
+// The lane's term of segment `seg` of tile `b`: its cur and prev (0 past the
+// grid), loaded ahead of the raw segment that uses them
+struct SnSegTerms {
+    float2 c, p;
+};
+__device__ __forceinline__ SnSegTerms sn_seg_load(const float2 *__restrict__ cur,
+                                                  const float2 *__restrict__ prev, int which,
+                                                  unsigned b, int seg, unsigned N, int dimx,
+                                                  int P) {
+    const unsigned L = b * (unsigned)kSnTile + 64u * seg + (threadIdx.x & 63);
+    SnSegTerms t{make_float2(0.0f, 0.0f), make_float2(0.0f, 0.0f)};
+    if (L < N) {
+        const unsigned j = L / (unsigned)dimx, i = L - j * (unsigned)dimx;
+        const size_t off = (size_t)j * (size_t)P + i;
+        if (!which) t.c = cur[off];
+        t.p = prev[off];
+    }
+    return t;
+}
+
+// The 64 terms of a segment (lane = term, `tv` its cur / prev) from the exact
 // running sum S, term by term where the binade changes.
-__device__ float sn_raw_segment(const float2 *__restrict__ cur, const float2 *__restrict__ prev,
-                                int which, unsigned b, int seg, unsigned N, int dimx, int P,
-                                float S) {
+__device__ float sn_raw_segment(SnSegTerms tv, int which, float S) {
     const int lane = threadIdx.x & 63;
-    const unsigned L = b * (unsigned)kSnTile + 64u * seg + lane;
-    const unsigned j = L / (unsigned)dimx, i = L - j * (unsigned)dimx;
-    double d[2];
-    sn_terms(cur, prev, L, N, i, j, P, d[0], d[1]);
-    const double dv = which ? d[1] : d[0];
+    // Field::operator- (Field.tpp:305-334) for |cur - prev|
+    const double dv = which ? sn_mag(tv.p.x, tv.p.y) : sn_mag(tv.c.x - tv.p.x, tv.c.y - tv.p.y);
     int pos = 0;
     while (pos < 64) {
         const int e = sn_region(S);
@@ -732,6 +734,8 @@ __device__ float sn_resolve(const float2 *__restrict__ cur, const float2 *__rest
     int enow = kSnLow;  // the binade of gnow
     int rawhere = 0;
     int made_at = -kSnSegs;  // segment at which gnow was made
+    int pf_seg = -1;         // segment whose terms pf holds
+    SnSegTerms pf{};
     bool no_more = false;    // a made set of entries served < 16 segments: step raw
     unsigned gnow = 0;
     while (s0 < kSnSegs) {
@@ -773,7 +777,15 @@ __device__ float sn_resolve(const float2 *__restrict__ cur, const float2 *__rest
             if (!nz) return S;  // every remaining term is 0
             s0 = first_lane(nz);
         }
-        S = sn_raw_segment(cur, prev, which, b, s0, N, dimx, P, S);
+        // this segment's terms (prefetched when the last raw one was s0 - 1),
+        // and the next one's loads in flight behind its steps
+        const SnSegTerms tv =
+            pf_seg == s0 ? pf : sn_seg_load(cur, prev, which, b, s0, N, dimx, P);
+        if (s0 + 1 < kSnSegs) {
+            pf = sn_seg_load(cur, prev, which, b, s0 + 1, N, dimx, P);
+            pf_seg = s0 + 1;
+        }
+        S = sn_raw_segment(tv, which, S);
         raw++;
         rawhere++;
         s0++;
