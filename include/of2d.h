@@ -211,6 +211,15 @@ int of2d_slab_create_local(of2d_slab **out, int dimx, int dimy, float alpha, int
  * order) and those of the |cur - prev| walk's resolves. */
 int of2d_motion_norms(const float *cur, const float *prev, int dimx, int dimy, int npairs,
                       float *sums, int *stats);
+/* The Logger norms of a chain of iterates u[0 .. niter] (niter + 1 fields of
+ * dimx*dimy*2 floats): sums[2k], sums[2k + 1] are those of the update from
+ * u[k] to u[k + 1], as of2d_motion_norms gives them, computed the way the
+ * registration loop does: in batches of `batch` (1..3) consecutive updates
+ * whose pass reads each iterate once, alternating between two sets of
+ * workspaces.  stats as of2d_motion_norms, per update.  Not in the
+ * reference: a test entry for the batched device norms. */
+int of2d_motion_norms_chain(const float *u, int dimx, int dimy, int niter, int batch,
+                            float *sums, int *stats);
 
 /* ---- library info ---- */
 const char *of2d_version(void);

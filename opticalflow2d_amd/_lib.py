@@ -71,6 +71,7 @@ SIGNATURES = {
     "of2d_slab_create_local": (C.c_int, [C.POINTER(C.c_void_p), C.c_int, C.c_int, C.c_float,
                                          C.c_int, C.c_int, C.c_int, C.c_void_p]),
     "of2d_motion_norms": (C.c_int, [_f32p, _f32p, C.c_int, C.c_int, C.c_int, _f32p, _i32p]),
+    "of2d_motion_norms_chain": (C.c_int, [_f32p, C.c_int, C.c_int, C.c_int, C.c_int, _f32p, _i32p]),
     "of2d_version": (C.c_char_p, []),
     "of2d_device_count": (C.c_int, [C.POINTER(C.c_int)]),
 }

@@ -189,6 +189,54 @@ int of2d_motion_norms(const float *cur, const float *prev, int dimx, int dimy, i
     return rc;
 }
 
+int of2d_motion_norms_chain(const float *u, int dimx, int dimy, int niter, int batch,
+                            float *sums, int *stats) {
+    if (!u || !sums || dimx <= 0 || dimy <= 0 || niter <= 0 || batch < 1 || batch > 3)
+        return OF2D_ERR_INVALID_ARGUMENT;
+    std::string err;
+    int rc = guarded(err, [&] {
+        const size_t n = (size_t)dimx * dimy * 2;
+        std::vector<of2d::Field<float2>> f((size_t)niter + 1);
+        for (size_t k = 0; k <= (size_t)niter; k++) {
+            f[k].alloc(dimx, dimy);
+            const size_t row = (size_t)dimx * sizeof(float2), pitch = (size_t)f[k].P * sizeof(float2);
+            OF2D_HIP(hipMemcpy2D(f[k].p, pitch, u + k * n, row, row, dimy, hipMemcpyHostToDevice));
+        }
+        // two sets of three workspaces, as Registration::run_chunked_exact
+        of2d::DevArray<unsigned char> ws[6];
+        bool used[6] = {};
+        for (auto &w : ws) w.alloc(of2d::seqnorm_workspace_bytes(dimx, dimy));
+        of2d::DevArray<float> out;
+        out.alloc(2 * (size_t)niter);
+        constexpr int kSnDbg = 10;
+        of2d::DevArray<int> dbg;
+        dbg.alloc(kSnDbg * (size_t)niter);
+        for (int t = 0, g = 0; t < niter; g++) {
+            of2d::SeqnormBatch B;
+            B.K = std::min(batch, niter - t);
+            for (int i = 0; i <= B.K; i++) B.u[i] = f[(size_t)t + i].p;
+            for (int i = 0; i < B.K; i++) {
+                const int w = 3 * (g & 1) + i;
+                B.ws[i] = ws[w].p;
+                B.use_profile[i] = used[w];
+                used[w] = true;
+                B.out[i] = out.p + 2 * (size_t)(t + i);
+                B.dbg[i] = dbg.p + kSnDbg * (size_t)(t + i);
+            }
+            of2d::launch_seqnorm_pass(B, dimx, dimy, f[0].P, nullptr);
+            of2d::launch_seqnorm_refine(B, dimx, dimy, f[0].P, nullptr);
+            of2d::launch_seqnorm_walk(B, dimx, dimy, f[0].P, nullptr);
+            t += B.K;
+        }
+        OF2D_HIP(hipMemcpy(sums, out.p, 2 * sizeof(float) * niter, hipMemcpyDeviceToHost));
+        if (stats)
+            OF2D_HIP(hipMemcpy2D(stats, 8 * sizeof(int), dbg.p, kSnDbg * sizeof(int),
+                                 8 * sizeof(int), niter, hipMemcpyDeviceToHost));
+    });
+    if (rc != OF2D_OK) g_gateway_err = err;
+    return rc;
+}
+
 // ------------------------------------------------------------------ gateway
 // static ImageRegistration *myImageRegistration (WrapperOpticalFlow2d.cpp:13)
 static of2d_ctx *g_single = nullptr;

@@ -240,6 +240,23 @@ const double *seqnorm_total(int dimx, int dimy, int P, void *ws, hipStream_t st)
 void launch_seqnorm_offsets(const double *const *totals, int r, double *out, hipStream_t st);
 void launch_seqnorm_refine(const float2 *cur, const float2 *prev, int dimx, int dimy, int P,
                            void *ws, bool use_profile, const double *p_off, hipStream_t st);
+// A batch of K <= 3 consecutive Logger updates of one loop: pair i is
+// (prev, cur) = (u[i], u[i + 1]) on workspace ws[i] (its own profile), so the
+// pass reads the K + 1 iterates once (a Jacobi triple's four arrays for three
+// updates) and each of check, fix and walk is one launch for the batch.
+struct SeqnormBatch {
+    int K = 1;
+    const float2 *u[4] = {};
+    void *ws[3] = {};
+    bool use_profile[3] = {};
+    const double *p_off[3] = {};  // refine: a row slab's predecessors' fp64 sums
+    const float *s_in[3] = {};    // walk: a row slab's predecessors' exact sums
+    float *out[3] = {};           // walk: the sums of pair i (device float[2])
+    int *dbg[3] = {};             // walk: cost counters (int[10]), optional
+};
+void launch_seqnorm_pass(const SeqnormBatch &b, int dimx, int dimy, int P, hipStream_t st);
+void launch_seqnorm_refine(const SeqnormBatch &b, int dimx, int dimy, int P, hipStream_t st);
+void launch_seqnorm_walk(const SeqnormBatch &b, int dimx, int dimy, int P, hipStream_t st);
 
 // ---------------------------------------------------------------- fields
 void launch_d2f(const double *in, int dimx, int dimy, float *out, int P, int row_offset,

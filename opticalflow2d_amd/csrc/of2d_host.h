@@ -117,7 +117,7 @@ struct Level {
     Field<float2> motion[2];
     int mcur = 0;
     Field<float2> dI;
-    Field<float2> est[9];  // [3] .. [8]: only for the exact-norm loop's ring
+    Field<float2> est[14];  // [3] .. [13]: only for the exact-norm loop's ring
     Field<float2> force, velocity, increment, corr, tmp;
     DevArray<double> cbuf[2];              // Curvature: two x|y double plane pairs (pitch P)
     DevArray<double> cC1T, cC0, cD1T, cD0;  // Curvature: REDFT10 / REDFT01 matrices
@@ -191,18 +191,19 @@ class Registration {
     // enqueue the exact norms of one Logger update into d_seq_[2t], [2t + 1]
     // (synchronous loops: Elastic, Fluid; workspace 0, on st_)
     void seqnorm(const Level &L, const float2 *cur, const float2 *prev, int t);
-    // run_chunked with the reference's float norms: every iterate in memory
-    // (single steps into a ring of four buffers, or with step3m triples into a
-    // ring of eight); each iteration's tables on sn_st_ and walk on wk_st_,
-    // alternating between two workspaces
+    // run_chunked with the reference's float norms: every iterate in memory,
+    // groups of up to three iterations (a step3m triple or single steps) into
+    // a ring of twelve buffers; each group's norms as one batch, its tables on
+    // sn_st_ and its walk on wk_st_, workspace set g & 1 (three workspaces)
     int run_chunked_exact(Level &L, int niter, int nb, const StepFn &step, int &final_buf,
                           const StepFn3M &step3m = nullptr);
     hipStream_t sn_st_ = nullptr, wk_st_ = nullptr;
-    static constexpr int kExactEv = 16;  // event ring (> ring buffers + 3)
+    static constexpr int kExactEv = 16;  // event ring per group (> 4 groups in flight)
+    static constexpr int kSeqWs = 6;     // two sets of three
     hipEvent_t ev_step_[kExactEv] = {}, ev_fix_[kExactEv] = {}, ev_walk_[kExactEv] = {};
-    DevArray<unsigned char> d_seqws_[2];  // seqnorm workspaces (level 0 size)
-    DevArray<float> d_seq_;               // per-iteration exact sums of a chunk
-    int seq_dx_[2] = {0, 0}, seq_dy_[2] = {0, 0};  // grid of each workspace's last call
+    DevArray<unsigned char> d_seqws_[kSeqWs];  // seqnorm workspaces (level 0 size)
+    DevArray<float> d_seq_;                    // per-iteration exact sums of a chunk
+    int seq_dx_[kSeqWs] = {}, seq_dy_[kSeqWs] = {};  // grid of each workspace's last call
     int chunk_ = 33;  // eleven fused triples per chunk
     int gi_ = -1;     // triple kernel: dI from Iaux (1), from dI (0), by size (-1)
     int device_ = -1;

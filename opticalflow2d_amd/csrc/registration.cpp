@@ -323,19 +323,22 @@ void Registration::seqnorm(const Level &L, const float2 *cur, const float2 *prev
 }
 
 // The chunked loop of run_chunked with the reference's float norms.  Every
-// iterate must be in memory for its norms: single steps write a ring of the
-// four buffers other than the chunk's start buffer a (kept for a replay), or,
-// with step3m (HS), triples write all three of their iterates into a ring of
-// eight.  The norms of iteration t run behind its step on two streams: the
-// bandwidth passes (seqnorm tables, sn_st_) and the latency-bound walk
-// (wk_st_), on workspace t mod 2, whose last walk (t - 2) also predicts them
-// (its profile).  Iterate t's buffer is next written by iterate t + R (R the
-// ring size), after the walk of t + 1, its last reader.
+// iterate must be in memory for its norms, so the iterations run in groups of
+// up to three (a step3m triple that stores all three iterates, HS; or single
+// steps) into a ring of the R buffers other than the chunk's start buffer a
+// (kept for a replay).  The norms of a group run behind its steps as one
+// batch (seqnorm_kernels.hip: pair i = iterates t + i - 1, t + i): the
+// bandwidth passes (tables, check, fix) on sn_st_ and the latency-bound walk
+// on wk_st_, so group g's walk overlaps group g + 1's steps and tables.  Group
+// g works on workspace set g & 1, whose last walk (group g - 2) left the
+// profile that predicts it.  Iterate m's buffer is read by the walks of the
+// groups of m and m + 1; iterate m + R rewrites it after both.
 int Registration::run_chunked_exact(Level &L, int niter, int nb, const StepFn &step,
                                     int &final_buf, const StepFn3M &step3m) {
     const double npx = (double)L.dx * L.dy;
     last_err_.clear();
-    const int R = step3m ? 8 : 4;
+    constexpr int R = 12;
+    static_assert(R + 1 <= (int)(sizeof(L.est) / sizeof(L.est[0])), "ring");
     for (int b = 3; b <= R; b++)
         if (!L.est[b].p) L.est[b].alloc(L.dx, L.dy);
     auto ring = [&](int a, int t) {  // the (t mod R)-th buffer other than a
@@ -343,51 +346,59 @@ int Registration::run_chunked_exact(Level &L, int niter, int nb, const StepFn &s
         return i < a ? i : i + 1;
     };
     auto src_of = [&](int a, int t) { return t == 0 ? a : ring(a, t - 1); };
-    auto ev = [](hipEvent_t *e, int t) { return e[t % kExactEv]; };
+    auto ev = [](hipEvent_t *e, int g) { return e[g % kExactEv]; };
     // OF2D_SN_DEBUG: the walks' cost counters per iteration to stderr
     // (resolves, raw segments, listed tiles, walk clocks; tools/ diagnostics)
     static const bool sn_debug = std::getenv("OF2D_SN_DEBUG") != nullptr;
     constexpr int kDbg = 10;
     DevArray<int> dbg;
     if (sn_debug) dbg.alloc(kDbg * (size_t)chunk_);
-    // a new loop: its first two calls per workspace start from a fresh state
-    bool walked[2] = {false, false};
-    int a = 0, k0 = 0;
+    // a new loop: each workspace's first call starts from a fresh state
+    bool walked[kSeqWs] = {};
+    std::vector<int> group_of((size_t)chunk_);
+    int a = 0, k0 = 0, g = 0;
     while (k0 < niter) {
         const int C = std::min(chunk_, niter - k0);
-        for (int t = 0; t < C;) {
-            const int k = (step3m && C - t >= 3) ? 3 : 1;
-            // the buffers of iterates t .. t + k - 1 held iterates t - R ..,
-            // last read by the walks up to t + k - R (walks run in order)
-            if (t + k - R >= 0) OF2D_HIP(hipStreamWaitEvent(st_, ev(ev_walk_, t + k - R), 0));
-            if (k == 3)
+        for (int t = 0; t < C; g++) {
+            const int k = std::min(3, C - t);
+            for (int m = t; m < t + k; m++) group_of[m] = g;
+            // the buffers of iterates t .. t + k - 1 held iterates t - R ..
+            // t + k - 1 - R, last read by the walk of iterate t + k - R's group
+            if (t + k - R >= 0) OF2D_HIP(hipStreamWaitEvent(st_, ev(ev_walk_, group_of[t + k - R]), 0));
+            if (k == 3 && step3m) {
                 step3m(L.est[src_of(a, t)].p, L.est[ring(a, t)].p, L.est[ring(a, t + 1)].p,
                        L.est[ring(a, t + 2)].p);
-            else
-                step(L.est[src_of(a, t)].p, L.est[ring(a, t)].p, d_partial_ + (size_t)t * nb * 2);
-            OF2D_HIP(hipEventRecord(ev(ev_step_, t), st_));
-            for (int m = t; m < t + k; m++) {
-                const int src = src_of(a, m), dst = ring(a, m), w = (k0 + m) & 1;
-                if (m == t) OF2D_HIP(hipStreamWaitEvent(sn_st_, ev(ev_step_, t), 0));
-                // workspace w: the walk two iterations back has read it and left
-                // its profile (wk_st_ runs the walks in order)
-                if (m >= 2) OF2D_HIP(hipStreamWaitEvent(sn_st_, ev(ev_walk_, m - 2), 0));
-                const bool use_prof = walked[w] && seq_dx_[w] == L.dx && seq_dy_[w] == L.dy;
+            } else {
+                for (int m = t; m < t + k; m++)
+                    step(L.est[src_of(a, m)].p, L.est[ring(a, m)].p, d_partial_ + (size_t)m * nb * 2);
+            }
+            OF2D_HIP(hipEventRecord(ev(ev_step_, g), st_));
+            SeqnormBatch B;
+            B.K = k;
+            B.u[0] = L.est[src_of(a, t)].p;
+            for (int i = 0; i < k; i++) {
+                const int w = 3 * (g & 1) + i;
+                B.u[i + 1] = L.est[ring(a, t + i)].p;
+                B.ws[i] = d_seqws_[w].p;
+                B.use_profile[i] = walked[w] && seq_dx_[w] == L.dx && seq_dy_[w] == L.dy;
                 seq_dx_[w] = L.dx;
                 seq_dy_[w] = L.dy;
                 walked[w] = true;
-                launch_seqnorm_tables(L.est[dst].p, L.est[src].p, L.dx, L.dy, L.P,
-                                      d_seqws_[w].p, use_prof, sn_st_);
-                OF2D_HIP(hipEventRecord(ev(ev_fix_, m), sn_st_));
-                OF2D_HIP(hipStreamWaitEvent(wk_st_, ev(ev_fix_, m), 0));
-                launch_seqnorm_walk(L.est[dst].p, L.est[src].p, L.dx, L.dy, L.P, d_seqws_[w].p,
-                                    nullptr, d_seq_.p + 2 * (size_t)m,
-                                    sn_debug ? dbg.p + kDbg * (size_t)m : nullptr, wk_st_);
-                OF2D_HIP(hipEventRecord(ev(ev_walk_, m), wk_st_));
+                B.out[i] = d_seq_.p + 2 * (size_t)(t + i);
+                B.dbg[i] = sn_debug ? dbg.p + kDbg * (size_t)(t + i) : nullptr;
             }
+            OF2D_HIP(hipStreamWaitEvent(sn_st_, ev(ev_step_, g), 0));
+            // workspace set g & 1: group g - 2's walk has read it and left its profile
+            if (g >= 2) OF2D_HIP(hipStreamWaitEvent(sn_st_, ev(ev_walk_, g - 2), 0));
+            launch_seqnorm_pass(B, L.dx, L.dy, L.P, sn_st_);
+            launch_seqnorm_refine(B, L.dx, L.dy, L.P, sn_st_);
+            OF2D_HIP(hipEventRecord(ev(ev_fix_, g), sn_st_));
+            OF2D_HIP(hipStreamWaitEvent(wk_st_, ev(ev_fix_, g), 0));
+            launch_seqnorm_walk(B, L.dx, L.dy, L.P, wk_st_);
+            OF2D_HIP(hipEventRecord(ev(ev_walk_, g), wk_st_));
             t += k;
         }
-        OF2D_HIP(hipStreamWaitEvent(st_, ev(ev_walk_, C - 1), 0));
+        OF2D_HIP(hipStreamWaitEvent(st_, ev(ev_walk_, g - 1), 0));  // walks run in order
         OF2D_HIP(hipMemcpyAsync(hs_.flt, d_seq_.p, sizeof(float) * 2 * C, hipMemcpyDeviceToHost,
                                 st_));
         check_status();  // synchronises st_ (and with it every norm of the chunk)

@@ -56,7 +56,6 @@ namespace {
 
 constexpr int kSnThreads = 256;                 // table kernels: 4 waves
 constexpr int kSnSegs = kSnTile / 64;           // 64-term segments per tile
-constexpr int kSnRounds = kSnSegs / (kSnThreads / 64);
 constexpr int kSnCand = 4;                      // candidate binades per tile and norm
 // relative width of the profile's prediction window (tables): a tile takes the
 // binades of [P (1 - w), P' / (1 - w)]; the check's tighter window around the
@@ -82,6 +81,12 @@ __host__ __device__ constexpr unsigned hdr_pack(int elo, int nc) {
 }
 __device__ __forceinline__ int hdr_elo(unsigned h) { return (int)(h & 0xffffu) - 512; }
 __device__ __forceinline__ int hdr_nc(unsigned h) { return (int)((h >> 16) & 7u); }
+
+// the wave's lanes where p holds (HIP's __ballot takes an int: a select and a
+// compare more per call)
+__device__ __forceinline__ unsigned long long sn_ballot(bool p) {
+    return __builtin_amdgcn_ballot_w64(p);
+}
 
 // binade of the running sum (S >= 0 or NaN)
 __device__ __forceinline__ int sn_region(float S) {
@@ -165,6 +170,47 @@ __device__ __forceinline__ sn_fn sn_term_fn(double d, double scale, bool &nan) {
     return fn_make(m, m);
 }
 
+// The increments from an fp32 estimate of the magnitude (round 4).  m(d, e)
+// only depends on where t = d 2^(23-e) lies relative to the half-integers
+// (the double sum's grid 2^(e-52) moves t by at most 2^-30), and an estimate
+// decides it wherever it lies clear of them.  The estimate
+//   q = fma(x, x, y*y) (two roundings: rel. error <= 2^-23), v_sqrt_f32 (1 ulp)
+// is within 1.5 2^-23 of d relative wherever q is a normal float well inside
+// the range (q in [2^-100, 2^120]; exact zeros are exact), so with
+// r = rint(t_est): |t_est - r| < 1/2 - (t 2^-19 + 2^-28) (8x the bound) puts
+// the exactly rounded t strictly inside (r - 1/2, r + 1/2): m = r, no tie.
+// Every other term (near a half-integer, a large term t >= 2^13, tiny or huge
+// components, NaN) takes the exact fp64 sequence; a wave does so only when
+// one of its lanes needs it (a fraction of a percent of waves past the first
+// tiles), so the pass runs on fp32 arithmetic and one sqrt per term.
+struct SnEst {
+    float d;   // the estimate of sqrt((double)x^2 + (double)y^2)
+    bool ok;   // its error bound holds
+    bool nz;   // the magnitude is not exactly 0 (NaN included)
+};
+__device__ __forceinline__ SnEst sn_est(float x, float y) {
+    SnEst v;
+    const float q = __builtin_fmaf(x, x, y * y);  // >= 0 (+0 for zeros), or NaN / inf
+    v.nz = ((__float_as_uint(x) | __float_as_uint(y)) << 1) != 0u;
+    v.d = __builtin_amdgcn_sqrtf(q);  // branch-free: sqrt(0) = 0
+    // q in [2^-100, 2^120] on its bit pattern (NaN / inf / tiny fall outside)
+    const unsigned qb = __float_as_uint(q) - 0x0D800000u;
+    v.ok = qb <= 0x7B800000u - 0x0D800000u || !v.nz;
+    return v;
+}
+// 2^(23-e) as a float (e in [kSnEmin, 127])
+__device__ __forceinline__ float sn_scale32(int e) {
+    return __uint_as_float((unsigned)(23 - e + 127) << 23);
+}
+// m of the estimate in the binade of scale32; false where it does not decide
+__device__ __forceinline__ bool sn_incr_est(const SnEst &v, float scale32, unsigned &m) {
+    const float t = v.d * scale32;
+    const float r = rintf(t);
+    const float thr = __builtin_fmaf(t, -0x1p-19f, 0.5f - 0x1p-28f);
+    m = (unsigned)r;
+    return v.ok && t < 8192.0f && fabsf(t - r) < thr;
+}
+
 // binade of a double bound, clamped to the float range
 __device__ __forceinline__ int sn_region_d(double v) {
     if (!(v >= 0x1p-100)) return kSnLow;
@@ -229,21 +275,301 @@ __device__ __forceinline__ size_t g_index(unsigned b, int n, int c, int s) {
 }
 
 // ---------------------------------------------------------------- tables
-// Entries of one tile for the candidate binades of its two headers: the tile
-// entries T (ALL) and, for the norms whose header asks for them (SEG), the
-// 64 segment entries G.  FIRST (the pass over every tile) also writes the fp64
-// tile sums, the nonzero-segment masks and the headers: candidates from the
-// profile (use_prof), none without one.
-template <bool FIRST>
-__device__ void sn_tile_tables(const float2 *__restrict__ cur, const float2 *__restrict__ prev,
-                               unsigned N, int dimx, int P, unsigned nt, const SnWs &ws,
-                               unsigned b, unsigned h0, unsigned h1, int use_prof) {
-    const int w = threadIdx.x / 64, lane = threadIdx.x & 63;
-    unsigned h[2] = {h0, h1};
-    if (FIRST) {
+// A batch of K consecutive Logger updates of one loop (round 4): pair i reads
+// prev = u[i], cur = u[i + 1] and works on workspace ws[i], so the pass over
+// K pairs reads K + 1 iterates instead of 2K (the triple kernel's three
+// iterates: 4 arrays for 3 updates).  The check, fix and walk take the batch's
+// pairs by blockIdx.y / blockIdx.x.
+constexpr int kSnMaxJobs = 3;
+struct SnJobs {
+    const float2 *u[kSnMaxJobs + 1];
+    SnWs ws[kSnMaxJobs];
+    int use_prof[kSnMaxJobs];
+    const double *p_off[kSnMaxJobs];  // check: a row slab's predecessors' fp64 sums
+    const float *s_in[kSnMaxJobs];    // walk: a row slab's predecessors' exact sums
+    float *out[kSnMaxJobs];
+    int *dbg[kSnMaxJobs];
+};
+
+constexpr int kSnPf = 2;  // segments per load group (the next group's loads in flight)
+
+// The lane's terms of consecutive segments of one tile: iterates j0 .. j0 + K
+// at linear index L = row jj, column ii (the next segment's), 0 past the grid
+template <int K>
+struct SnLoader {
+    unsigned L, ii, jj;
+    __device__ __forceinline__ SnLoader(unsigned b, unsigned dimx) {
+        L = b * (unsigned)kSnTile + (threadIdx.x & 63);
+        jj = L / dimx;
+        ii = L - jj * dimx;
+    }
+    __device__ __forceinline__ void next(const SnJobs &J, int j0, unsigned N, unsigned dimx,
+                                         unsigned P, float2 (&v)[K + 1]) {
+#pragma unroll
+        for (int k = 0; k <= K; k++) v[k] = make_float2(0.0f, 0.0f);
+        if (L < N) {
+            const size_t off = (size_t)jj * (size_t)P + ii;
+#pragma unroll
+            for (int k = 0; k <= K; k++) v[k] = J.u[j0 + k][off];
+        }
+        L += 64u;
+        ii += 64u;
+        while (ii >= dimx) {
+            ii -= dimx;
+            jj++;
+        }
+    }
+};
+
+// The pass over tile b for pairs 0 .. K - 1 (one wave): per norm the fp64 tile
+// sum A (a prediction: fp32 lane sums of the estimates), the nonzero-segment
+// mask Z, the header (candidates from the profile, none without one) and, for
+// NC candidate binades (0, 1 or 2), the tile entries T.
+// Each lane adds its terms' increments (sn_incr_est: fp32 arithmetic, one
+// sqrt; the exact fp64 sequence in the waves where a lane's estimate does not
+// decide), so a tile entry is one saturating wave sum at the end.  Segment
+// entries come from the fix, for the tiles the check lists.
+template <int K, int NC>
+__device__ __forceinline__ void sn_wave_pass(const SnJobs &J, unsigned N, int dimx, int P,
+                                             unsigned nt, unsigned b, const unsigned (&hd)[K][2]) {
+    const int lane = threadIdx.x & 63;
+    int nc[K][2];
+    float sc32[K][2][kSnCand];
+#pragma unroll
+    for (int i = 0; i < K; i++)
+#pragma unroll
         for (int n = 0; n < 2; n++) {
-            h[n] = hdr_pack(0, 0);
-            if (use_prof) {
+            nc[i][n] = hdr_nc(hd[i][n]);
+            // a candidate the header does not have gets scale 0: its
+            // increments are 0 and decided, so every term computes all of them
+            // without a branch
+#pragma unroll
+            for (int c = 0; c < kSnCand; c++)
+                sc32[i][n][c] = c < nc[i][n] ? sn_scale32(hdr_elo(hd[i][n]) + c) : 0.0f;
+        }
+    constexpr int NCA = NC > 0 ? NC : 1;
+    unsigned tl[K][2][NCA];  // the lane's sum of increments per candidate (<= 64 2^25)
+    unsigned bl[K][2];       // the lane's tie / NaN candidates (bit c)
+    float fs[K][2];
+    bool zv[K][2];  // lane s: segment s has a nonzero magnitude
+#pragma unroll
+    for (int i = 0; i < K; i++)
+#pragma unroll
+        for (int n = 0; n < 2; n++) {
+            fs[i][n] = 0.0f;
+            zv[i][n] = false;
+            bl[i][n] = 0u;
+#pragma unroll
+            for (int c = 0; c < NCA; c++) tl[i][n][c] = 0u;
+        }
+    SnLoader<K> ld(b, (unsigned)dimx);
+    float2 cv[kSnPf][K + 1];
+#pragma unroll
+    for (int d = 0; d < kSnPf; d++) ld.next(J, 0, N, (unsigned)dimx, (unsigned)P, cv[d]);
+    for (int s0 = 0; s0 < kSnSegs; s0 += kSnPf) {
+        float2 nv[kSnPf][K + 1];
+        if (s0 + kSnPf < kSnSegs)
+#pragma unroll
+            for (int d = 0; d < kSnPf; d++) ld.next(J, 0, N, (unsigned)dimx, (unsigned)P, nv[d]);
+#pragma unroll
+        for (int d = 0; d < kSnPf; d++) {
+            const int s = s0 + d;
+#pragma unroll
+            for (int i = 0; i < K; i++) {
+#pragma unroll
+                for (int n = 0; n < 2; n++) {
+                    // Field::operator- (Field.tpp:305-334) for |cur - prev|
+                    const float x = n ? cv[d][i].x : cv[d][i + 1].x - cv[d][i].x;
+                    const float y = n ? cv[d][i].y : cv[d][i + 1].y - cv[d][i].y;
+                    const SnEst v = sn_est(x, y);
+                    const bool nz = sn_ballot(v.nz) != 0ull;
+                    zv[i][n] = lane == s ? nz : zv[i][n];
+                    unsigned m[NCA];
+                    bool unc = !v.ok;
+#pragma unroll
+                    for (int c = 0; c < NCA; c++) {
+                        m[c] = 0u;
+                        if (NC > 0) unc |= !sn_incr_est(v, sc32[i][n][c], m[c]);
+                    }
+                    float dv = v.d;
+                    if (sn_ballot(unc)) {
+                        // tiny / huge / non-finite components or an undecided
+                        // increment: the exact fp64 magnitude and sequence (the
+                        // same m where the estimate decided).  The empty asm
+                        // keeps the fp64 work inside this rare branch.
+                        float xx = x, yy = y;
+                        asm volatile("" : "+v"(xx), "+v"(yy));
+                        const double dd = sn_mag(xx, yy);
+                        dv = v.ok ? dv : (float)dd;
+                        const int e0 = hdr_elo(hd[i][n]);
+                        if (NC > 0)
+#pragma unroll
+                            for (int c = 0; c < NCA; c++) {
+                                bool bad = false;
+                                const double sc = c < nc[i][n] ? sn_scale(e0 + c) : 0.0;
+                                m[c] = sn_incr(dd, sc, bad);
+                                bl[i][n] |= bad ? 1u << c : 0u;
+                            }
+                    }
+                    fs[i][n] += dv;  // a prediction only (the check's prefix)
+                    if (NC > 0)
+#pragma unroll
+                        for (int c = 0; c < NCA; c++) tl[i][n][c] += m[c];
+                }
+            }
+        }
+#pragma unroll
+        for (int d = 0; d < kSnPf; d++)
+#pragma unroll
+            for (int k = 0; k <= K; k++) cv[d][k] = nv[d][k];
+    }
+    auto sat = [](unsigned p, unsigned x) {
+        return ((p | x) & kSnBad) | sn_sat(p & ~kSnBad, x & ~kSnBad);
+    };
+#pragma unroll
+    for (int i = 0; i < K; i++) {
+        const SnWs &ws = J.ws[i];
+#pragma unroll
+        for (int n = 0; n < 2; n++) {
+            unsigned hh = hd[i][n];
+            if (NC > 0) {
+                unsigned tv = 0u;
+                bool anybad = false;
+#pragma unroll
+                for (int c = 0; c < NCA; c++) {
+                    if (c >= nc[i][n]) continue;
+                    const bool bad = sn_ballot((bl[i][n] >> c) & 1u) != 0ull;
+                    const unsigned l = tl[i][n][c];
+                    const unsigned t =
+                        wave_reduce((l < kSnSat ? l : kSnSat), sat) | (bad ? kSnBad : 0u);
+                    if (lane == c) tv = t;
+                    anybad |= bad;
+                }
+                if (lane < nc[i][n]) ws.T[(2 * (size_t)b + n) * kSnCand + lane] = tv;
+                // a tie or NaN among the entries: the walk will want segment entries
+                if (anybad) hh |= kHdrSegReq;
+            }
+            const double a = wave_reduce((double)fs[i][n], [](double p, double x) { return p + x; });
+            const unsigned long long zm = sn_ballot(zv[i][n]);
+            if (zm == 0ull) hh = kHdrZero;  // every magnitude exactly 0
+            else if (a != a) hh = hdr_pack(0, 0) | kHdrNan;
+            if (lane == 0) {
+                ws.A[2 * (size_t)b + n] = a;
+                ws.Z[2 * (size_t)b + n] = zm;
+                ws.H[2 * (size_t)b + n] = hh;
+            }
+        }
+    }
+}
+
+// The fix's entries of one listed tile of pair j (one wave): for each norm
+// whose header is pending (new candidates) or asks for segment entries, the 64
+// segment entries G of every candidate (one DPP sum per segment; lane s holds
+// segment s's until the stores) and the tile entries T, their saturating sum.
+__device__ __forceinline__ void sn_wave_fix(const SnJobs &J, int j, unsigned N, int dimx, int P,
+                                            unsigned b) {
+    const int lane = threadIdx.x & 63;
+    const SnWs &ws = J.ws[j];
+    unsigned hd[2];
+    int nc[2], elo[2];
+#pragma unroll
+    for (int n = 0; n < 2; n++) {
+        hd[n] = ws.H[2 * (size_t)b + n];
+        nc[n] = (hd[n] & (kHdrPending | kHdrSegReq)) ? hdr_nc(hd[n]) : 0;
+        elo[n] = hdr_elo(hd[n]);
+    }
+    unsigned gv[2][kSnCand];
+#pragma unroll
+    for (int n = 0; n < 2; n++)
+#pragma unroll
+        for (int c = 0; c < kSnCand; c++) gv[n][c] = 0u;
+    SnLoader<1> ld(b, (unsigned)dimx);
+    float2 cv[kSnPf][2];
+#pragma unroll
+    for (int d = 0; d < kSnPf; d++) ld.next(J, j, N, (unsigned)dimx, (unsigned)P, cv[d]);
+    for (int s0 = 0; s0 < kSnSegs; s0 += kSnPf) {
+        float2 nv[kSnPf][2];
+        if (s0 + kSnPf < kSnSegs)
+#pragma unroll
+            for (int d = 0; d < kSnPf; d++) ld.next(J, j, N, (unsigned)dimx, (unsigned)P, nv[d]);
+#pragma unroll
+        for (int d = 0; d < kSnPf; d++) {
+            const int s = s0 + d;
+#pragma unroll
+            for (int n = 0; n < 2; n++) {
+                if (nc[n] == 0) continue;
+                // Field::operator- (Field.tpp:305-334) for |cur - prev|
+                const float x = n ? cv[d][0].x : cv[d][1].x - cv[d][0].x;
+                const float y = n ? cv[d][0].y : cv[d][1].y - cv[d][0].y;
+                const SnEst v = sn_est(x, y);
+                unsigned m[kSnCand];
+                bool bad[kSnCand], unc = false;
+#pragma unroll
+                for (int c = 0; c < kSnCand; c++) {
+                    m[c] = 0u;
+                    bad[c] = false;
+                    if (c < nc[n]) unc |= !sn_incr_est(v, sn_scale32(elo[n] + c), m[c]);
+                }
+                if (sn_ballot(unc)) {
+                    const double dd = sn_mag(x, y);
+#pragma unroll
+                    for (int c = 0; c < kSnCand; c++)
+                        if (c < nc[n]) m[c] = sn_incr(dd, sn_scale(elo[n] + c), bad[c]);
+                }
+#pragma unroll
+                for (int c = 0; c < kSnCand; c++) {
+                    if (c >= nc[n]) continue;
+                    const unsigned t = wave_sum(m[c]);  // <= 64 2^25
+                    const bool tb = sn_ballot(bad[c]) != 0ull;
+                    const unsigned e = (t < kSnSat ? t : kSnSat) | (tb ? kSnBad : 0u);
+                    gv[n][c] = lane == s ? e : gv[n][c];
+                }
+            }
+        }
+#pragma unroll
+        for (int d = 0; d < kSnPf; d++)
+#pragma unroll
+            for (int k = 0; k < 2; k++) cv[d][k] = nv[d][k];
+    }
+#pragma unroll
+    for (int n = 0; n < 2; n++) {
+        if (nc[n] == 0) continue;
+        unsigned tv = 0u;
+#pragma unroll
+        for (int c = 0; c < kSnCand; c++) {
+            if (c >= nc[n]) continue;
+            ws.G[g_index(b, n, c, lane)] = gv[n][c];
+            const unsigned t = wave_reduce(gv[n][c], [](unsigned p, unsigned x) {
+                return ((p | x) & kSnBad) | sn_sat(p & ~kSnBad, x & ~kSnBad);
+            });
+            if (lane == c) tv = t;
+        }
+        if (lane < nc[n]) ws.T[(2 * (size_t)b + n) * kSnCand + lane] = tv;
+        if (lane == 0) ws.H[2 * (size_t)b + n] = (hd[n] & ~(kHdrPending | kHdrSegReq)) | kHdrSeg;
+    }
+}
+
+// the pass over every tile: one wave per tile, K pairs; the candidate count
+// picks the form (none: no profile; one or two: the usual); tiles where the
+// profile's window spans more binades (the first ones) are left to the fix
+template <int K>
+__global__ __launch_bounds__(kSnThreads) void seqnorm_tables(unsigned N, int dimx, int P,
+                                                            unsigned nt, SnJobs J) {
+    if (blockIdx.x == 0 && threadIdx.x < 4)
+#pragma unroll
+        for (int i = 0; i < K; i++) J.ws[i].cnt[threadIdx.x] = 0;  // seqnorm_check's list
+    const unsigned b = (unsigned)__builtin_amdgcn_readfirstlane(
+        (int)(blockIdx.x * (kSnThreads / 64) + threadIdx.x / 64));
+    if (b >= nt) return;
+    unsigned hd[K][2];
+    int ncmax = 0;
+#pragma unroll
+    for (int i = 0; i < K; i++) {
+        const SnWs &ws = J.ws[i];
+#pragma unroll
+        for (int n = 0; n < 2; n++) {
+            unsigned h = hdr_pack(0, 0);
+            if (J.use_prof[i]) {
                 // the last call's running sums scaled by the trend of its
                 // totals (|cur - prev| shrinks from update to update)
                 const int src = prof_src(ws, n);
@@ -251,135 +577,26 @@ __device__ void sn_tile_tables(const float2 *__restrict__ cur, const float2 *__r
                 const float t0 = ws.tot[2 * src], t1 = ws.tot[2 * src + 1];
                 double r = (src == n && t1 > 0.0f && t0 > 0.0f) ? (double)t0 / t1 : 1.0;
                 r = r < 0.25 ? 0.25 : (r > 4.0 ? 4.0 : r);
-                h[n] = cand_window((double)pr[b] * r * (1.0 - kSnWin),
-                                   (double)pr[b + 1] * r / (1.0 - kSnWin));
+                h = cand_window((double)pr[b] * r * (1.0 - kSnWin),
+                                (double)pr[b + 1] * r / (1.0 - kSnWin));
             }
+            hd[i][n] = (unsigned)__builtin_amdgcn_readfirstlane((int)h);  // uniform
+            ncmax = max(ncmax, hdr_nc(hd[i][n]));
         }
     }
-    int nc[2];
-    bool tab[2], seg[2];
-    double scale[2][kSnCand];
-    for (int n = 0; n < 2; n++) {
-        tab[n] = FIRST || (h[n] & kHdrPending);
-        seg[n] = !FIRST && (h[n] & kHdrSegReq);
-        nc[n] = (tab[n] || seg[n]) ? hdr_nc(h[n]) : 0;
+    if (ncmax > 2) {
+        // more candidates than the pass's fixed form: the fix makes this
+        // tile's entries (rare: tiles where the sum still climbs binades)
 #pragma unroll
-        for (int c = 0; c < kSnCand; c++)
-            scale[n][c] = sn_scale(c < nc[n] ? hdr_elo(h[n]) + c : 0);
+        for (int i = 0; i < K; i++)
+#pragma unroll
+            for (int n = 0; n < 2; n++)
+                if (hdr_nc(hd[i][n])) hd[i][n] |= kHdrPending;
+        ncmax = 0;
     }
-    unsigned tacc[2][kSnCand] = {};
-    bool tbad[2][kSnCand] = {};
-    double fs[2] = {0.0, 0.0};
-    unsigned long long zm[2] = {0ull, 0ull};
-    // segment s = kSnThreads/64 * r + w: 64 consecutive terms per wave and
-    // round; every round's loads are issued before the first is used
-    float2 cv[kSnRounds], pv[kSnRounds];
-    {
-        unsigned L = b * (unsigned)kSnTile + 64u * w + lane;
-        unsigned j = L / (unsigned)dimx, i = L - j * (unsigned)dimx;
-#pragma unroll
-        for (int r = 0; r < kSnRounds; r++) {
-            cv[r] = pv[r] = make_float2(0.0f, 0.0f);
-            if (L < N) {
-                const size_t off = (size_t)j * (size_t)P + i;
-                cv[r] = cur[off];
-                pv[r] = prev[off];
-            }
-            L += kSnThreads;
-            i += kSnThreads;
-            while (i >= (unsigned)dimx) {
-                i -= (unsigned)dimx;
-                j++;
-            }
-        }
-    }
-#pragma unroll
-    for (int r = 0; r < kSnRounds; r++) {
-        const int s = (kSnThreads / 64) * r + w;
-        double d[2];
-        d[0] = sn_mag(cv[r].x - pv[r].x, cv[r].y - pv[r].y);  // Field::operator- (Field.tpp:305-334)
-        d[1] = sn_mag(pv[r].x, pv[r].y);
-#pragma unroll
-        for (int n = 0; n < 2; n++) {
-            if (FIRST) {
-                fs[n] += d[n];
-                if (__ballot(d[n] != 0.0)) zm[n] |= 1ull << s;
-            }
-#pragma unroll
-            for (int c = 0; c < kSnCand; c++) {
-                if (c >= nc[n]) continue;
-                bool bad = false;
-                const unsigned m = sn_incr(d[n], scale[n][c], bad);  // <= 2^25
-                tacc[n][c] = sn_sat(tacc[n][c], m);
-                tbad[n][c] |= bad;
-                if (seg[n]) {  // 64 of them fit in 32 bits
-                    const unsigned t = wave_sum(m);
-                    const unsigned e = (t < kSnSat ? t : kSnSat) | (__ballot(bad) ? kSnBad : 0u);
-                    if (lane == 0) ws.G[g_index(b, n, c, s)] = e;
-                }
-            }
-        }
-    }
-    __shared__ unsigned st[2][kSnCand][kSnThreads / 64];
-    __shared__ double sf[2][kSnThreads / 64];
-    __shared__ unsigned long long sz[2][kSnThreads / 64];
-    auto sat = [](unsigned a, unsigned x) {
-        return ((a | x) & kSnBad) | sn_sat(a & ~kSnBad, x & ~kSnBad);
-    };
-    for (int n = 0; n < 2; n++) {
-#pragma unroll
-        for (int c = 0; c < kSnCand; c++) {
-            if (c >= nc[n]) continue;
-            const unsigned t = wave_reduce(tacc[n][c] | (tbad[n][c] ? kSnBad : 0u), sat);
-            if (lane == 0) st[n][c][w] = t;
-        }
-        if (FIRST) {
-            const double f = wave_reduce(fs[n], [](double a, double x) { return a + x; });
-            if (lane == 0) {
-                sf[n][w] = f;
-                sz[n][w] = zm[n];
-            }
-        }
-    }
-    __syncthreads();
-    if (threadIdx.x < 2) {
-        const int n = threadIdx.x;
-        if (tab[n])
-            for (int c = 0; c < nc[n]; c++) {
-                unsigned t = st[n][c][0];
-                for (int k = 1; k < kSnThreads / 64; k++) t = sat(t, st[n][c][k]);
-                ws.T[(2 * (size_t)b + n) * kSnCand + c] = t;
-            }
-        unsigned hh = h[n] & ~(kHdrPending | kHdrSegReq);
-        if (seg[n]) hh |= kHdrSeg;
-        if (FIRST)  // a tie or NaN among the entries: the walk will want segment entries
-            for (int c = 0; c < nc[n]; c++)
-                if (st[n][c][0] & kSnBad || st[n][c][1] & kSnBad || st[n][c][2] & kSnBad ||
-                    st[n][c][3] & kSnBad)
-                    hh |= kHdrSegReq;
-        if (FIRST) {
-            double a = 0.0;
-            unsigned long long z = 0;
-            for (int k = 0; k < kSnThreads / 64; k++) {
-                a += sf[n][k];
-                z |= sz[n][k];
-            }
-            ws.A[2 * (size_t)b + n] = a;
-            ws.Z[2 * (size_t)b + n] = z;
-            if (a == 0.0) hh = kHdrZero;
-            else if (a != a) hh = hdr_pack(0, 0) | kHdrNan;
-        }
-        ws.H[2 * (size_t)b + n] = hh;
-    }
-    __syncthreads();  // st / sf / sz are reused by the next tile of the block
-}
-
-__global__ __launch_bounds__(kSnThreads) void seqnorm_tables(const float2 *__restrict__ cur,
-                                                            const float2 *__restrict__ prev,
-                                                            unsigned N, int dimx, int P,
-                                                            unsigned nt, SnWs ws, int use_prof) {
-    if (blockIdx.x == 0 && threadIdx.x < 4) ws.cnt[threadIdx.x] = 0;  // seqnorm_check's list
-    sn_tile_tables<true>(cur, prev, N, dimx, P, nt, ws, blockIdx.x, 0, 0, use_prof);
+    if (ncmax == 0) sn_wave_pass<K, 0>(J, N, dimx, P, nt, b, hd);
+    else if (ncmax == 1) sn_wave_pass<K, 1>(J, N, dimx, P, nt, b, hd);
+    else sn_wave_pass<K, 2>(J, N, dimx, P, nt, b, hd);
 }
 
 // fp64 prefix of the tile sums (a prediction: any order) -> the binades the
@@ -399,7 +616,9 @@ __device__ __forceinline__ double sn_drift(const SnWs &ws, unsigned nt, int src,
     const double f = ws.prof[(size_t)src * (nt + 1) + b], q = ws.Pp[(size_t)src * (nt + 1) + b];
     return (q > 0.0 && f > 0.0 && f < INFINITY) ? f / q : 1.0;
 }
-__global__ __launch_bounds__(kSnChk) void seqnorm_check_sums(unsigned nt, SnWs ws, int use_prof) {
+__global__ __launch_bounds__(kSnChk) void seqnorm_check_sums(unsigned nt, SnJobs J) {
+    const SnWs &ws = J.ws[blockIdx.y];
+    const int use_prof = J.use_prof[blockIdx.y];
     const unsigned b = blockIdx.x * kSnChk + threadIdx.x;
     __shared__ double sh[2][kSnChk / 64];
     for (int n = 0; n < 2; n++) {
@@ -420,8 +639,9 @@ __global__ __launch_bounds__(kSnChk) void seqnorm_check_sums(unsigned nt, SnWs w
 // exclusive scan of the nb block sums (in place) plus p_off (a row slab's
 // predecessors: the prediction is of the global running sum); Pp[nt] <- the
 // total
-__global__ __launch_bounds__(kSnScan) void seqnorm_check_scan(unsigned nt, unsigned nb, SnWs ws,
-                                                              const double *__restrict__ p_off) {
+__global__ __launch_bounds__(kSnScan) void seqnorm_check_scan(unsigned nt, unsigned nb, SnJobs J) {
+    const SnWs &ws = J.ws[blockIdx.y];
+    const double *p_off = J.p_off[blockIdx.y];
     const unsigned chunk = (nb + kSnScan - 1) / kSnScan;
     const unsigned k0 = min(nb, threadIdx.x * chunk), k1 = min(nb, k0 + chunk);
     __shared__ double sh[2][kSnScan];
@@ -460,18 +680,22 @@ __global__ __launch_bounds__(kSnScan) void seqnorm_check_scan(unsigned nt, unsig
         // and while they predicted it: a walk that stepped many raw segments
         // (binades its tiles' candidates missed) leaves a profile whose drift
         // has moved on, and the next call on the workspace takes the wide window
+        // (2: totals within 1.25x, the drift +-1/64; 1: within 2.5x, as the
+        // loop's workspace sets see sums six updates apart early in a loop,
+        // +-1/32; 0: not usable)
         for (int n = 0; n < 2; n++) {
             const int src = prof_src(ws, n);
             const double old = ws.Pp[(size_t)src * (nt + 1) + nt];
-            ws.cnt[1 + n] = (old > 0.0 && total[n] > 0.0 && total[n] < 1.25 * old &&
-                             total[n] > 0.8 * old && ws.miss[src] <= kSnMissMax)
-                                ? 1u
-                                : 0u;
+            const double q = old > 0.0 ? total[n] / old : 0.0;
+            const bool ok = total[n] > 0.0 && ws.miss[src] <= kSnMissMax;
+            ws.cnt[1 + n] = !ok ? 0u : (q < 1.25 && q > 0.8) ? 2u : (q < 2.5 && q > 0.4) ? 1u : 0u;
         }
         for (int n = 0; n < 2; n++) ws.Pp[(size_t)n * (nt + 1) + nt] = total[n];
     }
 }
-__global__ __launch_bounds__(kSnChk) void seqnorm_check(unsigned nt, SnWs ws, int use_prof) {
+__global__ __launch_bounds__(kSnChk) void seqnorm_check(unsigned nt, SnJobs J) {
+    const SnWs &ws = J.ws[blockIdx.y];
+    const int use_prof = J.use_prof[blockIdx.y];
     const unsigned b = blockIdx.x * kSnChk + threadIdx.x;
     const bool active = b < nt;
     const int lane = threadIdx.x & 63, w = threadIdx.x / 64;
@@ -509,11 +733,11 @@ __global__ __launch_bounds__(kSnChk) void seqnorm_check(unsigned nt, SnWs ws, in
             // factor 16 (the kSnCand binades below 1/16 above it: past 2^24
             // terms most small terms vanish below half an ulp and the float
             // sum falls well behind; a miss costs the walk term-level steps)
-            const bool prof = use_prof && ws.cnt[1 + n] != 0;
+            const unsigned pq = use_prof ? ws.cnt[1 + n] : 0u;
+            const double wd = pq == 2 ? 1.0 / 64 : 1.0 / 32;
             const unsigned want =
-                prof ? cand_window(Pb[n] * d0[n] * (1.0 - 1.0 / 64),
-                                   (Pb[n] + a[n]) * d1[n] * (1.0 + 1.0 / 64))
-                     : cand_window(Pb[n] * (1.0 / 16), (Pb[n] + a[n]) * (1.0 + 1.0 / 16));
+                pq ? cand_window(Pb[n] * d0[n] * (1.0 - wd), (Pb[n] + a[n]) * d1[n] * (1.0 + wd))
+                   : cand_window(Pb[n] * (1.0 / 16), (Pb[n] + a[n]) * (1.0 + 1.0 / 16));
             const int wl = hdr_elo(want), wn = hdr_nc(want), hl = hdr_elo(h[n]), hn = hdr_nc(h[n]);
             unsigned hh = h[n];
             if (wn > 0 && (wl < hl || wl + wn > hl + hn)) hh = want | kHdrPending;
@@ -553,16 +777,17 @@ __global__ void seqnorm_offsets(RankTotals t, int r, double *__restrict__ out) {
     }
 }
 
-// the listed tiles: new tile entries and / or segment entries
-__global__ __launch_bounds__(kSnThreads) void seqnorm_fix(const float2 *__restrict__ cur,
-                                                         const float2 *__restrict__ prev,
-                                                         unsigned N, int dimx, int P,
-                                                         unsigned nt, SnWs ws) {
-    const unsigned cnt = ws.cnt[0];
-    for (unsigned k = blockIdx.x; k < cnt; k += gridDim.x) {
-        const unsigned b = ws.list[k];
-        sn_tile_tables<false>(cur, prev, N, dimx, P, nt, ws, b, ws.H[2 * (size_t)b],
-                              ws.H[2 * (size_t)b + 1], 0);
+// the listed tiles of pair blockIdx.y: new tile and segment entries, one wave
+// per tile
+__global__ __launch_bounds__(kSnThreads) void seqnorm_fix(unsigned N, int dimx, int P,
+                                                         unsigned nt, SnJobs J) {
+    const int j = blockIdx.y;
+    const unsigned cnt = J.ws[j].cnt[0];
+    const unsigned w = (unsigned)__builtin_amdgcn_readfirstlane((int)(threadIdx.x / 64));
+    for (unsigned k = blockIdx.x * (kSnThreads / 64) + w; k < cnt;
+         k += gridDim.x * (kSnThreads / 64)) {
+        const unsigned b = (unsigned)__builtin_amdgcn_readfirstlane((int)J.ws[j].list[k]);
+        sn_wave_fix(J, j, N, dimx, P, b);
     }
 }
 
@@ -638,7 +863,7 @@ __device__ float sn_raw_segment(SnSegTerms tv, int which, float S) {
         const int e = sn_region(S);
         if (e == kSnNonfinite) {
             // inf stays inf unless a NaN follows; NaN stays NaN
-            if (__ballot(lane >= pos && dv != dv)) S = __uint_as_float(0x7fc00000u);
+            if (sn_ballot(lane >= pos && dv != dv)) S = __uint_as_float(0x7fc00000u);
             return S;
         }
         const bool low = (e == kSnLow);
@@ -655,7 +880,7 @@ __device__ float sn_raw_segment(SnSegTerms tv, int which, float S) {
         const sn_fn excl = lane_below(incl);
         const unsigned R = fn_apply(excl, M);
         const bool fail = lane >= pos && (bad || fn_apply(f, R) > kSnLimit);
-        const unsigned long long fm = __ballot(fail);
+        const unsigned long long fm = sn_ballot(fail);
         if (!fm) {
             if (!low) S = sn_make(e, fn_apply(fn_make(lane_at(fn_e(incl), 63), lane_at(fn_o(incl), 63)), M));
             return S;
@@ -681,6 +906,7 @@ __device__ unsigned sn_segments_now(const float2 *__restrict__ cur, const float2
                                     int P) {
     const int lane = threadIdx.x & 63;
     const double scale = sn_scale(e);
+    const float scale32 = sn_scale32(e);
     unsigned mine = 0;
     const int sb = sfrom & ~7;
     unsigned L = b * (unsigned)kSnTile + 64u * sb + lane;
@@ -706,11 +932,14 @@ __device__ unsigned sn_segments_now(const float2 *__restrict__ cur, const float2
         for (int k = 0; k < kSnNowBatch; k++) {
             if (s0 + k >= kSnSegs) break;
             // Field::operator- (Field.tpp:305-334) for |cur - prev|
-            const double d = which ? sn_mag(pv[k].x, pv[k].y)
-                                   : sn_mag(cv[k].x - pv[k].x, cv[k].y - pv[k].y);
+            const float vx = which ? pv[k].x : cv[k].x - pv[k].x;
+            const float vy = which ? pv[k].y : cv[k].y - pv[k].y;
             bool bad = false;
-            const unsigned t = wave_sum(sn_incr(d, scale, bad));
-            const unsigned g = (t < kSnSat ? t : kSnSat) | (__ballot(bad) ? kSnBad : 0u);
+            unsigned m;
+            const bool unc = !sn_incr_est(sn_est(vx, vy), scale32, m);
+            if (sn_ballot(unc) && unc) m = sn_incr(sn_mag(vx, vy), scale, bad);
+            const unsigned t = wave_sum(m);
+            const unsigned g = (t < kSnSat ? t : kSnSat) | (sn_ballot(bad) ? kSnBad : 0u);
             if (lane == s0 + k) mine = g;
         }
     }
@@ -767,7 +996,7 @@ __device__ float sn_resolve(const float2 *__restrict__ cur, const float2 *__rest
             const unsigned incl = wave_incl_sat(v);
             const unsigned excl = lane_below(incl);
             const bool fail = lane >= s0 && ((gc & kSnBad) || M + incl > kSnLimit);
-            const unsigned long long fm = __ballot(fail);
+            const unsigned long long fm = sn_ballot(fail);
             if (!fm) return sn_make(e, M + lane_at(incl, 63));
             const int q = first_lane(fm);
             S = sn_make(e, M + lane_at(excl, q));  // exact: below the limit
@@ -795,19 +1024,22 @@ __device__ float sn_resolve(const float2 *__restrict__ cur, const float2 *__rest
 
 constexpr int kSnAhead = 8;  // windows loaded per step: the next step's loads hide behind them
 
-// One wave per norm walks the tiles in windows of 64 (lane = tile): the
+// One wave per norm and pair walks the tiles in windows of 64 (lane = tile): the
 // saturating scan of the entries for S's binade, a resolve at each tile whose
 // entry does not apply.  Writes every tile's start sum into the profile.
 // dbg: resolves (per norm), raw segments (per norm), listed tiles, walk and
 // resolve clocks, tiles given the walk's own segment entries (per norm).
-__global__ __launch_bounds__(64) void seqnorm_walk(const float2 *__restrict__ cur,
-                                                   const float2 *__restrict__ prev, unsigned N,
-                                                   int dimx, int P, unsigned nt, SnWs ws,
-                                                   const float *__restrict__ s_in,
-                                                   float *__restrict__ out,
-                                                   int *__restrict__ dbg) {
-    const int n = blockIdx.x;  // 0: |cur - prev|, 1: |prev|
+__global__ __launch_bounds__(64) void seqnorm_walk(unsigned N, int dimx, int P, unsigned nt,
+                                                   SnJobs J) {
+    const int job = blockIdx.x >> 1;
+    const int n = blockIdx.x & 1;  // 0: |cur - prev|, 1: |prev|
     const int lane = threadIdx.x;
+    const float2 *__restrict__ prev = J.u[job];
+    const float2 *__restrict__ cur = J.u[job + 1];
+    const SnWs &ws = J.ws[job];
+    const float *__restrict__ s_in = J.s_in[job];
+    float *__restrict__ out = J.out[job];
+    int *__restrict__ dbg = J.dbg[job];
     float *prof = ws.prof + (size_t)n * (nt + 1);
     __shared__ unsigned lh[kSnAhead][64], lt[kSnAhead][kSnCand][64];
     unsigned hn[kSnAhead], tn[kSnAhead][kSnCand];
@@ -851,7 +1083,7 @@ __global__ __launch_bounds__(64) void seqnorm_walk(const float2 *__restrict__ cu
                 const int e = sn_region(S);
                 if (e == kSnNonfinite) {
                     if (lane >= start && t < nt) prof[t] = S;
-                    nan |= __ballot(lane >= start && (h & kHdrNan)) != 0ull;
+                    nan |= sn_ballot(lane >= start && (h & kHdrNan)) != 0ull;
                     break;
                 }
                 const bool low = (e == kSnLow);
@@ -871,7 +1103,7 @@ __global__ __launch_bounds__(64) void seqnorm_walk(const float2 *__restrict__ cu
                 const unsigned incl = wave_incl_sat(v);
                 const unsigned excl = lane_below(incl);
                 fail = fail || (lane >= start && M + incl > kSnLimit);
-                const unsigned long long fm = __ballot(fail);
+                const unsigned long long fm = sn_ballot(fail);
                 const int q = fm ? first_lane(fm) : 64;
                 // tile start sums of the lanes up to the first failing one: exact
                 if (lane >= start && lane <= q && t < nt)
@@ -950,13 +1182,56 @@ unsigned check_geometry(int dimx, int dimy, int P) {
 }
 }  // namespace
 
-void launch_seqnorm_pass(const float2 *cur, const float2 *prev, int dimx, int dimy, int P,
-                         void *ws, bool use_profile, hipStream_t st) {
+namespace {
+SnJobs jobs_of(const SeqnormBatch &B, unsigned nt) {
+    if (B.K < 1 || B.K > kSnMaxJobs) throw std::invalid_argument("launch_seqnorm: batch size");
+    SnJobs J{};
+    for (int i = 0; i <= B.K; i++) J.u[i] = B.u[i];
+    for (int i = 0; i < B.K; i++) {
+        J.ws[i] = carve(B.ws[i], nt);
+        J.use_prof[i] = B.use_profile[i] ? 1 : 0;
+        J.p_off[i] = B.p_off[i];
+        J.s_in[i] = B.s_in[i];
+        J.out[i] = B.out[i];
+        J.dbg[i] = B.dbg[i];
+    }
+    return J;
+}
+}  // namespace
+
+void launch_seqnorm_pass(const SeqnormBatch &B, int dimx, int dimy, int P, hipStream_t st) {
     const unsigned nt = check_geometry(dimx, dimy, P);
     const unsigned N = (unsigned)((size_t)dimx * dimy);
-    const SnWs w = carve(ws, nt);
-    hipLaunchKernelGGL(seqnorm_tables, dim3(nt), dim3(kSnThreads), 0, st, cur, prev, N, dimx, P,
-                       nt, w, use_profile ? 1 : 0);
+    const SnJobs J = jobs_of(B, nt);
+    const dim3 grid((nt + kSnThreads / 64 - 1) / (kSnThreads / 64));
+    switch (B.K) {
+        case 1: hipLaunchKernelGGL(seqnorm_tables<1>, grid, dim3(kSnThreads), 0, st, N, dimx, P, nt, J); break;
+        case 2: hipLaunchKernelGGL(seqnorm_tables<2>, grid, dim3(kSnThreads), 0, st, N, dimx, P, nt, J); break;
+        default: hipLaunchKernelGGL(seqnorm_tables<3>, grid, dim3(kSnThreads), 0, st, N, dimx, P, nt, J); break;
+    }
+    OF2D_HIP(hipGetLastError());
+}
+
+void launch_seqnorm_refine(const SeqnormBatch &B, int dimx, int dimy, int P, hipStream_t st) {
+    const unsigned nt = check_geometry(dimx, dimy, P);
+    const unsigned N = (unsigned)((size_t)dimx * dimy);
+    const SnJobs J = jobs_of(B, nt);
+    const unsigned nb = (nt + 1 + kSnChk - 1) / kSnChk;  // blocks over tiles 0 .. nt
+    hipLaunchKernelGGL(seqnorm_check_sums, dim3(nb, B.K), dim3(kSnChk), 0, st, nt, J);
+    hipLaunchKernelGGL(seqnorm_check_scan, dim3(1, B.K), dim3(kSnScan), 0, st, nt, nb, J);
+    hipLaunchKernelGGL(seqnorm_check, dim3(nb, B.K), dim3(kSnChk), 0, st, nt, J);
+    OF2D_HIP(hipGetLastError());
+    // one wave per listed tile: up to 1024 waves per pair
+    const unsigned fb = std::min((nt + kSnThreads / 64 - 1) / (kSnThreads / 64), 256u);
+    hipLaunchKernelGGL(seqnorm_fix, dim3(fb, B.K), dim3(kSnThreads), 0, st, N, dimx, P, nt, J);
+    OF2D_HIP(hipGetLastError());
+}
+
+void launch_seqnorm_walk(const SeqnormBatch &B, int dimx, int dimy, int P, hipStream_t st) {
+    const unsigned nt = check_geometry(dimx, dimy, P);
+    const unsigned N = (unsigned)((size_t)dimx * dimy);
+    hipLaunchKernelGGL(seqnorm_walk, dim3(2 * B.K), dim3(64), 0, st, N, dimx, P, nt,
+                       jobs_of(B, nt));
     OF2D_HIP(hipGetLastError());
 }
 
@@ -976,35 +1251,45 @@ void launch_seqnorm_offsets(const double *const *totals, int r, double *out, hip
     OF2D_HIP(hipGetLastError());
 }
 
+// single pairs
+namespace {
+SeqnormBatch one(const float2 *cur, const float2 *prev, void *ws, bool use_profile) {
+    SeqnormBatch B;
+    B.K = 1;
+    B.u[0] = prev;
+    B.u[1] = cur;
+    B.ws[0] = ws;
+    B.use_profile[0] = use_profile;
+    return B;
+}
+}  // namespace
+
+void launch_seqnorm_pass(const float2 *cur, const float2 *prev, int dimx, int dimy, int P,
+                         void *ws, bool use_profile, hipStream_t st) {
+    launch_seqnorm_pass(one(cur, prev, ws, use_profile), dimx, dimy, P, st);
+}
+
 void launch_seqnorm_refine(const float2 *cur, const float2 *prev, int dimx, int dimy, int P,
                            void *ws, bool use_profile, const double *p_off, hipStream_t st) {
-    const unsigned nt = check_geometry(dimx, dimy, P);
-    const unsigned N = (unsigned)((size_t)dimx * dimy);
-    const SnWs w = carve(ws, nt);
-    const unsigned nb = (nt + 1 + kSnChk - 1) / kSnChk;  // blocks over tiles 0 .. nt
-    hipLaunchKernelGGL(seqnorm_check_sums, dim3(nb), dim3(kSnChk), 0, st, nt, w,
-                       use_profile ? 1 : 0);
-    hipLaunchKernelGGL(seqnorm_check_scan, dim3(1), dim3(kSnScan), 0, st, nt, nb, w, p_off);
-    hipLaunchKernelGGL(seqnorm_check, dim3(nb), dim3(kSnChk), 0, st, nt, w, use_profile ? 1 : 0);
-    OF2D_HIP(hipGetLastError());
-    hipLaunchKernelGGL(seqnorm_fix, dim3(std::min(nt, 1024u)), dim3(kSnThreads), 0, st, cur,
-                       prev, N, dimx, P, nt, w);
-    OF2D_HIP(hipGetLastError());
+    SeqnormBatch B = one(cur, prev, ws, use_profile);
+    B.p_off[0] = p_off;
+    launch_seqnorm_refine(B, dimx, dimy, P, st);
 }
 
 void launch_seqnorm_tables(const float2 *cur, const float2 *prev, int dimx, int dimy, int P,
                            void *ws, bool use_profile, hipStream_t st) {
-    launch_seqnorm_pass(cur, prev, dimx, dimy, P, ws, use_profile, st);
-    launch_seqnorm_refine(cur, prev, dimx, dimy, P, ws, use_profile, nullptr, st);
+    const SeqnormBatch B = one(cur, prev, ws, use_profile);
+    launch_seqnorm_pass(B, dimx, dimy, P, st);
+    launch_seqnorm_refine(B, dimx, dimy, P, st);
 }
 
 void launch_seqnorm_walk(const float2 *cur, const float2 *prev, int dimx, int dimy, int P,
                          void *ws, const float *s_in, float *out, int *dbg, hipStream_t st) {
-    const unsigned nt = check_geometry(dimx, dimy, P);
-    const unsigned N = (unsigned)((size_t)dimx * dimy);
-    hipLaunchKernelGGL(seqnorm_walk, dim3(2), dim3(64), 0, st, cur, prev, N, dimx, P, nt,
-                       carve(ws, nt), s_in, out, dbg);
-    OF2D_HIP(hipGetLastError());
+    SeqnormBatch B = one(cur, prev, ws, false);
+    B.s_in[0] = s_in;
+    B.out[0] = out;
+    B.dbg[0] = dbg;
+    launch_seqnorm_walk(B, dimx, dimy, P, st);
 }
 
 void launch_seqnorm(const float2 *cur, const float2 *prev, int dimx, int dimy, int P, void *ws,

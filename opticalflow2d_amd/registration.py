@@ -154,6 +154,26 @@ def motion_norms(cur, prev, dims: Sequence[int]):
     return sums, res
 
 
+def motion_norms_chain(u, dims: Sequence[int], batch: int = 3):
+    """The Logger norms of each update of a chain of iterates ``u``
+    (float32 ``[niter + 1, dimx*dimy, 2]``), computed in batches of ``batch``
+    updates as the registration loop runs them (include/of2d.h
+    of2d_motion_norms_chain).  Returns ``(sums float32[niter, 2], stats
+    int32[niter, 8])``."""
+    dimx, dimy = int(dims[0]), int(dims[1])
+    a = np.ascontiguousarray(np.asarray(u, np.float32).reshape(-1))
+    n = 2 * dimx * dimy
+    if a.size % n or a.size < 2 * n:
+        raise ValueError("u needs (niter + 1) * dimx*dimy*2 floats")
+    niter = a.size // n - 1
+    sums = np.zeros(2 * niter, np.float32)
+    res = np.zeros(8 * niter, np.int32)
+    L = _lib.lib()
+    check(L.of2d_motion_norms_chain(a, dimx, dimy, niter, int(batch), sums, res),
+          L.of2d_gateway_last_error().decode())
+    return sums.reshape(niter, 2), res.reshape(niter, 8)
+
+
 # ------------------------------------------------------------------ object API
 class ImageRegistration:
     """Handle on one registration context (of2d_create ... of2d_destroy).

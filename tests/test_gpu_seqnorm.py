@@ -80,6 +80,28 @@ def test_ties_every_term(gpu, oracle):
     check(oracle, cur, prev, (4500, 4000))
 
 
+@pytest.mark.parametrize("base", [1.5, 0.75])
+def test_near_half_ulps(gpu, oracle, base):
+    """Magnitudes within a few float ulps of a half-ulp of the running sum:
+    |(base, y)| with y in [0, 2^-8] is base + [0, 2^-17.6], so d / ulp(S)
+    lies just above a half-integer by less than, about and more than the
+    fp32 estimate's decision margin (seqnorm_kernels.hip sn_incr_est): both
+    the estimate and the exact fp64 sequence decide terms there, with ties
+    (y = 0) and the 2^23 / 2^24 binades of S among them."""
+    rng = np.random.default_rng(31 if base == 1.5 else 32)
+    dims = (4096, 4096)
+    n = dims[0] * dims[1]
+    prev = np.zeros((n, 2), np.float32)
+    prev[:, 0] = np.float32(base)
+    prev[:, 0] -= rng.integers(0, 3, n).astype(np.float32) * np.float32(2.0 ** -23)
+    prev[:, 1] = rng.uniform(0, 2.0 ** -8, n).astype(np.float32)
+    prev[rng.random(n) < 0.1, 1] = 0.0
+    cur = np.zeros_like(prev)
+    cur[:, 0] = prev[:, 0] * np.float32(2.0)
+    cur[:, 1] = prev[:, 1] * np.float32(3.0)
+    check(oracle, cur, prev, dims)
+
+
 def test_leading_zeros_and_tiny(gpu, oracle):
     rng = np.random.default_rng(11)
     dims = (3000, 200)
@@ -152,3 +174,38 @@ def test_profile_misprediction(gpu, oracle):
         curs.append(p + (rng.normal(0, 1e-3, (n, 2)) * scale).astype(np.float32))
         prevs.append(p)
     check_seq(oracle, curs, prevs, dims)
+
+
+def hs_like_chain(dims, niter, seed):
+    """u_k = A (1 - 0.8^k) + noise: smooth fields converging geometrically, as
+    a registration loop's iterates do (|u_k - u_{k-1}| shrinks each update)."""
+    rng = np.random.default_rng(seed)
+    dimx, dimy = dims
+    x = np.arange(dimx, dtype=np.float32)[None, :] / dimx
+    y = np.arange(dimy, dtype=np.float32)[:, None] / dimy
+    A = np.stack([1.5 * np.sin(6.3 * x + 2.0 * y) + 0.4 * np.cos(17.0 * y),
+                  1.2 * np.cos(5.1 * y - 3.0 * x) + 0.3 * np.sin(23.0 * x)], -1)
+    A = A.astype(np.float32).reshape(-1, 2)
+    u = np.zeros((niter + 1, dimx * dimy, 2), np.float32)
+    for k in range(1, niter + 1):
+        w = np.float32(1.0 - 0.8 ** k)
+        u[k] = A * w + rng.normal(0, 1e-3, A.shape).astype(np.float32)
+    return u
+
+
+@pytest.mark.parametrize("batch", [1, 2, 3])
+@pytest.mark.parametrize("dims,niter", [((4096, 4096), 7), ((1000, 1003), 8), ((37, 5), 4)])
+def test_batched_chain(gpu, oracle, batch, dims, niter):
+    """The registration loop's batches (one pass over K + 1 iterates for K
+    updates, the check / fix / walk of the K updates in one launch each, two
+    workspace sets predicting each other's successors): every update's sums
+    bit for bit, ragged last batches included."""
+    from opticalflow2d_amd.registration import motion_norms_chain
+    u = hs_like_chain(dims, niter, 40 + batch)
+    got, res = motion_norms_chain(u, dims, batch)
+    for k in range(niter):
+        want = oracle_sums(oracle, u[k + 1], u[k])
+        assert got[k].view(np.uint32).tolist() == want.view(np.uint32).tolist(), (k, got[k], want)
+    if dims == (4096, 4096):
+        # a cost figure, not a result: predicted updates resolve few tiles
+        assert res[2:, :2].max() < 200, res
