@@ -168,6 +168,9 @@ int of2d_slab_time_kernel(of2d_slab *s, int nlaunch, double *avg_us);
  * launch, interior/edge split (0/1), triple kernel derives dI from Iaux (0/1)};
  * returns the number of entries written */
 int of2d_slab_info(const of2d_slab *s, int *info, int n);
+/* the Logger errors of the last of2d_slab_run's iterations (the global ones:
+ * the same on every rank), up to n into out; returns how many there are */
+int of2d_slab_last_errors(const of2d_slab *s, float *out, int n);
 /* wall time (ms, HIP events) of the last of2d_slab_run on this rank */
 int of2d_slab_last_run_ms(const of2d_slab *s, double *ms);
 /* the triple kernel's own average launch time (us) inside the last run,
@@ -175,10 +178,16 @@ int of2d_slab_last_run_ms(const of2d_slab *s, double *ms);
  * first 64 chunks on the solver's stream (halo exchange included for N > 1),
  * and the number of launches that average covers */
 int of2d_slab_last_run_kernel_us(const of2d_slab *s, double *avg_us, int *nlaunch);
-/* tuning switches (no reference counterpart; results are bit-identical either way):
+/* options (no reference counterpart):
  *   "hs_gradients_from_image" (-1 auto = default, 0, 1): the triple kernel
  *   derives dI from Iaux in the kernel (24 B/px per launch) instead of reading
- *   dI (28); auto does so when dI + It (12 B/px) exceed the 256 MB MALL */
+ *   dI (28); auto does so when dI + It (12 B/px) exceed the 256 MB MALL;
+ *   bit-identical either way
+ *   "logger_fp64" (0 = default / 1): as of2d_set_option's; 0 takes the
+ *   convergence-on Logger norms as the reference does (one float running sum
+ *   over the slabs in rank order, so the break falls on the one-grid
+ *   reference's iteration), 1 sums the fused fp64 partials (fixed_iters runs
+ *   always do) */
 int of2d_slab_set_option(of2d_slab *s, const char *key, double value);
 int of2d_slab_destroy(of2d_slab *s);
 const char *of2d_slab_last_error(const of2d_slab *s);

@@ -898,15 +898,13 @@ void launch_increment(const float2 *u, const float4 *vel, float2 *R, int dimx, i
     OF2D_HIP(hipGetLastError());
 }
 
-int sor_increment_workers() {
-    static const int nc = [] {
-        // A/B knob: worker workgroups (-1: every CU the strips leave; 0: separate
-        // increment pass)
-        const char *e = std::getenv("OF2D_SOR_NCONS");
-        return e ? std::atoi(e) : -1;
-    }();
-    return nc;
-}
+// Worker workgroups of the increment behind the sweep: -1 every CU the strips
+// leave, 0 a separate increment pass (an A/B build knob: -DOF2D_SOR_NCONS=n,
+// tools/build_variant.sh)
+#ifndef OF2D_SOR_NCONS
+#define OF2D_SOR_NCONS -1
+#endif
+int sor_increment_workers() { return OF2D_SOR_NCONS; }
 
 void launch_sor_increment(float4 *vb, int dimx, int dimy, int P, float mu, float lambda,
                           float omega, void *H, unsigned epoch, unsigned *ticket,

@@ -43,6 +43,25 @@ struct DeviceError : std::runtime_error {
                                       " at " __FILE__ ":" + std::to_string(__LINE__));   \
     } while (0)
 
+// Restores the calling thread's current device when the scope ends (normally
+// or by an exception); bind() switches it meanwhile.  The multi-device paths
+// switch devices per rank, and a caller's own device must survive every entry
+// point.
+class DeviceScope {
+   public:
+    DeviceScope() { (void)hipGetDevice(&prev_); }
+    explicit DeviceScope(int dev) : DeviceScope() { bind(dev); }
+    ~DeviceScope() {
+        if (prev_ >= 0) (void)hipSetDevice(prev_);
+    }
+    void bind(int dev) { OF2D_HIP(hipSetDevice(dev)); }
+    DeviceScope(const DeviceScope &) = delete;
+    DeviceScope &operator=(const DeviceScope &) = delete;
+
+   private:
+    int prev_ = -1;
+};
+
 // status bits written by kernels (one word per context, zeroed per call)
 constexpr unsigned kStatusDivZero = 1u;
 constexpr unsigned kStatusExpBound = 2u;  // scaling-and-squaring count above the host bound
@@ -232,12 +251,15 @@ void launch_seqnorm_walk(const float2 *cur, const float2 *prev, int dimx, int di
                          void *ws, const float *s_in, float *out, int *dbg, hipStream_t st);
 // launch_seqnorm_tables in parts for row slabs: the pass over the slab, its
 // fp64 total (returned: device double[2] inside ws), the predecessors' totals
-// summed in rank order (device pointers, peer-readable), and the check / fix
-// with that offset (p_off, device double[2], optional)
+// chained in rank order for K pairs (poff = the previous rank's nxt, or 0
+// without one; nxt = poff + tot: device double[K][2] each, prev_nxt
+// peer-readable), and the
+// check / fix with that offset (p_off, device double[2], optional)
 void launch_seqnorm_pass(const float2 *cur, const float2 *prev, int dimx, int dimy, int P,
                          void *ws, bool use_profile, hipStream_t st);
 const double *seqnorm_total(int dimx, int dimy, int P, void *ws, hipStream_t st);
-void launch_seqnorm_offsets(const double *const *totals, int r, double *out, hipStream_t st);
+void launch_seqnorm_offset_chain(const double *prev_nxt, const double *const *tot, int K,
+                                 double *poff, double *nxt, hipStream_t st);
 void launch_seqnorm_refine(const float2 *cur, const float2 *prev, int dimx, int dimy, int P,
                            void *ws, bool use_profile, const double *p_off, hipStream_t st);
 // A batch of K <= 3 consecutive Logger updates of one loop: pair i is
@@ -254,6 +276,10 @@ struct SeqnormBatch {
     float *out[3] = {};           // walk: the sums of pair i (device float[2])
     int *dbg[3] = {};             // walk: cost counters (int[10]), optional
 };
+// diagnostics (tools/seqnorm_bench; synchronous): the workspace's list count
+// and profile flags (cnt[0..3]), then per norm the tiles with segment entries,
+// with more than one candidate, with none (out[12])
+void seqnorm_ws_stats(const void *ws, int dimx, int dimy, unsigned *out);
 void launch_seqnorm_pass(const SeqnormBatch &b, int dimx, int dimy, int P, hipStream_t st);
 void launch_seqnorm_refine(const SeqnormBatch &b, int dimx, int dimy, int P, hipStream_t st);
 void launch_seqnorm_walk(const SeqnormBatch &b, int dimx, int dimy, int P, hipStream_t st);

@@ -17,7 +17,9 @@
 //   halo      before step t a rank copies its neighbours' boundary rows of
 //             u_{t-1} into its own ghost j-lines (after their step t-1)
 //   Logger    reference-exact (default): each rank's seqnorm tables with the
-//             fp64 totals of the ranks before it as the prediction offset, then
+//             fp64 totals of the ranks before it as the prediction offset
+//             (chained rank by rank: a rank reads only its neighbours'
+//             memory, the pairs whose peer access multi_for enables), then
 //             the walks chained in rank order, rank r starting from rank r-1's
 //             exact running sums — the linear order of Motion::norm
 //             (Motion.cpp:42-49) crosses the slabs in rank order, so the sums
@@ -47,18 +49,19 @@ struct RankSlab {
     Field<float2> dI;
     Field<float> It, Iref, Iaux;
     DevArray<double> partial, sums, poff;
+    DevArray<double> nxt;  // [4][2]: poff + this slab's total per iteration slot (t & 3)
     DevArray<unsigned> status;
     DevArray<unsigned char> ws[2];
     DevArray<float> seq;
     const double *tot[2] = {nullptr, nullptr};
     bool walked[2] = {false, false};
-    hipEvent_t ev_step[4] = {}, ev_tot[4] = {}, ev_fix[4] = {}, ev_walk[4] = {};
+    hipEvent_t ev_step[4] = {}, ev_fix[4] = {}, ev_walk[4] = {}, ev_off[4] = {};
     ~RankSlab() {
         (void)hipSetDevice(dev);
         for (hipStream_t s : {st, sn, wk})
             if (s) (void)hipStreamSynchronize(s);
         for (int k = 0; k < 4; k++)
-            for (hipEvent_t e : {ev_step[k], ev_tot[k], ev_fix[k], ev_walk[k]})
+            for (hipEvent_t e : {ev_step[k], ev_fix[k], ev_walk[k], ev_off[k]})
                 if (e) (void)hipEventDestroy(e);
         for (hipStream_t s : {st, sn, wk})
             if (s) (void)hipStreamDestroy(s);
@@ -87,7 +90,10 @@ void copy(void *dst, int dd, const void *src, int sd, size_t bytes, hipStream_t 
 }
 }  // namespace
 
-void Registration::multi_release() { lv_multi_.clear(); }
+void Registration::multi_release() {
+    DeviceScope scope;  // ~RankSlab switches to each rank's device
+    lv_multi_.clear();
+}
 
 MultiHS &Registration::multi_for(int s) {
     if ((int)lv_multi_.size() <= s) lv_multi_.resize(s + 1);
@@ -96,7 +102,8 @@ MultiHS &Registration::multi_for(int s) {
     auto m = std::make_shared<MultiHS>();
     m->dx = L.dx;
     m->dy = L.dy;
-    OF2D_HIP(hipGetDevice(&m->home));
+    DeviceScope scope;  // switched per rank below
+    m->home = home_;
     int count = 0;
     OF2D_HIP(hipGetDeviceCount(&count));
     const int n = ngpus_;
@@ -119,7 +126,7 @@ MultiHS &Registration::multi_for(int s) {
         for (hipStream_t *s : {&R->st, &R->sn, &R->wk})
             OF2D_HIP(hipStreamCreateWithFlags(s, hipStreamNonBlocking));
         for (int e = 0; e < 4; e++)
-            for (hipEvent_t *ev : {&R->ev_step[e], &R->ev_tot[e], &R->ev_fix[e], &R->ev_walk[e]})
+            for (hipEvent_t *ev : {&R->ev_step[e], &R->ev_fix[e], &R->ev_walk[e], &R->ev_off[e]})
                 OF2D_HIP(hipEventCreateWithFlags(ev, hipEventDisableTiming));
         for (auto &f : R->u) f.alloc(L.dx, R->nrows);  // one ghost j-line each side: the halo
         R->dI.alloc(L.dx, R->nrows);
@@ -130,6 +137,7 @@ MultiHS &Registration::multi_for(int s) {
         R->partial.alloc((size_t)nb * 2 * chunk_);
         R->sums.alloc(2 * (size_t)chunk_);
         R->poff.alloc(2);
+        R->nxt.alloc(8);
         R->status.alloc(64);
         for (auto &w : R->ws) w.alloc(seqnorm_workspace_bytes(L.dx, R->nrows));
         R->seq.alloc(2 * (size_t)chunk_);
@@ -220,7 +228,6 @@ int Registration::loop_hs_multi(int s, float alpha, int &final_buf) {
     // the reference's float norms of iteration t, rank by rank
     auto norms = [&](int in, int out, int t, int kglob) {
         const int w = kglob & 1;
-        const double *totals[kMaxLocalRanks];
         bool use_prof[kMaxLocalRanks];
         for (int k = 0; k < n; k++) {
             RankSlab &R = *M.r[k];
@@ -233,15 +240,22 @@ int Registration::loop_hs_multi(int s, float alpha, int &final_buf) {
             launch_seqnorm_pass(R.u[out].p, R.u[in].p, L.dx, R.nrows, L.P, R.ws[w].p,
                                 use_prof[k], R.sn);
             R.tot[w] = seqnorm_total(L.dx, R.nrows, L.P, R.ws[w].p, R.sn);
-            totals[k] = R.tot[w];
-            OF2D_HIP(hipEventRecord(R.ev_tot[t & 3], R.sn));
         }
+        // the offsets chained in rank order: rank k reads only rank k - 1's
+        // slot t & 3, which rank k - 1 rewrites four iterations later, after
+        // rank k has read it (the wait on rank k's ev_off of t - 4)
         for (int k = 0; k < n; k++) {
             RankSlab &R = *M.r[k];
             OF2D_HIP(hipSetDevice(R.dev));
-            for (int q = 0; q < k; q++)
-                OF2D_HIP(hipStreamWaitEvent(R.sn, M.r[q]->ev_tot[t & 3], 0));
-            launch_seqnorm_offsets(totals, k, R.poff.p, R.sn);
+            const double *prev_nxt = nullptr;
+            if (k > 0) {
+                OF2D_HIP(hipStreamWaitEvent(R.sn, M.r[k - 1]->ev_off[t & 3], 0));
+                prev_nxt = M.r[k - 1]->nxt.p + 2 * (t & 3);
+            }
+            if (k < n - 1 && t >= 4) OF2D_HIP(hipStreamWaitEvent(R.sn, M.r[k + 1]->ev_off[t & 3], 0));
+            launch_seqnorm_offset_chain(prev_nxt, &R.tot[w], 1, R.poff.p, R.nxt.p + 2 * (t & 3),
+                                        R.sn);
+            OF2D_HIP(hipEventRecord(R.ev_off[t & 3], R.sn));
             launch_seqnorm_refine(R.u[out].p, R.u[in].p, L.dx, R.nrows, L.P, R.ws[w].p,
                                   use_prof[k], R.poff.p, R.sn);
             OF2D_HIP(hipEventRecord(R.ev_fix[t & 3], R.sn));

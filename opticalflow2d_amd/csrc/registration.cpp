@@ -184,8 +184,12 @@ void Registration::set_option(const std::string &key, double v) {
 }
 
 void Registration::ensure_device() {
-    if (ready_) return;
+    if (ready_) {
+        OF2D_HIP(hipSetDevice(home_));  // the entry point's DeviceScope restores the caller's
+        return;
+    }
     if (device_ >= 0) OF2D_HIP(hipSetDevice(device_));
+    OF2D_HIP(hipGetDevice(&home_));
     OF2D_HIP(hipStreamCreateWithFlags(&st_, hipStreamNonBlocking));
     OF2D_HIP(hipStreamCreateWithFlags(&sn_st_, hipStreamNonBlocking));
     OF2D_HIP(hipStreamCreateWithFlags(&wk_st_, hipStreamNonBlocking));
@@ -231,6 +235,7 @@ void Registration::ensure_device() {
 
 // ImageRegistration::set_reference_image / set_moving_image (:103-121)
 void Registration::set_images(const double *ref, const double *mov) {
+    DeviceScope scope;  // the caller's device again on return
     ensure_device();
     const size_t n0 = (size_t)dimx_ * dimy_;
     Level &L0 = lv_[0];
@@ -266,6 +271,7 @@ void Registration::check_reported_status(unsigned st) {
 
 // ImageRegistration::estimate_motion (:133-156)
 void Registration::estimate() {
+    DeviceScope scope;  // the caller's device again on return
     ensure_device();
     iters_.clear();
     OF2D_HIP(hipMemsetAsync(d_status_, 0, 64 * sizeof(unsigned), st_));
@@ -586,6 +592,7 @@ int Registration::loop_hs(Level &L, int niter, float alpha, int &final_buf) {
 
 // WrapperOpticalFlow2d.cpp:105-117 -> Motion::copy_motion_to_input
 void Registration::get_motion(double *out) {
+    DeviceScope scope;  // the caller's device again on return
     ensure_device();
     Level &L0 = lv_[0];
     launch_motion_to_planar(L0.cur_motion(), L0.P, dimx_, dimy_, d_stage_, st_);
@@ -596,6 +603,7 @@ void Registration::get_motion(double *out) {
 
 // WrapperOpticalFlow2d.cpp:120-137: Imov.set_image; Imov.warp2d(motion[0])
 void Registration::warp(const double *in, double *out) {
+    DeviceScope scope;  // the caller's device again on return
     ensure_device();
     Level &L0 = lv_[0];
     const size_t n0 = (size_t)dimx_ * dimy_;

@@ -48,6 +48,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <vector>
 
 #include "of2d_device.h"
 
@@ -291,7 +292,18 @@ struct SnJobs {
     int *dbg[kSnMaxJobs];
 };
 
-constexpr int kSnPf = 2;  // segments per load group (the next group's loads in flight)
+// segments in flight per wave: a ring of kSnRing segment buffers, each
+// reloaded with the segment kSnRing ahead right after its own is consumed,
+// so a load has kSnRing - 1 segments' arithmetic to arrive (the pass: 4 x
+// (K + 1) float2; the fix, one pair: 8 x 2)
+#ifndef OF2D_SN_ABL
+#define OF2D_SN_ABL 0  // timing ablations of the pass (results wrong when set)
+#endif
+#ifndef OF2D_SN_RING3
+#define OF2D_SN_RING3 4
+#endif
+template <int K>
+constexpr int sn_ring() { return K == 1 ? 8 : (K == 2 ? 4 : OF2D_SN_RING3); }
 
 // The lane's terms of consecutive segments of one tile: iterates j0 .. j0 + K
 // at linear index L = row jj, column ii (the next segment's), 0 past the grid
@@ -363,16 +375,13 @@ __device__ __forceinline__ void sn_wave_pass(const SnJobs &J, unsigned N, int di
             for (int c = 0; c < NCA; c++) tl[i][n][c] = 0u;
         }
     SnLoader<K> ld(b, (unsigned)dimx);
-    float2 cv[kSnPf][K + 1];
+    constexpr int D = sn_ring<K>();
+    float2 cv[D][K + 1];
 #pragma unroll
-    for (int d = 0; d < kSnPf; d++) ld.next(J, 0, N, (unsigned)dimx, (unsigned)P, cv[d]);
-    for (int s0 = 0; s0 < kSnSegs; s0 += kSnPf) {
-        float2 nv[kSnPf][K + 1];
-        if (s0 + kSnPf < kSnSegs)
+    for (int d = 0; d < D; d++) ld.next(J, 0, N, (unsigned)dimx, (unsigned)P, cv[d]);
+    for (int s0 = 0; s0 < kSnSegs; s0 += D) {
 #pragma unroll
-            for (int d = 0; d < kSnPf; d++) ld.next(J, 0, N, (unsigned)dimx, (unsigned)P, nv[d]);
-#pragma unroll
-        for (int d = 0; d < kSnPf; d++) {
+        for (int d = 0; d < D; d++) {
             const int s = s0 + d;
 #pragma unroll
             for (int i = 0; i < K; i++) {
@@ -381,6 +390,10 @@ __device__ __forceinline__ void sn_wave_pass(const SnJobs &J, unsigned N, int di
                     // Field::operator- (Field.tpp:305-334) for |cur - prev|
                     const float x = n ? cv[d][i].x : cv[d][i + 1].x - cv[d][i].x;
                     const float y = n ? cv[d][i].y : cv[d][i + 1].y - cv[d][i].y;
+#if OF2D_SN_ABL == 2  // timing only: the loads and a sum, no arithmetic
+                    fs[i][n] += x + y;
+                    continue;
+#endif
                     const SnEst v = sn_est(x, y);
                     const bool nz = sn_ballot(v.nz) != 0ull;
                     zv[i][n] = lane == s ? nz : zv[i][n];
@@ -417,11 +430,8 @@ __device__ __forceinline__ void sn_wave_pass(const SnJobs &J, unsigned N, int di
                         for (int c = 0; c < NCA; c++) tl[i][n][c] += m[c];
                 }
             }
+            if (s0 + D < kSnSegs) ld.next(J, 0, N, (unsigned)dimx, (unsigned)P, cv[d]);
         }
-#pragma unroll
-        for (int d = 0; d < kSnPf; d++)
-#pragma unroll
-            for (int k = 0; k <= K; k++) cv[d][k] = nv[d][k];
     }
     auto sat = [](unsigned p, unsigned x) {
         return ((p | x) & kSnBad) | sn_sat(p & ~kSnBad, x & ~kSnBad);
@@ -484,16 +494,13 @@ __device__ __forceinline__ void sn_wave_fix(const SnJobs &J, int j, unsigned N, 
 #pragma unroll
         for (int c = 0; c < kSnCand; c++) gv[n][c] = 0u;
     SnLoader<1> ld(b, (unsigned)dimx);
-    float2 cv[kSnPf][2];
+    constexpr int D = sn_ring<1>();
+    float2 cv[D][2];
 #pragma unroll
-    for (int d = 0; d < kSnPf; d++) ld.next(J, j, N, (unsigned)dimx, (unsigned)P, cv[d]);
-    for (int s0 = 0; s0 < kSnSegs; s0 += kSnPf) {
-        float2 nv[kSnPf][2];
-        if (s0 + kSnPf < kSnSegs)
+    for (int d = 0; d < D; d++) ld.next(J, j, N, (unsigned)dimx, (unsigned)P, cv[d]);
+    for (int s0 = 0; s0 < kSnSegs; s0 += D) {
 #pragma unroll
-            for (int d = 0; d < kSnPf; d++) ld.next(J, j, N, (unsigned)dimx, (unsigned)P, nv[d]);
-#pragma unroll
-        for (int d = 0; d < kSnPf; d++) {
+        for (int d = 0; d < D; d++) {
             const int s = s0 + d;
 #pragma unroll
             for (int n = 0; n < 2; n++) {
@@ -525,11 +532,8 @@ __device__ __forceinline__ void sn_wave_fix(const SnJobs &J, int j, unsigned N, 
                     gv[n][c] = lane == s ? e : gv[n][c];
                 }
             }
+            if (s0 + D < kSnSegs) ld.next(J, j, N, (unsigned)dimx, (unsigned)P, cv[d]);
         }
-#pragma unroll
-        for (int d = 0; d < kSnPf; d++)
-#pragma unroll
-            for (int k = 0; k < 2; k++) cv[d][k] = nv[d][k];
     }
 #pragma unroll
     for (int n = 0; n < 2; n++) {
@@ -552,9 +556,12 @@ __device__ __forceinline__ void sn_wave_fix(const SnJobs &J, int j, unsigned N, 
 // the pass over every tile: one wave per tile, K pairs; the candidate count
 // picks the form (none: no profile; one or two: the usual); tiles where the
 // profile's window spans more binades (the first ones) are left to the fix
+#ifndef OF2D_SN_WPE
+#define OF2D_SN_WPE 1
+#endif
 template <int K>
-__global__ __launch_bounds__(kSnThreads) void seqnorm_tables(unsigned N, int dimx, int P,
-                                                            unsigned nt, SnJobs J) {
+__global__ __launch_bounds__(kSnThreads) __attribute__((amdgpu_waves_per_eu(OF2D_SN_WPE)))
+void seqnorm_tables(unsigned N, int dimx, int P, unsigned nt, SnJobs J) {
     if (blockIdx.x == 0 && threadIdx.x < 4)
 #pragma unroll
         for (int i = 0; i < K; i++) J.ws[i].cnt[threadIdx.x] = 0;  // seqnorm_check's list
@@ -594,6 +601,9 @@ __global__ __launch_bounds__(kSnThreads) void seqnorm_tables(unsigned N, int dim
                 if (hdr_nc(hd[i][n])) hd[i][n] |= kHdrPending;
         ncmax = 0;
     }
+#if OF2D_SN_ABL  // timing only: no tile entries
+    ncmax = 0;
+#endif
     if (ncmax == 0) sn_wave_pass<K, 0>(J, N, dimx, P, nt, b, hd);
     else if (ncmax == 1) sn_wave_pass<K, 1>(J, N, dimx, P, nt, b, hd);
     else sn_wave_pass<K, 2>(J, N, dimx, P, nt, b, hd);
@@ -765,15 +775,19 @@ __global__ __launch_bounds__(256) void seqnorm_total(unsigned nt, SnWs ws) {
                                                   sh[threadIdx.x][2] + sh[threadIdx.x][3];
 }
 
-struct RankTotals {
-    const double *p[kMaxLocalRanks];
+// A row slab's prediction offsets for K pairs, chained in rank order: poff =
+// the previous rank's running totals (0 for rank 0), nxt = poff + this slab's
+// totals (read by the next rank; only adjacent ranks touch each other's memory)
+struct SnTotals {
+    const double *p[kSnMaxJobs];
 };
-// out[n] = sum of the totals of ranks 0 .. r-1 (rank order)
-__global__ void seqnorm_offsets(RankTotals t, int r, double *__restrict__ out) {
-    if (threadIdx.x < 2) {
-        double s = 0.0;
-        for (int q = 0; q < r; q++) s += t.p[q][threadIdx.x];
-        out[threadIdx.x] = s;
+__global__ void seqnorm_offset_chain(const double *__restrict__ prev_nxt, SnTotals tot, int K,
+                                     double *__restrict__ poff, double *__restrict__ nxt) {
+    const int i = threadIdx.x >> 1, n = threadIdx.x & 1;
+    if (i < K) {
+        const double o = prev_nxt ? prev_nxt[2 * i + n] : 0.0;
+        poff[2 * i + n] = o;
+        nxt[2 * i + n] = o + tot.p[i][n];
     }
 }
 
@@ -1243,12 +1257,31 @@ const double *seqnorm_total(int dimx, int dimy, int P, void *ws, hipStream_t st)
     return w.tot64;
 }
 
-void launch_seqnorm_offsets(const double *const *totals, int r, double *out, hipStream_t st) {
-    if (r < 0 || r > kMaxLocalRanks) throw std::invalid_argument("launch_seqnorm_offsets: rank");
-    RankTotals t{};
-    for (int q = 0; q < r; q++) t.p[q] = totals[q];
-    hipLaunchKernelGGL(seqnorm_offsets, dim3(1), dim3(64), 0, st, t, r, out);
+void launch_seqnorm_offset_chain(const double *prev_nxt, const double *const *tot, int K,
+                                 double *poff, double *nxt, hipStream_t st) {
+    if (K < 1 || K > kSnMaxJobs) throw std::invalid_argument("launch_seqnorm_offset_chain: K");
+    SnTotals t{};
+    for (int i = 0; i < K; i++) t.p[i] = tot[i];
+    hipLaunchKernelGGL(seqnorm_offset_chain, dim3(1), dim3(64), 0, st, prev_nxt, t, K, poff, nxt);
     OF2D_HIP(hipGetLastError());
+}
+
+void seqnorm_ws_stats(const void *ws, int dimx, int dimy, unsigned *out) {
+    const unsigned nt = check_geometry(dimx, dimy, dimx);
+    const SnWs w = carve(const_cast<void *>(ws), nt);
+    unsigned cnt[4];
+    std::vector<unsigned> H(2 * (size_t)nt);
+    OF2D_HIP(hipMemcpy(cnt, w.cnt, sizeof cnt, hipMemcpyDeviceToHost));
+    OF2D_HIP(hipMemcpy(H.data(), w.H, H.size() * sizeof(unsigned), hipMemcpyDeviceToHost));
+    for (int k = 0; k < 4; k++) out[k] = cnt[k];
+    for (int k = 4; k < 12; k++) out[k] = 0;
+    for (size_t b = 0; b < nt; b++)
+        for (int n = 0; n < 2; n++) {
+            const unsigned h = H[2 * b + n];
+            out[4 + n] += (h & kHdrSeg) ? 1u : 0u;
+            out[6 + n] += (h & (kHdrZero | kHdrNan)) ? 0u : (unsigned)((h >> 16) & 7u) > 1u;
+            out[8 + n] += (h & (kHdrZero | kHdrNan)) ? 0u : (unsigned)((h >> 16) & 7u) == 0u;
+        }
 }
 
 // single pairs

@@ -26,8 +26,11 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <condition_variable>
+#include <memory>
+#include <thread>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -43,8 +46,18 @@
             throw ::of2d::DeviceError(std::string("RCCL error: ") + ncclGetErrorString(r_)); \
     } while (0)
 
+namespace of2d {
+struct SlabExact;  // the reference-exact Logger's state (below)
+}
+
 struct of2d_slab {
     int dimx = 0, dimy = 0, rank = 0, nranks = 1, rb = 0, re = 0, nrows = 0, P = 0;
+    // convergence-on runs: the Logger's norms as the reference takes them
+    // (float running sums in linear order across the slabs, SlabExact), or
+    // fp64 sums of the fused partials ("logger_fp64"); fixed_iters runs take
+    // no break and always use the fp64 sums
+    bool logger_fp64 = false;
+    of2d::SlabExact *ex = nullptr;
     int device = 0;
     float alpha = 0.0f;
     hipStream_t st = nullptr;
@@ -103,6 +116,10 @@ struct of2d_slab {
 // on a single GPU, where RCCL refuses two ranks on one device.
 struct of2d_slab_group {
     int n = 0;
+    // exact Logger: per rank, the groups whose offset / walk it has enqueued
+    // (the next rank waits for its neighbour's count before waiting on the
+    // neighbour's event); groups are counted over the slabs' lifetime
+    std::unique_ptr<std::atomic<long>[]> off_done, walk_done;
     std::mutex m;
     std::condition_variable cv;
     int arrived = 0;
@@ -302,6 +319,245 @@ SlabGeometry slab_geometry(const of2d_slab *s) {
 }
 }  // namespace
 
+// ---------------------------------------------------------------- exact Logger
+// The reference's Logger norms over the slabs (Motion.cpp:42-49 as
+// Logger::update_error takes them, Logger.cpp:32-51): one float running sum in
+// the global linear order, which crosses the slabs in rank order.  As on one
+// device (Registration::run_chunked_exact) every iterate stays in memory: the
+// iterations run in groups of up to three (a triple launch that stores all
+// three iterates, with its 3-line halo, or single steps with 1-line halos)
+// into a ring of kExR buffers, and each group's norms are one batch of
+// seqnorm launches (seqnorm_kernels.hip) over this slab's rows:
+//   sn  the pass, the slab's fp64 totals, the prediction offsets chained in
+//       rank order (rank r receives r - 1's running fp64 totals and sends its
+//       own on), the check / fix
+//   wk  the walk, chained in rank order: rank r starts from rank r - 1's
+//       exact running sums after its last term and passes its own on, so the
+//       last rank's walk ends with the reference's sums bit for bit
+// Over RCCL the chains are ncclRecv / ncclSend of 2K doubles / floats on
+// communicators of their own (one per stream: comm keeps the halo); in an
+// in-process group the next rank waits for its neighbour's event and reads its
+// device memory.  At each chunk's end the last rank's sums decide the break
+// on every rank (ncclBroadcast / a read of its memory).
+namespace of2d {
+constexpr int kExR = 12;   // ring buffers besides the chunk's start buffer
+constexpr int kExEv = 16;  // event / slot ring per group
+struct SlabExact {
+    Field<float2> extra[kExR + 1 - 3];  // buffers 3 .. kExR (0 .. 2 are the slab's u)
+    DevArray<unsigned char> ws[6];      // two sets of three workspaces
+    bool walked[6] = {};
+    hipStream_t sn = nullptr, wk = nullptr;
+    hipEvent_t ev_step[kExEv] = {}, ev_fix[kExEv] = {}, ev_walk[kExEv] = {}, ev_off[kExEv] = {};
+    DevArray<double> poff;    // [3][2] this group's prediction offsets
+    DevArray<double> nxt;     // [kExEv][3][2] offsets + this slab's totals, per group slot
+    DevArray<double> nxt_in;  // [kExEv][3][2] the previous rank's (RCCL)
+    DevArray<float> seq;      // [chunk][2] exact running sums after this slab
+    DevArray<float> sin;      // [kExEv][3][2] the previous rank's (RCCL)
+    ncclComm_t comm_sn = nullptr, comm_wk = nullptr;
+    long gseq = 0;  // groups enqueued over the slab's life (the same on every rank)
+    int dev = 0;
+    ~SlabExact() {
+        (void)hipSetDevice(dev);
+        for (hipStream_t q : {sn, wk})
+            if (q) (void)hipStreamSynchronize(q);
+        if (comm_sn) ncclCommDestroy(comm_sn);
+        if (comm_wk) ncclCommDestroy(comm_wk);
+        for (int k = 0; k < kExEv; k++)
+            for (hipEvent_t e : {ev_step[k], ev_fix[k], ev_walk[k], ev_off[k]})
+                if (e) (void)hipEventDestroy(e);
+        for (hipStream_t q : {sn, wk})
+            if (q) (void)hipStreamDestroy(q);
+    }
+};
+}  // namespace of2d
+
+namespace {
+using of2d::kExEv;
+using of2d::kExR;
+
+of2d::Field<float2> &exbuf(of2d_slab *s, int k) { return k < 3 ? s->u[k] : s->ex->extra[k - 3]; }
+
+// first exact run: the ring, workspaces, streams, events and (RCCL) the two
+// chain communicators, split from the halo communicator by every rank together
+void exact_setup(of2d_slab *s) {
+    if (s->ex) return;
+    auto *E = new of2d::SlabExact();
+    s->ex = E;
+    E->dev = s->device;
+    for (auto &f : E->extra) f.alloc(s->dimx, s->nrows, 3);
+    for (auto &w : E->ws) w.alloc(of2d::seqnorm_workspace_bytes(s->dimx, s->nrows));
+    OF2D_HIP(hipStreamCreateWithFlags(&E->sn, hipStreamNonBlocking));
+    OF2D_HIP(hipStreamCreateWithFlags(&E->wk, hipStreamNonBlocking));
+    for (int k = 0; k < kExEv; k++)
+        for (hipEvent_t *e : {&E->ev_step[k], &E->ev_fix[k], &E->ev_walk[k], &E->ev_off[k]})
+            OF2D_HIP(hipEventCreateWithFlags(e, hipEventDisableTiming));
+    E->poff.alloc(6);
+    E->nxt.alloc(6 * kExEv);
+    E->nxt_in.alloc(6 * kExEv);
+    E->seq.alloc(2 * (size_t)s->chunk);
+    E->sin.alloc(6 * kExEv);
+    if (s->comm && s->nranks > 1) {
+        OF2D_NCCL(ncclCommSplit(s->comm, 0, s->rank, &E->comm_sn, nullptr));
+        OF2D_NCCL(ncclCommSplit(s->comm, 0, s->rank, &E->comm_wk, nullptr));
+    }
+}
+
+// in-process group: wait until rank r has enqueued group g's record of `done`
+void wait_rank(const std::atomic<long> &done, long g) {
+    const auto t0 = std::chrono::steady_clock::now();
+    while (done.load(std::memory_order_acquire) <= g) {
+        std::this_thread::yield();
+        if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(60))
+            throw std::runtime_error("slab group: a rank did not reach the Logger chain");
+    }
+}
+
+// The convergence-on run with the reference's Logger; *done = iterations
+int run_exact(of2d_slab *s, int niter) {
+    exact_setup(s);
+    of2d::SlabExact &E = *s->ex;
+    of2d_slab_group *grp = s->grp;
+    const bool rccl = E.comm_sn != nullptr;
+    const int n = s->nranks, r = s->rank;
+    const of2d_slab *up = grp && r > 0 ? grp->slabs[r - 1] : nullptr;
+    const float alphasq = s->alpha * s->alpha;
+    const double npx = (double)s->dimx * s->dimy;
+    const int nb = slab_geometry(s).nb;
+    unsigned *range_flag = s->d_status + of2d::kRangeFlagWord;
+    const float *ia = use_gi(s) ? s->Imov.p : nullptr;
+    for (bool &w : E.walked) w = false;  // a new loop: no profile yet
+    auto ring = [](int a, int t) {  // the (t mod kExR)-th buffer other than a
+        const int i = t % kExR;
+        return i < a ? i : i + 1;
+    };
+    auto src_of = [&](int a, int t) { return t == 0 ? a : ring(a, t - 1); };
+    auto ev = [](hipEvent_t *e, long g) { return e[g % kExEv]; };
+    auto part = [&](int t) { return s->d_partial + (size_t)t * nb * 2; };
+    // one step from buffer `in` to `out` with its 1-line halo (chunk tails, replays)
+    auto single = [&](int in, int out, double *partial) {
+        float2 *uin = exbuf(s, in).p;
+        halo_exchange(s, uin, 1, s->st);
+        of2d::launch_hs_jacobi(uin, exbuf(s, out).p, s->dI.p, s->It.p, s->P, s->dimx, s->nrows,
+                               s->rb, s->dimy, alphasq, partial, s->d_status, s->st);
+    };
+    std::vector<long> group_of((size_t)s->chunk);
+    int a = s->start, k0 = 0;
+    while (k0 < niter) {
+        const int C = std::min(s->chunk, niter - k0);
+        long g = 0;
+        for (int t = 0; t < C; t += 0) {
+            const int k = std::min(3, C - t);
+            g = E.gseq++;
+            for (int m = t; m < t + k; m++) group_of[m] = g;
+            // the buffers of iterates t .. t + k - 1 held iterates t - kExR ..,
+            // last read by the walk of iterate t + k - kExR's group
+            if (t + k - kExR >= 0)
+                OF2D_HIP(hipStreamWaitEvent(s->st, ev(E.ev_walk, group_of[t + k - kExR]), 0));
+            if (k == 3) {
+                float2 *uin = exbuf(s, src_of(a, t)).p;
+                halo_exchange(s, uin, 3, s->st);
+                of2d::launch_hs_jacobi3(uin, exbuf(s, ring(a, t + 2)).p, s->dI.p, s->It.p, s->P,
+                                        s->dimx, s->nrows, s->rb, s->dimy, alphasq, -3,
+                                        s->nrows + 3, part(t), part(t + 1), part(t + 2),
+                                        s->d_status, range_flag, s->st, -1, -1, ia,
+                                        exbuf(s, ring(a, t)).p, exbuf(s, ring(a, t + 1)).p);
+            } else {
+                for (int m = t; m < t + k; m++) single(src_of(a, m), ring(a, m), part(m));
+            }
+            OF2D_HIP(hipEventRecord(ev(E.ev_step, g), s->st));
+            // the group's norms as one batch on this slab's rows
+            of2d::SeqnormBatch B;
+            B.K = k;
+            B.u[0] = exbuf(s, src_of(a, t)).p;
+            const double *tot[3];
+            for (int i = 0; i < k; i++) {
+                const int w = 3 * (int)(g & 1) + i;
+                B.u[i + 1] = exbuf(s, ring(a, t + i)).p;
+                B.ws[i] = E.ws[w].p;
+                B.use_profile[i] = E.walked[w];
+                E.walked[w] = true;
+                B.p_off[i] = E.poff.p + 2 * i;
+                B.out[i] = E.seq.p + 2 * (size_t)(t + i);
+            }
+            OF2D_HIP(hipStreamWaitEvent(E.sn, ev(E.ev_step, g), 0));
+            // workspace set g & 1: group g - 2's walk has read it and left its profile
+            if (g >= 2) OF2D_HIP(hipStreamWaitEvent(E.sn, ev(E.ev_walk, g - 2), 0));
+            of2d::launch_seqnorm_pass(B, s->dimx, s->nrows, s->P, E.sn);
+            for (int i = 0; i < k; i++)
+                tot[i] = of2d::seqnorm_total(s->dimx, s->nrows, s->P, B.ws[i], E.sn);
+            double *nxt = E.nxt.p + 6 * (g % kExEv);
+            const double *prev_nxt = nullptr;
+            if (r > 0 && rccl) {
+                double *in = E.nxt_in.p + 6 * (g % kExEv);
+                OF2D_NCCL(ncclRecv(in, 2 * k, ncclDouble, r - 1, E.comm_sn, E.sn));
+                prev_nxt = in;
+            } else if (r > 0 && grp) {
+                wait_rank(grp->off_done[r - 1], g);
+                OF2D_HIP(hipStreamWaitEvent(E.sn, ev(up->ex->ev_off, g), 0));
+                prev_nxt = up->ex->nxt.p + 6 * (g % kExEv);
+            }
+            of2d::launch_seqnorm_offset_chain(prev_nxt, tot, k, E.poff.p, nxt, E.sn);
+            if (rccl && r < n - 1)
+                OF2D_NCCL(ncclSend(nxt, 2 * k, ncclDouble, r + 1, E.comm_sn, E.sn));
+            OF2D_HIP(hipEventRecord(ev(E.ev_off, g), E.sn));
+            if (grp) grp->off_done[r].store(g + 1, std::memory_order_release);
+            of2d::launch_seqnorm_refine(B, s->dimx, s->nrows, s->P, E.sn);
+            OF2D_HIP(hipEventRecord(ev(E.ev_fix, g), E.sn));
+            OF2D_HIP(hipStreamWaitEvent(E.wk, ev(E.ev_fix, g), 0));
+            if (r > 0 && rccl) {
+                float *in = E.sin.p + 6 * (g % kExEv);
+                OF2D_NCCL(ncclRecv(in, 2 * k, ncclFloat, r - 1, E.comm_wk, E.wk));
+                for (int i = 0; i < k; i++) B.s_in[i] = in + 2 * i;
+            } else if (r > 0 && grp) {
+                wait_rank(grp->walk_done[r - 1], g);
+                OF2D_HIP(hipStreamWaitEvent(E.wk, ev(up->ex->ev_walk, g), 0));
+                for (int i = 0; i < k; i++) B.s_in[i] = up->ex->seq.p + 2 * (size_t)(t + i);
+            }
+            of2d::launch_seqnorm_walk(B, s->dimx, s->nrows, s->P, E.wk);
+            if (rccl && r < n - 1)
+                OF2D_NCCL(ncclSend(E.seq.p + 2 * (size_t)t, 2 * k, ncclFloat, r + 1, E.comm_wk,
+                                   E.wk));
+            OF2D_HIP(hipEventRecord(ev(E.ev_walk, g), E.wk));
+            if (grp) grp->walk_done[r].store(g + 1, std::memory_order_release);
+            t += k;
+        }
+        // the chunk's global sums: the last rank's walks
+        if (rccl)
+            OF2D_NCCL(ncclBroadcast(E.seq.p, E.seq.p, 2 * (size_t)C, ncclFloat, n - 1, E.comm_wk,
+                                    E.wk));
+        OF2D_HIP(hipStreamSynchronize(E.wk));
+        OF2D_HIP(hipStreamSynchronize(E.sn));
+        const of2d_slab *last = grp ? grp->slabs[n - 1] : s;
+        if (grp) grp->barrier();  // every rank's walks of the chunk are done
+        OF2D_HIP(hipMemcpy(s->hs.flt, last->ex->seq.p, sizeof(float) * 2 * C,
+                           hipMemcpyDeviceToHost));
+        if (grp) grp->barrier();  // read before the last rank's next chunk rewrites it
+        OF2D_HIP(hipMemcpyAsync(s->hs.status, s->d_status, sizeof(unsigned),
+                                hipMemcpyDeviceToHost, s->st));
+        OF2D_HIP(hipStreamSynchronize(s->st));
+        if (s->hs.status[0] & of2d::kStatusDivZero)
+            throw std::runtime_error("Divide by zero exception");
+        for (int t = 0; t < C; t++) {
+            const int kk = k0 + t;
+            const float e = of2d::logger_error(s->hs.flt[2 * t], s->hs.flt[2 * t + 1], npx);
+            s->errs.push_back(e);
+            if (e < 0.001f && kk > 1) {  // ImageRegistrationOpticalFlow.cpp:131-134
+                // iteration t's buffer was reused by iteration t + kExR: replay
+                // (every rank: the sums are global)
+                if (t + kExR <= C - 1)
+                    for (int q = 0; q <= t; q++) single(src_of(a, q), ring(a, q), s->d_partial);
+                s->fin = ring(a, t);
+                return kk + 1;
+            }
+        }
+        a = ring(a, C - 1);
+        k0 += C;
+    }
+    s->fin = a;
+    return niter;
+}
+}  // namespace
+
 extern "C" {
 
 int of2d_slab_bounds(int dimy, int rank, int nranks, int *row_begin, int *row_end) {
@@ -405,6 +661,12 @@ int of2d_slab_group_create(of2d_slab_group **out, int nranks) {
     g->slabs.assign(nranks, nullptr);
     g->ptr.assign(nranks, nullptr);
     g->flag.assign(nranks, 0);
+    g->off_done.reset(new std::atomic<long>[nranks]);
+    g->walk_done.reset(new std::atomic<long>[nranks]);
+    for (int r = 0; r < nranks; r++) {
+        g->off_done[r] = 0;
+        g->walk_done[r] = 0;
+    }
     *out = g;
     return OF2D_OK;
 }
@@ -575,6 +837,17 @@ int of2d_slab_run(of2d_slab *s, int niter, int fixed_iters, int *iters_done) {
         if (s->start_dirty) s->u[s->start].zero(s->st);
         s->start_dirty = true;
         int a = s->start, k0 = 0, done = -1;
+        if (!fixed_iters && !s->logger_fp64) {
+            done = run_exact(s, niter);
+            if (s->fin >= 3) {  // into a buffer of u[] (get_motion, the next run's start)
+                const int x = (s->start + 1) % 3;
+                OF2D_HIP(hipMemcpyAsync(s->u[x].p, exbuf(s, s->fin).p,
+                                        sizeof(float2) * (size_t)s->nrows * s->P,
+                                        hipMemcpyDeviceToDevice, s->st));
+                s->fin = x;
+            }
+            k0 = niter;  // skips the fused-partials loop
+        }
         while (k0 < niter && done < 0) {
             const int C = std::min(fixed_iters ? s->chunk_fixed : s->chunk, niter - k0);
             auto part = [&](int t) { return s->d_partial + (size_t)t * nb * 2; };
@@ -754,6 +1027,10 @@ int of2d_slab_info(const of2d_slab *s, int *info, int n) {
 
 int of2d_slab_set_option(of2d_slab *s, const char *key, double value) {
     if (!s || !key) return OF2D_ERR_INVALID_ARGUMENT;
+    if (std::strcmp(key, "logger_fp64") == 0) {
+        s->logger_fp64 = value != 0.0;
+        return OF2D_OK;
+    }
     if (std::strcmp(key, "hs_gradients_from_image") == 0) {
         s->gi = value < 0.0 ? -1 : (value != 0.0 ? 1 : 0);
         return OF2D_OK;
@@ -769,6 +1046,13 @@ int of2d_slab_last_run_kernel_us(const of2d_slab *s, double *avg_us, int *nlaunc
     return OF2D_OK;
 }
 
+int of2d_slab_last_errors(const of2d_slab *s, float *out, int n) {
+    if (!s || (n > 0 && !out)) return -OF2D_ERR_INVALID_ARGUMENT;
+    const int k = std::min(n, (int)s->errs.size());
+    for (int i = 0; i < k; i++) out[i] = s->errs[i];
+    return (int)s->errs.size();
+}
+
 int of2d_slab_last_run_ms(const of2d_slab *s, double *ms) {
     if (!s || !ms) return OF2D_ERR_INVALID_ARGUMENT;
     *ms = s->last_ms;
@@ -779,6 +1063,11 @@ int of2d_slab_destroy(of2d_slab *s) {
     if (!s) return OF2D_ERR_INVALID_ARGUMENT;
     if (s->st) (void)hipStreamSynchronize(s->st);
     if (s->comm_st) (void)hipStreamSynchronize(s->comm_st);
+    if (s->ex) {
+        (void)hipSetDevice(s->device);
+        for (auto &f : s->ex->extra) f.release();
+        delete s->ex;
+    }
     if (s->comm) ncclCommDestroy(s->comm);
     if (s->grp) {
         std::lock_guard<std::mutex> lk(s->grp->m);

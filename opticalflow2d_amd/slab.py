@@ -153,6 +153,16 @@ class SlabSolver:
         self._chk(_lib.lib().of2d_slab_last_run_kernel_us(self._h, C.byref(us), C.byref(n)))
         return us.value, n.value
 
+    def errors(self) -> np.ndarray:
+        """The Logger errors of the last run's iterations (float32; global)."""
+        L = _lib.lib()
+        k = L.of2d_slab_last_errors(self._h, np.zeros(1, np.float32), 0)
+        if k < 0:
+            self._chk(-k)
+        out = np.zeros(max(k, 1), np.float32)
+        L.of2d_slab_last_errors(self._h, out, k)
+        return out[:k]
+
     def last_run_ms(self) -> float:
         ms = C.c_double(0.0)
         self._chk(_lib.lib().of2d_slab_last_run_ms(self._h, C.byref(ms)))

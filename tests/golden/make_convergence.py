@@ -12,8 +12,10 @@ and a SHA-256 of the final motion's float32 bits, so a GPU test can compare a
 for the oracle with the Logger's norms summed in double (oracle_set_logger_fp64):
 at 4096^2 the reference's sequential FLOAT running sum (Motion.cpp:42-49)
 rounds each of its 16.7 M additions at ~1 ulp of the sum, so its error can
-cross 0.001 an iteration away from where the exactly summed error does; the
-GPU sums in fp64 and follows the exact-norm break.
+cross 0.001 an iteration away from where the exactly summed error does.  The
+GPU's default Logger reproduces the float running sum bit for bit
+(seqnorm_kernels.hip) and is checked against the reference-semantics records;
+its `logger_fp64` mode sums in fp64 and is checked against "exact_norms".
 
     python tests/golden/make_convergence.py [--exact-only] [name ...]
 """

@@ -29,13 +29,14 @@ def _bits(a):
     return np.asarray(a, dtype=np.float32).view(np.uint32)
 
 
-def run_group(ref, mov, alpha, nranks, niter, fixed, gi=-1):
+def run_group(ref, mov, alpha, nranks, niter, fixed, gi=-1, fp64=0, errors=False):
     dimx, dimy = ref.shape
     g = SlabGroup(nranks)
     slabs = [SlabSolver(dimx, dimy, alpha, r, nranks, group=g) for r in range(nranks)]
     try:
         for s in slabs:
             s.set_option("hs_gradients_from_image", gi)
+            s.set_option("logger_fp64", fp64)
             lo, hi = halo_rows(dimy, s.rank, nranks)
             s.set_images(ref[:, lo:hi], mov[:, lo:hi])
         done, errs = [None] * nranks, [None] * nranks
@@ -54,6 +55,10 @@ def run_group(ref, mov, alpha, nranks, niter, fixed, gi=-1):
         assert not any(t.is_alive() for t in th), "a rank did not finish"
         assert errs == [None] * nranks, errs
         m = np.concatenate([s.motion() for s in slabs], axis=1)
+        if errors:
+            errs = [s.errors() for s in slabs]
+            assert all(np.array_equal(e.view(np.uint32), errs[0].view(np.uint32)) for e in errs)
+            return m, done, errs[0]
         return m, done
     finally:
         for s in slabs:
@@ -61,10 +66,11 @@ def run_group(ref, mov, alpha, nranks, niter, fixed, gi=-1):
         g.close()
 
 
-def run_single(ref, mov, alpha, niter, fixed):
+def run_single(ref, mov, alpha, niter, fixed, fp64=0):
     dimx, dimy = ref.shape
     s = SlabSolver(dimx, dimy, alpha)
     try:
+        s.set_option("logger_fp64", fp64)
         s.set_images(ref, mov)
         it = s.run(niter, fixed_iters=fixed)
         return s.motion(), it
@@ -92,14 +98,41 @@ def test_slab_group_fixed_iterations_bitwise(gpu, dimx, dimy, nranks, niter, gi)
     assert np.array_equal(_bits(mN), _bits(m1))
 
 
+@pytest.mark.parametrize("fp64", [0, 1])
 @pytest.mark.parametrize("nranks", [2, 3])
-def test_slab_group_break_replay(gpu, nranks):
-    """Default semantics: every rank sees the all-reduced Logger sums, breaks at
-    the same iteration and replays single steps (with their one-line exchanges)
-    from the chunk's start buffer."""
+def test_slab_group_break_replay(gpu, nranks, fp64):
+    """Convergence on: every rank sees the global Logger sums (fp64 = 0: the
+    last rank's chained float running sums; 1: the all-reduced fp64 sums),
+    breaks at the same iteration and replays single steps (with their one-line
+    exchanges) from the chunk's start buffer."""
     ref, mov = S.texture_pair(192, seed=7)
-    m1, it1 = run_single(ref, mov, 0.1, 1000, False)
+    m1, it1 = run_single(ref, mov, 0.1, 1000, False, fp64)
     assert it1 < 1000
-    mN, itN = run_group(ref, mov, 0.1, nranks, 1000, False)
+    mN, itN = run_group(ref, mov, 0.1, nranks, 1000, False, fp64=fp64)
     assert itN == [it1] * nranks
     assert np.array_equal(_bits(mN), _bits(m1))
+
+
+@pytest.mark.parametrize("nranks", [1, 2, 3, 8])
+def test_slab_group_reference_logger_4096(gpu, nranks):
+    """The reference's Logger across slabs: one float running sum in linear
+    order, chained through the ranks' walks (Motion.cpp:42-49), so the slab
+    group breaks where the one-grid reference does.  Bar: the 4096^2 texture
+    fixture (tests/golden/convergence_hs_texture4096.json, the oracle's record
+    of the reference semantics): 102 iterations, the motion's sha256 and every
+    iteration's error bit for bit, on 1, 2, 3 and 8 slabs."""
+    import json
+    import hashlib
+    import os
+    from conftest import GOLDEN
+    fx = json.load(open(os.path.join(GOLDEN, "convergence_hs_texture4096.json")))
+    ref, mov = S.texture_pair(fx["n"])
+    m, done, errs = run_group(ref, mov, fx["alpha"], nranks, fx["niter"][0], False,
+                              errors=True)
+    assert done == fx["iterations_executed"] * nranks
+    f = np.asarray(m, np.float32)
+    planar = np.concatenate([f[:, :, 0].reshape(-1, order="F"),
+                             f[:, :, 1].reshape(-1, order="F")])
+    assert hashlib.sha256(planar.tobytes()).hexdigest() == fx["motion_sha256_f32_planar"]
+    want = np.asarray(fx["errors"], np.float32)
+    assert errs.view(np.uint32).tolist() == want.view(np.uint32).tolist()

@@ -3,7 +3,8 @@
 # own time limit, logs in gpurun_out/<tag>_<step>.log; stops at the first
 # step that fails (a fault, abort or time limit ends the call there).
 #   tools/gpu.sh <tag> <step>...
-# steps: tests (pytest -m gpu), sntests (Logger-norm tests), smoke, bench,
+# steps: tests (pytest -m gpu), sntests (Logger-norm tests), slabtests
+#        (slab group / RCCL / ngpus tests), smoke, bench,
 #        prof (rocprofv3 kernel stats of bench.py), conv (convergence-on
 #        timings at 4096^2), convprof (their kernel trace + stats),
 #        configs (bench_configs.py), ranks (ngpus timings), snbench /
@@ -28,6 +29,7 @@ for s in "$@"; do
     case $s in
         tests) run tests 900 $PT -m gpu tests ;;
         sntests) run sntests 600 $PT tests/test_gpu_seqnorm.py tests/test_gpu_convergence.py ;;
+        slabtests) run slabtests 900 $PT tests/test_gpu_slab_local.py tests/test_gpu_rccl.py tests/test_gpu_ranks.py ;;
         smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
         bench) run bench 600 python bench.py ;;
         prof) run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/$O/${tag}_prof" -o k -- python3 "$R/bench.py" --no-cpu-baseline ;;
@@ -36,6 +38,7 @@ for s in "$@"; do
         configs) run configs 900 python -u bench_configs.py ;;
         ranks) run ranks 600 python -u tools/time_ranks.py ;;
         snbench) run snbench 300 bash -c "tools/seqnorm_bench 4096 12 3 0.95 && tools/seqnorm_bench 4096 12 1 0.95 && tools/seqnorm_bench 4096 12 3 0.8" ;;
+        snws) run snws 300 env SNB_WS=1 tools/seqnorm_bench 4096 12 3 0.95 ;;
         sndebug) run sndebug 300 env OF2D_SN_DEBUG=1 python -u tools/time_convergence.py 4096 1 ;;
         snprof) run snprof 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/$O/${tag}_snprof" -o k -- "$R/tools/seqnorm_bench" 4096 24 3 ;;
         *) echo "unknown step $s"; exit 2 ;;

@@ -86,6 +86,16 @@ int main(int argc, char **argv) {
             CK(hipEventRecord(e[2], st));
             of2d::launch_seqnorm_walk(S, n, n, P, st);
             CK(hipEventRecord(e[3], st));
+            if (rep > 0 && std::getenv("SNB_WS")) {
+                CK(hipStreamSynchronize(st));
+                for (int i = 0; i < S.K; i++) {
+                    unsigned q[12];
+                    of2d::seqnorm_ws_stats(S.ws[i], n, n, q);
+                    std::printf("  update %d ws %d: listed %u prof %u %u | seg %u %u multi %u %u none %u %u\n",
+                                t + i, 3 * (g & 1) + i, q[0], q[1], q[2], q[4], q[5], q[6], q[7],
+                                q[8], q[9]);
+                }
+            }
             t += S.K;
         }
         CK(hipStreamSynchronize(st));
