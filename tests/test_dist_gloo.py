@@ -6,12 +6,17 @@ over RCCL: chunks of 32 iterations run as fused launches of K = 3 (then a
 pair / single tail); before each launch K ghost j-lines above and below are
 exchanged (the first K / last K owned lines); step k of a launch is computed
 on the owned rows plus K-k halo rows on each side (their gradients come from
-image halo rows); the global-j border rule; the Logger sums of the owned rows
-all-reduced per iteration.  The step itself is a
-numpy float32 restatement (elementwise IEEE ops in the reference's order).
+image halo rows); the global-j border rule; the Logger's norms as the
+reference takes them (Motion.cpp:42-49): one float running sum in linear
+order, which crosses the slabs in rank order, so each rank continues the sums
+it receives from the rank above and passes them on, and the last rank's sums
+decide the break on every rank (slab.cpp run_exact: the walks chained by
+ncclRecv / ncclSend, the sums broadcast from the last rank).  The step itself
+is a numpy float32 restatement (elementwise IEEE ops in the reference's order).
 The gathered motion must equal the single-grid oracle bit for bit, and the
 iteration count with convergence on must match the oracle's.
 """
+import math
 import os
 import socket
 import tempfile
@@ -107,13 +112,22 @@ def _worker(rank, world, port, dimx, dimy, niter, fixed, outdir):
             u[H + rows:H + rows + lines] = dn.numpy()
 
     def sums(new, old):
-        d = (new - old).astype(np.float64)
-        p = old.astype(np.float64)
-        t = torch.tensor([float(np.sqrt(d[..., 0] ** 2 + d[..., 1] ** 2).sum()),
-                          float(np.sqrt(p[..., 0] ** 2 + p[..., 1] ** 2).sum())],
-                         dtype=torch.float64)
-        dist.all_reduce(t)
-        return logger_error(float(t[0]), float(t[1]), dimx * dimy)
+        """Logger::update_error's two norms: the float running sums continued
+        from the rank above over this slab's rows (x fastest), passed on."""
+        S = torch.zeros(2, dtype=torch.float32)
+        if rank > 0:
+            dist.recv(S, rank - 1)
+        out = []
+        for k, f in enumerate((new - old, old)):  # Field::operator-, then prev
+            acc = F(S[k].item())
+            for x, y in f.reshape(-1, 2).tolist():
+                acc = F(float(acc) + math.sqrt(x * x + y * y))  # (float)((double)S + d)
+            out.append(acc)
+        S = torch.tensor(out, dtype=torch.float32)
+        if rank < world - 1:
+            dist.send(S, rank + 1)
+        dist.broadcast(S, world - 1)
+        return logger_error(S[0].item(), S[1].item(), dimx * dimy)
 
     def fused(K):
         """K iterations of one fused launch: states of the owned rows after each."""
