@@ -171,7 +171,7 @@ class Registration {
     int loop_curvature(Level &L, int niter, int &final_buf);
     // HS over ngpus_ row slabs in this process (ranks.cpp)
     int loop_hs_multi(int s, float alpha, int &final_buf);
-    MultiHS &multi_for(int s);
+    MultiHS &multi_for(int s, float alpha);
     void multi_release();
     int ngpus_ = 1;
     std::vector<std::shared_ptr<MultiHS>> lv_multi_;

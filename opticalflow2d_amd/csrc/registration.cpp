@@ -298,7 +298,8 @@ void Registration::estimate_level(int s) {
         // *Iaux = *Imov; Iaux->warp2d(*motion)
         launch_warp(L.Imov.p, L.cur_motion(), L.Iaux.p, L.dx, L.dy, L.P, st_);
         // HS over several devices: the ranks take their gradients themselves
-        const bool multi = reg_ == 0 && ngpus_ > 1 && L.dy >= ngpus_;
+        // (the slabs need >= 3 j-lines each: coarser levels run on one device)
+        const bool multi = reg_ == 0 && ngpus_ > 1 && L.dy >= 3 * ngpus_ && L.dx >= 3;
         if (!demons && !multi)
             launch_gradients(L.Iref.p, L.Iaux.p, L.dI.p, L.It.p, L.dx, L.dy, L.P, st_);
         L.est[0].zero(st_);  // motion_est starts at zero (reset() at :141 / new Motion)

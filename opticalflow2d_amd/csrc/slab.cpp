@@ -374,6 +374,7 @@ struct SlabExact {
 namespace {
 using of2d::kExEv;
 using of2d::kExR;
+void slab_prepare(of2d_slab *s);
 
 of2d::Field<float2> &exbuf(of2d_slab *s, int k) { return k < 3 ? s->u[k] : s->ex->extra[k - 3]; }
 
@@ -699,6 +700,46 @@ int of2d_slab_set_images(of2d_slab *s, const double *Iref_rows, const double *Im
             of2d::launch_d2f(s->d_stage, s->dimx, rows, dst.p - (long)up3 * s->P, s->P, 0,
                              s->st);
         }
+        slab_prepare(s);
+    });
+}
+}  // extern "C"
+
+namespace of2d {
+void slab_set_images_device(of2d_slab *s, const float *Iref, const float *Iaux, int srcP,
+                            int src_dev) {
+    if (srcP != s->P) throw std::invalid_argument("slab: image pitch differs from the slab's");
+    DeviceScope scope(s->device);
+    const int lo = std::max(s->rb - 3, 0), hi = std::min(s->re + 3, s->dimy);
+    const size_t bytes = sizeof(float) * (size_t)(hi - lo) * s->P;
+    const long dst = (long)(lo - s->rb) * s->P;
+    for (int which = 0; which < 2; which++) {
+        const float *src = (which ? Iaux : Iref) + (size_t)lo * s->P;
+        float *d = (which ? s->Imov : s->Iref).p + dst;
+        if (src_dev == s->device)
+            OF2D_HIP(hipMemcpyAsync(d, src, bytes, hipMemcpyDeviceToDevice, s->st));
+        else
+            OF2D_HIP(hipMemcpyPeerAsync(d, s->device, src, src_dev, bytes, s->st));
+    }
+    slab_prepare(s);
+}
+
+void slab_copy_estimate(of2d_slab *s, float2 *dst, int dst_dev) {
+    DeviceScope scope(s->device);
+    const size_t bytes = sizeof(float2) * (size_t)s->nrows * s->P;
+    if (dst_dev == s->device)
+        OF2D_HIP(hipMemcpyAsync(dst, s->u[s->fin].p, bytes, hipMemcpyDeviceToDevice, s->st));
+    else
+        OF2D_HIP(hipMemcpyPeerAsync(dst, dst_dev, s->u[s->fin].p, s->device, bytes, s->st));
+    OF2D_HIP(hipStreamSynchronize(s->st));
+}
+}  // namespace of2d
+
+namespace {
+// the images are in the slab (rows [rb-3, re+3) clipped): gradients, zeroed
+// motion and the division tests, as every image pair needs them
+void slab_prepare(of2d_slab *s) {
+    {
         // IterativeSolver::set_derivatives(Iref, Iaux = Imov) on the owned rows
         // plus the two halo rows on each side that the fused kernels' first
         // steps need
@@ -727,8 +768,11 @@ int of2d_slab_set_images(of2d_slab *s, const double *Iref_rows, const double *Im
         s->divzero_voted = false;
         OF2D_HIP(hipMemsetAsync(s->d_status, 0, sizeof(unsigned), s->st));
         OF2D_HIP(hipStreamSynchronize(s->st));
-    });
+    }
 }
+}  // namespace
+
+extern "C" {
 
 int of2d_slab_reserve(of2d_slab *s, int niter) {
     if (!s || niter < 0) return OF2D_ERR_INVALID_ARGUMENT;

@@ -87,3 +87,21 @@ def test_config_scale_reference_break_8_ranks(gpu):
     planar = np.concatenate([f[:, :, 0].reshape(-1, order="F"), f[:, :, 1].reshape(-1, order="F")])
     assert hashlib.sha256(planar.tobytes()).hexdigest() == fx["motion_sha256_f32_planar"]
     assert e.view(np.uint32).tolist() == np.asarray(fx["errors"], np.float32).view(np.uint32).tolist()
+
+
+def test_ranks_on_distinct_devices(gpu):
+    """With two or more devices the ranks sit on different ones ((device + r)
+    mod count): the halo copies, the chained Logger's reads of the neighbour's
+    memory and the fp64 mode's sums go between devices (peer access enabled
+    for every pair used).  Four ranks, so some pairs are not neighbours.
+    Skipped on a one-GPU box."""
+    import torch
+    if torch.cuda.device_count() < 2:
+        pytest.skip("one device")
+    ref, mov = S.texture_pair(256, seed=6, ny=200)
+    args = ((256, 200), [300], 0, [0.1], 1, ref, mov)
+    for opts in ({}, {"logger_fp64": 1}, {"fixed_iters": 1}):
+        a = run(*args, **opts)
+        b = run(*args, ngpus=4, **opts)
+        assert a[0] == b[0]
+        assert np.array_equal(a[1], b[1])

@@ -1,0 +1,38 @@
+"""Wall time per iteration of the in-process multi-device HS path
+(of2d_set_option "ngpus", csrc/ranks.cpp) at 4096^2 against one rank: fixed
+iterations and convergence on (the reference-exact Logger).  On a one-GPU box
+every rank runs on device 0, so the figures are the path's overhead at equal
+total work.
+
+    python tools/time_ranks.py [n] [reps]
+"""
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from opticalflow2d_amd import ImageRegistration, set_print_sink  # noqa: E402
+from opticalflow2d_amd import synthetic as S  # noqa: E402
+
+set_print_sink(lambda s: None)
+n = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
+reps = int(sys.argv[2]) if len(sys.argv) > 2 else 3
+ref, mov = S.texture_pair(n)
+for mode, opts, niter in (("fixed 999", {"fixed_iters": 1}, 999), ("convergence", {}, 1000)):
+    base = None
+    for ng in (1, 2, 8):
+        with ImageRegistration((n, n), [niter], 0, 0, [0.1], ngpus=ng, **opts) as r:
+            r.set_images(ref, mov)
+            r.estimate()  # warm-up (allocations, the ranks' threads' first launches)
+            ts = []
+            for _ in range(reps):
+                r.set_images(ref, mov)
+                t0 = time.perf_counter()
+                r.estimate()
+                ts.append(time.perf_counter() - t0)
+            it = r.iterations()[0]
+        t = min(ts)
+        us = t * 1e6 / it
+        base = base or us
+        print(f"{mode:12s} {n}^2 ngpus={ng}: {it} iterations, {t*1e3:.2f} ms "
+              f"({us:.1f} us/iteration, {us / base:.3f}x of ngpus=1)", flush=True)
