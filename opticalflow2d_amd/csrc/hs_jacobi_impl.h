@@ -24,6 +24,12 @@
 #include <type_traits>
 
 
+// the intermediate iterates of the MID triple (read again by the Logger's pass
+// right behind it): default cache policy (0) or non-temporal (1), an A/B knob
+#ifndef OF2D_HS_MID_NT
+#define OF2D_HS_MID_NT 0
+#endif
+
 namespace of2d {
 namespace hs {
 
@@ -789,8 +795,8 @@ __device__ __forceinline__ void jacobi3_body(
         auto stmid = [&](float2 *m, int sp, const Row<2> &v) __attribute__((always_inline)) {
             float2 *dst = m + (long)J(sp) * P + x;
             if (x + 2 <= dimx)
-                *reinterpret_cast<float4 *>(dst) =
-                    make_float4(v.v[0].x, v.v[0].y, v.v[1].x, v.v[1].y);
+                st4<OF2D_HS_MID_NT != 0>(reinterpret_cast<float4 *>(dst),
+                                         make_float4(v.v[0].x, v.v[0].y, v.v[1].x, v.v[1].y));
             else
                 dst[0] = v.v[0];
         };

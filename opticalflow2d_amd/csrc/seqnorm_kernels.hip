@@ -179,9 +179,10 @@ __device__ __forceinline__ sn_fn sn_term_fn(double d, double scale, bool &nan) {
 // is within 1.5 2^-23 of d relative wherever q is a normal float well inside
 // the range (q in [2^-100, 2^120]; exact zeros are exact), so with
 // r = rint(t_est): |t_est - r| < 1/2 - (t 2^-19 + 2^-28) (8x the bound) puts
-// the exactly rounded t strictly inside (r - 1/2, r + 1/2): m = r, no tie.
-// Every other term (near a half-integer, a large term t >= 2^13, tiny or huge
-// components, NaN) takes the exact fp64 sequence; a wave does so only when
+// the exactly rounded t strictly inside (r - 1/2, r + 1/2): m = r < 2^18, no
+// tie.  Every other term (near a half-integer, a large term t >= 2^18 whose
+// margin is gone, tiny or huge components, NaN) takes the exact fp64 sequence;
+// a wave does so only when
 // one of its lanes needs it (a fraction of a percent of waves past the first
 // tiles), so the pass runs on fp32 arithmetic and one sqrt per term.
 struct SnEst {
@@ -209,7 +210,7 @@ __device__ __forceinline__ bool sn_incr_est(const SnEst &v, float scale32, unsig
     const float r = rintf(t);
     const float thr = __builtin_fmaf(t, -0x1p-19f, 0.5f - 0x1p-28f);
     m = (unsigned)r;
-    return v.ok && t < 8192.0f && fabsf(t - r) < thr;
+    return v.ok && fabsf(t - r) < thr;  // never for t >= 2^18 (thr <= 0), inf or NaN
 }
 
 // binade of a double bound, clamped to the float range

@@ -102,6 +102,22 @@ def test_near_half_ulps(gpu, oracle, base):
     check(oracle, cur, prev, dims)
 
 
+@pytest.mark.parametrize("sigma", [2.0, 4.0])
+def test_heavy_tailed_magnitudes(gpu, oracle, sigma):
+    """Lognormal magnitudes: terms from far below half an ulp of the running
+    sum to thousands of ulps (t = d / ulp(S) up to and past 2^13 and 2^18,
+    where the fp32 estimate's margin shrinks and then vanishes), so both the
+    estimate and the exact fp64 sequence decide many terms of every tile."""
+    rng = np.random.default_rng(int(sigma * 10))
+    dims = (2048, 1500)
+    n = dims[0] * dims[1]
+    mag = rng.lognormal(0.0, sigma, n).astype(np.float32)
+    ang = rng.uniform(0, 2 * np.pi, n)
+    prev = np.stack([mag * np.cos(ang), mag * np.sin(ang)], -1).astype(np.float32)
+    cur = prev + (rng.lognormal(-3.0, sigma, (n, 1)) * rng.normal(0, 1, (n, 2))).astype(np.float32)
+    check(oracle, cur, prev, dims)
+
+
 def test_leading_zeros_and_tiny(gpu, oracle):
     rng = np.random.default_rng(11)
     dims = (3000, 200)
