@@ -4,6 +4,9 @@ headline).  One JSON line per configuration:
 
   cfg1  HS 256^2 translated square, 200 iterations, MEX call sequence
         (init -> register -> get -> warp -> close) through the gateway
+  cfg2c HS 4096^2, convergence on (the default: the reference's Logger and
+        break, niter 1000): the texture and procedural pairs of the
+        convergence fixtures, iterations, seconds and us per iteration
   cfg3  Thirion's Demons 4096^2 (params [1, 0.25, 2, 2, 5, Composition])
   cfg4  viscous fluid 8192^2, 3-level pyramid (params [0.25, 0.0])
   cfg5  HS 16384^2 on one GPU (the 1-GPU point of the row-slab config)
@@ -91,6 +94,31 @@ def cfg1():
             "sum_motion": float(m.sum()), "cpu_baseline": {"cores": 1, "kind": "port"}}
 
 
+def cfg2c():
+    """Config 2's grid with the default semantics: the loop runs until the
+    reference's break (ImageRegistrationOpticalFlow.cpp:131-134) on the
+    reference's float Logger norms, from zero motion each time."""
+    from opticalflow2d_amd import ImageRegistration
+    from opticalflow2d_amd import synthetic as S
+    n = 4096
+    out = {"config": f"cfg2c HS {n}^2 convergence on (reference Logger, niter 1000)"}
+    for name, (ref, mov) in (("texture", S.texture_pair(n)),
+                             ("procedural", S.procedural_pair(n, 0, n))):
+        best, it = 1e30, None
+        for rep in range(3):  # the first is the warm-up
+            with ImageRegistration((n, n), [1000], 0, 0, [0.1]) as r:
+                r.set_images(ref, mov)
+                t0 = time.perf_counter()
+                r.estimate()
+                dt = time.perf_counter() - t0
+                it = r.iterations()[0]
+            if rep:
+                best = min(best, dt)
+        out[name] = {"iterations": it, "gpu_wall_s": round(best, 4),
+                     "us_per_iter": round(1e6 * best / it, 1)}
+    return out
+
+
 def cfg3(iters):
     from opticalflow2d_amd import synthetic as S
     n = 4096
@@ -154,7 +182,7 @@ def cfg5(iters):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--configs", default="1,3,4,5")
+    ap.add_argument("--configs", default="1,2c,3,4,5")
     ap.add_argument("--iters", type=int, default=0, help="override iteration counts")
     ap.add_argument("--no-cpu", action="store_true", help="skip the oracle samples (A/B runs)")
     a = ap.parse_args()
@@ -165,6 +193,8 @@ def main():
     for c in a.configs.split(","):
         if c == "1":
             r = cfg1()
+        elif c == "2c":
+            r = cfg2c()
         elif c == "3":
             r = cfg3(a.iters or 100)
         elif c == "4":

@@ -53,6 +53,12 @@ constexpr int kCr = OF2D_DEMONS_CR;
 // results are wrong): 1 no bilinear warp (the tile reads Imov at the pixel),
 // 2 no force (the correction is the gradient), 3 no sigma_fluid convolution,
 // 4 no composition (the update is an addition)
+// A/B knob (round 4): 1 warps the moving image once per iteration into a
+// scratch plane (warp_kernel, 16 B/px) and the fused kernel loads the warped
+// slots instead of warping 1.3 slots per output pixel itself
+#ifndef OF2D_DEMONS_WARP1
+#define OF2D_DEMONS_WARP1 0
+#endif
 #ifndef OF2D_DEMONS_ABL
 #define OF2D_DEMONS_ABL 0
 #endif
@@ -584,7 +590,7 @@ __global__ __launch_bounds__(256) OF2D_DEMONS_FUSED_ATTR void demons_fused_kerne
                 if (xedge) wrap(a[q], b[q]);
                 valid[q] = q0 + q < NW && s < WW * WH;
             }
-            if (OF2D_DEMONS_ABL == 1) {
+            if (OF2D_DEMONS_ABL == 1 || OF2D_DEMONS_WARP1) {  // Imov: the warped image
 #pragma unroll
                 for (int q = 0; q < BW; q++) {
                     in[q] = valid[q] && (unsigned)a[q] < (unsigned)dimx &&
@@ -823,6 +829,11 @@ void launch_demons_update(const float *Iref, const float *Imov, const float2 *u,
         return;
     }
     const dim3 g(gx, conv_grid(dimx, dimy).y);
+    if (OF2D_DEMONS_WARP1) {  // corr is free on this path: the warped plane
+        float *iw = reinterpret_cast<float *>(corr);
+        launch_warp(Imov, u, iw, dimx, dimy, P, st);
+        Imov = iw;
+    }
     float rsx = 0.0f;
     const bool fast = (float)wfull == 1.0f && pow2_reciprocal(sigma_xsq, &rsx);
     auto go = [&](auto kern) {

@@ -457,8 +457,7 @@ __device__ __forceinline__ void sn_wave_pass(const SnJobs &J, unsigned N, int di
                     anybad |= bad;
                 }
                 if (lane < nc[i][n]) ws.T[(2 * (size_t)b + n) * kSnCand + lane] = tv;
-                // a tie or NaN among the entries: the walk will want segment entries
-                if (anybad) hh |= kHdrSegReq;
+                (void)anybad;  // a tie or NaN: the entry fails in the walk, which resolves it
             }
             const double a = wave_reduce((double)fs[i][n], [](double p, double x) { return p + x; });
             const unsigned long long zm = sn_ballot(zv[i][n]);
@@ -614,8 +613,8 @@ void seqnorm_tables(unsigned N, int dimx, int P, unsigned nt, SnJobs J) {
 // float sum can be in across each tile: the prefix times the last call's
 // drift of the float sum from it (use_prof; 1/64 either side), or the prefix
 // alone (1/16 either side).  A tile whose entries miss one is listed for new
-// tile entries (pending); a tile across which the sum may change binade is
-// listed for segment entries (the walk resolves it).  Three launches over
+// tile entries (pending); the walk makes the segment entries of the tiles it
+// resolves itself (sn_help).  Three launches over
 // every tile: (1) the last call's drift at each tile (read before this call
 // rewrites Pp) and the sums of blocks of kSnChk tiles, (2) one block scans the
 // block sums, (3) each block scans its tiles from its offset and checks them.
@@ -752,9 +751,8 @@ __global__ __launch_bounds__(kSnChk) void seqnorm_check(unsigned nt, SnJobs J) {
             const int wl = hdr_elo(want), wn = hdr_nc(want), hl = hdr_elo(h[n]), hn = hdr_nc(h[n]);
             unsigned hh = h[n];
             if (wn > 0 && (wl < hl || wl + wn > hl + hn)) hh = want | kHdrPending;
-            if (wn > 1 || b == 0) hh |= kHdrSegReq;
             if (hh != h[n]) ws.H[2 * (size_t)b + n] = hh;
-            listed |= (hh & (kHdrPending | kHdrSegReq)) != 0;
+            listed |= (hh & kHdrPending) != 0;
         }
         ws.Pp[(size_t)n * (nt + 1) + b] = Pb[n];
     }
@@ -911,54 +909,120 @@ __device__ float sn_raw_segment(SnSegTerms tv, int which, float S) {
     return S;
 }
 
-// The segment entries of tile b for binade e, made by the walk's wave when
-// the tables hold none for it (a missed binade): lane s receives segment s's,
-// for the segments from sfrom (rounded down to 8) on.  Coalesced segments,
-// kSnNowBatch of them in flight: ~18 us for a whole tile.
-constexpr int kSnNowBatch = 32;
-__device__ unsigned sn_segments_now(const float2 *__restrict__ cur, const float2 *__restrict__ prev,
-                                    int which, unsigned b, int sfrom, int e, unsigned N, int dimx,
-                                    int P) {
+// Segment entries made on demand (round 4).  A walk block is the walker wave
+// and kSnHelpers helper waves; at a tile whose segment entries the
+// workspace lacks for S's binade (a crossing, a tie, a missed prediction) the
+// walker posts a request in LDS and the eight waves make the entries of the
+// tile's segments from sfrom on for binades e and e + 1 (a crossing goes up
+// one binade), segment s by wave s mod 8: ~3 us, against ~18 us for the
+// walker alone and ~1.1 us per segment stepped raw.  The check no longer
+// lists tiles for segment entries ahead of the walk.
+constexpr int kSnHelpers = 7;
+constexpr int kSnWalkWaves = 1 + kSnHelpers;
+constexpr unsigned kSnHelpExit = 0xffffffffu;
+struct SnHelp {
+    unsigned seq, done;  // request number (the walker's), helpers finished with it
+    unsigned b;
+    int e, sfrom;
+    unsigned g[2][kSnSegs];  // entries for binades e, e + 1
+};
+
+// wave `part`'s share of the request: segments s = sfrom + part + 8k
+__device__ void sn_help_part(const float2 *__restrict__ cur, const float2 *__restrict__ prev,
+                             int which, unsigned b, int sfrom, int e, unsigned N, int dimx, int P,
+                             int part, SnHelp &hp) {
     const int lane = threadIdx.x & 63;
-    const double scale = sn_scale(e);
-    const float scale32 = sn_scale32(e);
-    unsigned mine = 0;
-    const int sb = sfrom & ~7;
-    unsigned L = b * (unsigned)kSnTile + 64u * sb + lane;
-    unsigned j = L / (unsigned)dimx, i = L - j * (unsigned)dimx;
-    for (int s0 = sb; s0 < kSnSegs; s0 += kSnNowBatch) {
-        float2 cv[kSnNowBatch], pv[kSnNowBatch];
+    constexpr int kMax = kSnSegs / kSnWalkWaves;
+    SnSegTerms tv[kMax];
 #pragma unroll
-        for (int k = 0; k < kSnNowBatch; k++) {
-            cv[k] = pv[k] = make_float2(0.0f, 0.0f);
-            if (s0 + k < kSnSegs && L < N) {
-                const size_t off = (size_t)j * (size_t)P + i;
-                if (!which) cv[k] = cur[off];
-                pv[k] = prev[off];
-            }
-            L += 64u;
-            i += 64u;
-            while (i >= (unsigned)dimx) {
-                i -= (unsigned)dimx;
-                j++;
-            }
+    for (int k = 0; k < kMax; k++) {
+        const int sg = sfrom + part + kSnWalkWaves * k;
+        tv[k] = SnSegTerms{make_float2(0.0f, 0.0f), make_float2(0.0f, 0.0f)};
+        if (sg < kSnSegs) tv[k] = sn_seg_load(cur, prev, which, b, sg, N, dimx, P);
+    }
+    const bool top = e >= 127;  // no binade above: its entries force raw steps
+    const float sc0 = sn_scale32(e), sc1 = top ? 0.0f : sn_scale32(e + 1);
+#pragma unroll
+    for (int k = 0; k < kMax; k++) {
+        const int sg = sfrom + part + kSnWalkWaves * k;
+        if (sg >= kSnSegs) break;
+        // Field::operator- (Field.tpp:305-334) for |cur - prev|
+        const float vx = which ? tv[k].p.x : tv[k].c.x - tv[k].p.x;
+        const float vy = which ? tv[k].p.y : tv[k].c.y - tv[k].p.y;
+        const SnEst v = sn_est(vx, vy);
+        unsigned m0, m1;
+        bool unc = !sn_incr_est(v, sc0, m0);
+        unc |= !sn_incr_est(v, sc1, m1);
+        bool bad0 = false, bad1 = false;
+        if (sn_ballot(unc)) {
+            const double dd = sn_mag(vx, vy);
+            m0 = sn_incr(dd, sn_scale(e), bad0);
+            m1 = top ? 0u : sn_incr(dd, sn_scale(e + 1), bad1);
         }
-#pragma unroll
-        for (int k = 0; k < kSnNowBatch; k++) {
-            if (s0 + k >= kSnSegs) break;
-            // Field::operator- (Field.tpp:305-334) for |cur - prev|
-            const float vx = which ? pv[k].x : cv[k].x - pv[k].x;
-            const float vy = which ? pv[k].y : cv[k].y - pv[k].y;
-            bool bad = false;
-            unsigned m;
-            const bool unc = !sn_incr_est(sn_est(vx, vy), scale32, m);
-            if (sn_ballot(unc) && unc) m = sn_incr(sn_mag(vx, vy), scale, bad);
-            const unsigned t = wave_sum(m);
-            const unsigned g = (t < kSnSat ? t : kSnSat) | (sn_ballot(bad) ? kSnBad : 0u);
-            if (lane == s0 + k) mine = g;
+        const unsigned t0 = wave_sum(m0), t1 = wave_sum(m1);
+        const bool b0 = sn_ballot(bad0) != 0ull, b1 = sn_ballot(bad1) != 0ull;
+        if (lane == 0) {
+            hp.g[0][sg] = (t0 < kSnSat ? t0 : kSnSat) | (b0 ? kSnBad : 0u);
+            hp.g[1][sg] = top ? (kSnSat | kSnBad) : (t1 < kSnSat ? t1 : kSnSat) | (b1 ? kSnBad : 0u);
         }
     }
-    return mine;
+}
+
+// the walker's request: entries of tile b's segments from sfrom for binades
+// e and e + 1 into g0, g1 (lane s: segment s)
+__device__ void sn_help(SnHelp &hp, unsigned &seq, const float2 *__restrict__ cur,
+                        const float2 *__restrict__ prev, int which, unsigned b, int sfrom, int e,
+                        unsigned N, int dimx, int P, unsigned &g0, unsigned &g1) {
+    const int lane = threadIdx.x & 63;
+    if (lane == 0) {
+        hp.b = b;
+        hp.e = e;
+        hp.sfrom = sfrom;
+        hp.done = 0u;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    seq++;
+    if (lane == 0) __hip_atomic_store(&hp.seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    sn_help_part(cur, prev, which, b, sfrom, e, N, dimx, P, 0, hp);
+    const long long t0 = wall_clock64();
+    bool late = false;
+    while (__hip_atomic_load(&hp.done, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) <
+           (unsigned)kSnHelpers) {
+        __builtin_amdgcn_s_sleep(1);
+        if (wall_clock64() - t0 > 100000000ll) {  // 1 s: the helpers are gone, do it alone
+            late = true;
+            break;
+        }
+    }
+    if (late)
+        for (int part = 1; part < kSnWalkWaves; part++)
+            sn_help_part(cur, prev, which, b, sfrom, e, N, dimx, P, part, hp);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    g0 = lane >= sfrom ? hp.g[0][lane] : 0u;
+    g1 = lane >= sfrom ? hp.g[1][lane] : 0u;
+}
+
+// a helper wave: serve the walker's requests until it posts kSnHelpExit
+__device__ void sn_helper(SnHelp &hp, const float2 *__restrict__ cur,
+                          const float2 *__restrict__ prev, int which, unsigned N, int dimx, int P,
+                          int part) {
+    const int lane = threadIdx.x & 63;
+    unsigned my = 0;
+    long long t0 = wall_clock64();
+    for (;;) {
+        const unsigned sq = __hip_atomic_load(&hp.seq, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (sq == kSnHelpExit) return;
+        if (sq == my) {
+            __builtin_amdgcn_s_sleep(2);
+            if (wall_clock64() - t0 > 3000000000ll) return;  // 30 s idle: the walker is gone
+            continue;
+        }
+        my = sq;
+        sn_help_part(cur, prev, which, hp.b, hp.sfrom, hp.e, N, dimx, P, part, hp);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        if (lane == 0) __hip_atomic_fetch_add(&hp.done, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        t0 = wall_clock64();
+    }
 }
 
 // Tile b from the exact running sum S: its segment entries where one covers
@@ -967,7 +1031,8 @@ __device__ unsigned sn_segments_now(const float2 *__restrict__ cur, const float2
 // the low sum).
 __device__ float sn_resolve(const float2 *__restrict__ cur, const float2 *__restrict__ prev,
                             int which, unsigned b, unsigned N, int dimx, int P, float S,
-                            unsigned h, const SnWs &ws, int &raw, int &made) {
+                            unsigned h, const SnWs &ws, int &raw, int &made, SnHelp &hp,
+                            unsigned &seq) {
     const int lane = threadIdx.x & 63;
     const int nc = (h & kHdrSeg) ? hdr_nc(h) : 0, elo = hdr_elo(h);
     const unsigned long long zm = ws.Z[2 * (size_t)b + which];
@@ -975,34 +1040,30 @@ __device__ float sn_resolve(const float2 *__restrict__ cur, const float2 *__rest
 #pragma unroll
     for (int c = 0; c < kSnCand; c++) g[c] = c < nc ? ws.G[g_index(b, which, c, lane)] : 0u;
     int s0 = 0;
-    int enow = kSnLow;  // the binade of gnow
-    int rawhere = 0;
-    int made_at = -kSnSegs;  // segment at which gnow was made
+    int enow = kSnLow;       // gnow0 / gnow1: the made entries of binades enow, enow + 1
+    int made_at = -kSnSegs;  // segment at which they were made
     int pf_seg = -1;         // segment whose terms pf holds
     SnSegTerms pf{};
-    bool no_more = false;    // a made set of entries served < 16 segments: step raw
-    unsigned gnow = 0;
+    bool no_more = false;    // made entries served < 4 segments: step raw
+    unsigned gnow0 = 0, gnow1 = 0;
     while (s0 < kSnSegs) {
         const int e = sn_region(S);
         const int c = e - elo;
         const bool table = c >= 0 && c < nc;
-        // the tile's own entries once raw steps have not brought S back into
-        // the tables' binades (~0.3 us per segment against ~1.1 us per raw one,
-        // ~18 us to make them: worth it only while S stays in the binade, so
-        // not again in a tile where S left made entries within 16 segments,
-        // e.g. a sum still growing through many binades; 256^2 config 1)
-        if (e != kSnLow && e != kSnNonfinite && !table && e != enow && enow != kSnLow &&
-            s0 - made_at < 16)
-            no_more = true;
-        if (e != kSnLow && e != kSnNonfinite && !table && e != enow && rawhere >= 6 &&
-            kSnSegs - s0 > 16 && !no_more) {
-            gnow = sn_segments_now(cur, prev, which, b, s0, e, N, dimx, P);
+        const bool valid = e != kSnLow && e != kSnNonfinite;
+        const bool mine = enow != kSnLow && (e == enow || e == enow + 1);
+        // entries of the binade pair S is in, made by the block's waves (not
+        // again in a tile where S left them within 4 segments: a sum still
+        // climbing through many binades, e.g. the first tiles; 256^2 config 1)
+        if (valid && !table && !mine && enow != kSnLow && s0 - made_at < 4) no_more = true;
+        if (valid && !table && !mine && kSnSegs - s0 > 2 && !no_more) {
+            sn_help(hp, seq, cur, prev, which, b, s0, e, N, dimx, P, gnow0, gnow1);
             enow = e;
             made_at = s0;
             made++;
         }
-        if (e != kSnLow && e != kSnNonfinite && (table || e == enow)) {
-            unsigned gc = table ? g[0] : gnow;
+        if (valid && (table || e == enow || e == enow + 1)) {
+            unsigned gc = table ? g[0] : (e == enow ? gnow0 : gnow1);
 #pragma unroll
             for (int k = 1; k < kSnCand; k++)
                 if (table && c == k) gc = g[k];
@@ -1031,7 +1092,6 @@ __device__ float sn_resolve(const float2 *__restrict__ cur, const float2 *__rest
         }
         S = sn_raw_segment(tv, which, S);
         raw++;
-        rawhere++;
         s0++;
     }
     return S;
@@ -1044,13 +1104,25 @@ constexpr int kSnAhead = 8;  // windows loaded per step: the next step's loads h
 // entry does not apply.  Writes every tile's start sum into the profile.
 // dbg: resolves (per norm), raw segments (per norm), listed tiles, walk and
 // resolve clocks, tiles given the walk's own segment entries (per norm).
-__global__ __launch_bounds__(64) void seqnorm_walk(unsigned N, int dimx, int P, unsigned nt,
-                                                   SnJobs J) {
+__global__ __launch_bounds__(64 * kSnWalkWaves) void seqnorm_walk(unsigned N, int dimx, int P,
+                                                                   unsigned nt, SnJobs J) {
     const int job = blockIdx.x >> 1;
     const int n = blockIdx.x & 1;  // 0: |cur - prev|, 1: |prev|
-    const int lane = threadIdx.x;
+    const int lane = threadIdx.x & 63;
     const float2 *__restrict__ prev = J.u[job];
     const float2 *__restrict__ cur = J.u[job + 1];
+    __shared__ SnHelp hp;
+    if (threadIdx.x == 0) {
+        hp.seq = 0u;
+        hp.done = 0u;
+    }
+    __syncthreads();  // the only barrier: from here wave 0 walks, the others help
+    const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / 64));
+    if (wv > 0) {
+        sn_helper(hp, cur, prev, n, N, dimx, P, wv);
+        return;
+    }
+    unsigned seq = 0;
     const SnWs &ws = J.ws[job];
     const float *__restrict__ s_in = J.s_in[job];
     float *__restrict__ out = J.out[job];
@@ -1129,7 +1201,8 @@ __global__ __launch_bounds__(64) void seqnorm_walk(unsigned N, int dimx, int P, 
                 }
                 if (!low) S = sn_make(e, M + lane_at(excl, q));
                 const long long r0 = wall_clock64();
-                S = sn_resolve(cur, prev, n, b0 + q, N, dimx, P, S, lane_at(h, q), ws, raw, made);
+                S = sn_resolve(cur, prev, n, b0 + q, N, dimx, P, S, lane_at(h, q), ws, raw, made,
+                               hp, seq);
                 cres += wall_clock64() - r0;
                 resolves++;
                 start = q + 1;
@@ -1141,7 +1214,7 @@ __global__ __launch_bounds__(64) void seqnorm_walk(unsigned N, int dimx, int P, 
         prof[nt] = S;
         ws.tot[2 * n + 1] = ws.tot[2 * n];
         ws.tot[2 * n] = S;
-        ws.miss[n] = (unsigned)(raw + 32 * made);  // as raw segments
+        ws.miss[n] = (unsigned)raw;  // segments its resolves stepped term by term
         out[n] = S;
         if (dbg) {
             dbg[n] = resolves;
@@ -1152,6 +1225,8 @@ __global__ __launch_bounds__(64) void seqnorm_walk(unsigned N, int dimx, int P, 
             if (n == 0) dbg[7] = (int)cres;
             dbg[8 + n] = made;
         }
+        // the helpers may go
+        __hip_atomic_store(&hp.seq, kSnHelpExit, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
 }
 
@@ -1245,7 +1320,7 @@ void launch_seqnorm_refine(const SeqnormBatch &B, int dimx, int dimy, int P, hip
 void launch_seqnorm_walk(const SeqnormBatch &B, int dimx, int dimy, int P, hipStream_t st) {
     const unsigned nt = check_geometry(dimx, dimy, P);
     const unsigned N = (unsigned)((size_t)dimx * dimy);
-    hipLaunchKernelGGL(seqnorm_walk, dim3(2 * B.K), dim3(64), 0, st, N, dimx, P, nt,
+    hipLaunchKernelGGL(seqnorm_walk, dim3(2 * B.K), dim3(64 * kSnWalkWaves), 0, st, N, dimx, P, nt,
                        jobs_of(B, nt));
     OF2D_HIP(hipGetLastError());
 }
