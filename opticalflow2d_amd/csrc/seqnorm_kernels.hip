@@ -293,15 +293,18 @@ struct SnJobs {
     int *dbg[kSnMaxJobs];
 };
 
-// segments in flight per wave: a ring of kSnRing segment buffers, each
-// reloaded with the segment kSnRing ahead right after its own is consumed,
-// so a load has kSnRing - 1 segments' arithmetic to arrive (the pass: 4 x
-// (K + 1) float2; the fix, one pair: 8 x 2)
+// segments in flight per wave: a ring of D segment buffers, each reloaded
+// with the segment D ahead right after its own is consumed, so a load has
+// D - 1 segments' arithmetic to arrive (the pass: 2-4 x (K + 1) float2; the
+// fix, one pair: 8 x 2)
 #ifndef OF2D_SN_ABL
 #define OF2D_SN_ABL 0  // timing ablations of the pass (results wrong when set)
 #endif
+// (K = 3: a ring of 2 measured 119 us per three-update pass against 144 for 4,
+// whose 155 VGPRs leave 3 waves per SIMD, and 93 for the loads alone;
+// profiles/r04g_sn_ring_ab.log)
 #ifndef OF2D_SN_RING3
-#define OF2D_SN_RING3 4
+#define OF2D_SN_RING3 2
 #endif
 template <int K>
 constexpr int sn_ring() { return K == 1 ? 8 : (K == 2 ? 4 : OF2D_SN_RING3); }
