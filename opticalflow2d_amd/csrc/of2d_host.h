@@ -193,11 +193,12 @@ class Registration {
     void seqnorm(const Level &L, const float2 *cur, const float2 *prev, int t);
     // run_chunked with the reference's float norms: every iterate in memory,
     // groups of up to three iterations (a step3m triple or single steps) into
-    // a ring of twelve buffers; each group's norms as one batch, its tables on
-    // sn_st_ and its walk on wk_st_, workspace set g & 1 (three workspaces)
+    // a ring of twelve buffers; each group's norms as one batch, its pass on
+    // sn_st_ and its walk on wk_st_[g & 1], workspace set g & 1 (three
+    // workspaces): the walks of consecutive groups run at once
     int run_chunked_exact(Level &L, int niter, int nb, const StepFn &step, int &final_buf,
                           const StepFn3M &step3m = nullptr);
-    hipStream_t sn_st_ = nullptr, wk_st_ = nullptr;
+    hipStream_t sn_st_ = nullptr, wk_st_[2] = {};
     static constexpr int kExactEv = 16;  // event ring per group (> 4 groups in flight)
     static constexpr int kSeqWs = 6;     // two sets of three
     hipEvent_t ev_step_[kExactEv] = {}, ev_fix_[kExactEv] = {}, ev_walk_[kExactEv] = {};

@@ -150,7 +150,8 @@ Registration::~Registration() {
     if (ev_fork_) (void)hipEventDestroy(ev_fork_);
     if (ev_join_) (void)hipEventDestroy(ev_join_);
     if (sn_st_) (void)hipStreamDestroy(sn_st_);
-    if (wk_st_) (void)hipStreamDestroy(wk_st_);
+    for (hipStream_t w : wk_st_)
+        if (w) (void)hipStreamDestroy(w);
     for (int k = 0; k < kExactEv; k++) {
         if (ev_step_[k]) (void)hipEventDestroy(ev_step_[k]);
         if (ev_fix_[k]) (void)hipEventDestroy(ev_fix_[k]);
@@ -192,7 +193,7 @@ void Registration::ensure_device() {
     OF2D_HIP(hipGetDevice(&home_));
     OF2D_HIP(hipStreamCreateWithFlags(&st_, hipStreamNonBlocking));
     OF2D_HIP(hipStreamCreateWithFlags(&sn_st_, hipStreamNonBlocking));
-    OF2D_HIP(hipStreamCreateWithFlags(&wk_st_, hipStreamNonBlocking));
+    for (hipStream_t &w : wk_st_) OF2D_HIP(hipStreamCreateWithFlags(&w, hipStreamNonBlocking));
     for (int k = 0; k < kExactEv; k++) {
         OF2D_HIP(hipEventCreateWithFlags(&ev_step_[k], hipEventDisableTiming));
         OF2D_HIP(hipEventCreateWithFlags(&ev_fix_[k], hipEventDisableTiming));
@@ -335,11 +336,13 @@ void Registration::seqnorm(const Level &L, const float2 *cur, const float2 *prev
 // steps) into a ring of the R buffers other than the chunk's start buffer a
 // (kept for a replay).  The norms of a group run behind its steps as one
 // batch (seqnorm_kernels.hip: pair i = iterates t + i - 1, t + i): the
-// bandwidth passes (tables, check, fix) on sn_st_ and the latency-bound walk
-// on wk_st_, so group g's walk overlaps group g + 1's steps and tables.  Group
-// g works on workspace set g & 1, whose last walk (group g - 2) left the
-// profile that predicts it.  Iterate m's buffer is read by the walks of the
-// groups of m and m + 1; iterate m + R rewrites it after both.
+// bandwidth pass on sn_st_ and the latency-bound walk on wk_st_[g & 1], so
+// group g's walk overlaps group g + 1's steps, pass and walk.  Group g works
+// on workspace set g & 1, whose last walk (group g - 2) left the profile that
+// predicts it; the walk resolves the tiles the prediction missed itself, so
+// the check and fix run only for pairs without a profile (a loop's first
+// groups).  Iterate m's buffer is read by the walks of the groups of m and
+// m + 1; iterate m + R rewrites it after both.
 int Registration::run_chunked_exact(Level &L, int niter, int nb, const StepFn &step,
                                     int &final_buf, const StepFn3M &step3m) {
     const double npx = (double)L.dx * L.dy;
@@ -366,6 +369,7 @@ int Registration::run_chunked_exact(Level &L, int niter, int nb, const StepFn &s
     int a = 0, k0 = 0, g = 0;
     while (k0 < niter) {
         const int C = std::min(chunk_, niter - k0);
+        const int g0 = g;  // the chunk's first group
         for (int t = 0; t < C; g++) {
             const int k = std::min(3, C - t);
             for (int m = t; m < t + k; m++) group_of[m] = g;
@@ -383,11 +387,13 @@ int Registration::run_chunked_exact(Level &L, int niter, int nb, const StepFn &s
             SeqnormBatch B;
             B.K = k;
             B.u[0] = L.est[src_of(a, t)].p;
+            bool fresh = false;  // a pair without a profile: the check and fix predict it
             for (int i = 0; i < k; i++) {
                 const int w = 3 * (g & 1) + i;
                 B.u[i + 1] = L.est[ring(a, t + i)].p;
                 B.ws[i] = d_seqws_[w].p;
                 B.use_profile[i] = walked[w] && seq_dx_[w] == L.dx && seq_dy_[w] == L.dy;
+                fresh |= !B.use_profile[i];
                 seq_dx_[w] = L.dx;
                 seq_dy_[w] = L.dy;
                 walked[w] = true;
@@ -398,14 +404,16 @@ int Registration::run_chunked_exact(Level &L, int niter, int nb, const StepFn &s
             // workspace set g & 1: group g - 2's walk has read it and left its profile
             if (g >= 2) OF2D_HIP(hipStreamWaitEvent(sn_st_, ev(ev_walk_, g - 2), 0));
             launch_seqnorm_pass(B, L.dx, L.dy, L.P, sn_st_);
-            launch_seqnorm_refine(B, L.dx, L.dy, L.P, sn_st_);
+            if (fresh) launch_seqnorm_refine(B, L.dx, L.dy, L.P, sn_st_);
             OF2D_HIP(hipEventRecord(ev(ev_fix_, g), sn_st_));
-            OF2D_HIP(hipStreamWaitEvent(wk_st_, ev(ev_fix_, g), 0));
-            launch_seqnorm_walk(B, L.dx, L.dy, L.P, wk_st_);
-            OF2D_HIP(hipEventRecord(ev(ev_walk_, g), wk_st_));
+            hipStream_t wk = wk_st_[g & 1];
+            OF2D_HIP(hipStreamWaitEvent(wk, ev(ev_fix_, g), 0));
+            launch_seqnorm_walk(B, L.dx, L.dy, L.P, wk);
+            OF2D_HIP(hipEventRecord(ev(ev_walk_, g), wk));
             t += k;
         }
-        OF2D_HIP(hipStreamWaitEvent(st_, ev(ev_walk_, g - 1), 0));  // walks run in order
+        // the last walk of each walk stream
+        for (int q = std::max(g - 2, g0); q < g; q++) OF2D_HIP(hipStreamWaitEvent(st_, ev(ev_walk_, q), 0));
         OF2D_HIP(hipMemcpyAsync(hs_.flt, d_seq_.p, sizeof(float) * 2 * C, hipMemcpyDeviceToHost,
                                 st_));
         check_status();  // synchronises st_ (and with it every norm of the chunk)

@@ -1182,7 +1182,9 @@ __global__ __launch_bounds__(64 * kSnWalkWaves) void seqnorm_walk(unsigned N, in
                 bool fail = false;
                 if (lane >= start && !(h & kHdrZero)) {
                     const int c = e - hdr_elo(h);
-                    if (low || c < 0 || c >= hdr_nc(h)) {
+                    // (pending: the pass left this tile's entries to a fix
+                    // that did not run; the resolve takes it)
+                    if (low || c < 0 || c >= hdr_nc(h) || (h & kHdrPending)) {
                         fail = true;
                     } else {
                         const unsigned w = lt[k][c][lane];
@@ -1406,7 +1408,10 @@ void launch_seqnorm_walk(const float2 *cur, const float2 *prev, int dimx, int di
 
 void launch_seqnorm(const float2 *cur, const float2 *prev, int dimx, int dimy, int P, void *ws,
                     bool use_profile, float *out, int *dbg, hipStream_t st) {
-    launch_seqnorm_tables(cur, prev, dimx, dimy, P, ws, use_profile, st);
+    // with a profile the walk resolves the tiles it mispredicted: no check / fix
+    const SeqnormBatch B = one(cur, prev, ws, use_profile);
+    launch_seqnorm_pass(B, dimx, dimy, P, st);
+    if (!use_profile) launch_seqnorm_refine(B, dimx, dimy, P, st);
     launch_seqnorm_walk(cur, prev, dimx, dimy, P, ws, nullptr, out, dbg, st);
 }
 
