@@ -848,32 +848,37 @@ __device__ __forceinline__ unsigned long long lanes_from(int k) {
     return k >= 64 ? 0ull : (~0ull << k);
 }
 
-// The lane's term of segment `seg` of tile `b`: its cur and prev (0 past the
-// grid), loaded ahead of the raw segment that uses them
+// The lane's term of segment `seg` of tile `b`: the vector whose magnitude it
+// is (cur - prev, Field::operator- (Field.tpp:305-334), or prev; 0 past the
+// grid), loaded ahead of the raw segment that uses it
 struct SnSegTerms {
-    float2 c, p;
+    float2 v;
 };
 __device__ __forceinline__ SnSegTerms sn_seg_load(const float2 *__restrict__ cur,
                                                   const float2 *__restrict__ prev, int which,
                                                   unsigned b, int seg, unsigned N, int dimx,
                                                   int P) {
     const unsigned L = b * (unsigned)kSnTile + 64u * seg + (threadIdx.x & 63);
-    SnSegTerms t{make_float2(0.0f, 0.0f), make_float2(0.0f, 0.0f)};
+    SnSegTerms t{make_float2(0.0f, 0.0f)};
     if (L < N) {
         const unsigned j = L / (unsigned)dimx, i = L - j * (unsigned)dimx;
         const size_t off = (size_t)j * (size_t)P + i;
-        if (!which) t.c = cur[off];
-        t.p = prev[off];
+        const float2 p = prev[off];
+        if (which) {
+            t.v = p;
+        } else {
+            const float2 c = cur[off];
+            t.v = make_float2(c.x - p.x, c.y - p.y);
+        }
     }
     return t;
 }
 
-// The 64 terms of a segment (lane = term, `tv` its cur / prev) from the exact
+// The 64 terms of a segment (lane = term, `tv` its vector) from the exact
 // running sum S, term by term where the binade changes.
-__device__ float sn_raw_segment(SnSegTerms tv, int which, float S) {
+__device__ float sn_raw_segment(SnSegTerms tv, float S) {
     const int lane = threadIdx.x & 63;
-    // Field::operator- (Field.tpp:305-334) for |cur - prev|
-    const double dv = which ? sn_mag(tv.p.x, tv.p.y) : sn_mag(tv.c.x - tv.p.x, tv.c.y - tv.p.y);
+    const double dv = sn_mag(tv.v.x, tv.v.y);
     int pos = 0;
     while (pos < 64) {
         const int e = sn_region(S);
@@ -928,6 +933,7 @@ struct SnHelp {
     unsigned b;
     int e, sfrom;
     unsigned g[2][kSnSegs];  // entries for binades e, e + 1
+    float2 v[kSnSegs][64];   // the request's terms (segments >= sfrom; 32 KB)
 };
 
 // wave `part`'s share of the request: segments s = sfrom + part + 8k
@@ -940,8 +946,14 @@ __device__ void sn_help_part(const float2 *__restrict__ cur, const float2 *__res
 #pragma unroll
     for (int k = 0; k < kMax; k++) {
         const int sg = sfrom + part + kSnWalkWaves * k;
-        tv[k] = SnSegTerms{make_float2(0.0f, 0.0f), make_float2(0.0f, 0.0f)};
+        tv[k] = SnSegTerms{make_float2(0.0f, 0.0f)};
         if (sg < kSnSegs) tv[k] = sn_seg_load(cur, prev, which, b, sg, N, dimx, P);
+    }
+    // the terms stay in LDS for the walker's raw steps in this tile
+#pragma unroll
+    for (int k = 0; k < kMax; k++) {
+        const int sg = sfrom + part + kSnWalkWaves * k;
+        if (sg < kSnSegs) hp.v[sg][lane] = tv[k].v;
     }
     const bool top = e >= 127;  // no binade above: its entries force raw steps
     const float sc0 = sn_scale32(e), sc1 = top ? 0.0f : sn_scale32(e + 1);
@@ -949,9 +961,7 @@ __device__ void sn_help_part(const float2 *__restrict__ cur, const float2 *__res
     for (int k = 0; k < kMax; k++) {
         const int sg = sfrom + part + kSnWalkWaves * k;
         if (sg >= kSnSegs) break;
-        // Field::operator- (Field.tpp:305-334) for |cur - prev|
-        const float vx = which ? tv[k].p.x : tv[k].c.x - tv[k].p.x;
-        const float vy = which ? tv[k].p.y : tv[k].c.y - tv[k].p.y;
+        const float vx = tv[k].v.x, vy = tv[k].v.y;
         const SnEst v = sn_est(vx, vy);
         unsigned m0, m1;
         bool unc = !sn_incr_est(v, sc0, m0);
@@ -1085,15 +1095,20 @@ __device__ float sn_resolve(const float2 *__restrict__ cur, const float2 *__rest
             if (!nz) return S;  // every remaining term is 0
             s0 = first_lane(nz);
         }
-        // this segment's terms (prefetched when the last raw one was s0 - 1),
-        // and the next one's loads in flight behind its steps
-        const SnSegTerms tv =
-            pf_seg == s0 ? pf : sn_seg_load(cur, prev, which, b, s0, N, dimx, P);
-        if (s0 + 1 < kSnSegs) {
-            pf = sn_seg_load(cur, prev, which, b, s0 + 1, N, dimx, P);
-            pf_seg = s0 + 1;
+        // this segment's terms: in LDS from the last request, or loaded
+        // (prefetched when the last raw one was s0 - 1, the next one's loads
+        // in flight behind its steps)
+        SnSegTerms tv;
+        if (enow != kSnLow && s0 >= made_at) {
+            tv.v = hp.v[s0][lane];
+        } else {
+            tv = pf_seg == s0 ? pf : sn_seg_load(cur, prev, which, b, s0, N, dimx, P);
+            if (s0 + 1 < kSnSegs) {
+                pf = sn_seg_load(cur, prev, which, b, s0 + 1, N, dimx, P);
+                pf_seg = s0 + 1;
+            }
         }
-        S = sn_raw_segment(tv, which, S);
+        S = sn_raw_segment(tv, S);
         raw++;
         s0++;
     }
