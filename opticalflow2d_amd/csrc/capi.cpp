@@ -215,18 +215,16 @@ int of2d_motion_norms_chain(const float *u, int dimx, int dimy, int niter, int b
             of2d::SeqnormBatch B;
             B.K = std::min(batch, niter - t);
             for (int i = 0; i <= B.K; i++) B.u[i] = f[(size_t)t + i].p;
-            bool fresh = false;  // as the registration: check / fix only without a profile
             for (int i = 0; i < B.K; i++) {
                 const int w = 3 * (g & 1) + i;
                 B.ws[i] = ws[w].p;
                 B.use_profile[i] = used[w];
-                fresh |= !used[w];
                 used[w] = true;
                 B.out[i] = out.p + 2 * (size_t)(t + i);
                 B.dbg[i] = dbg.p + kSnDbg * (size_t)(t + i);
             }
             of2d::launch_seqnorm_pass(B, dimx, dimy, f[0].P, nullptr);
-            if (fresh) of2d::launch_seqnorm_refine(B, dimx, dimy, f[0].P, nullptr);
+            of2d::launch_seqnorm_refine(B, dimx, dimy, f[0].P, nullptr);
             of2d::launch_seqnorm_walk(B, dimx, dimy, f[0].P, nullptr);
             t += B.K;
         }

@@ -340,8 +340,8 @@ void Registration::seqnorm(const Level &L, const float2 *cur, const float2 *prev
 // group g's walk overlaps group g + 1's steps, pass and walk.  Group g works
 // on workspace set g & 1, whose last walk (group g - 2) left the profile that
 // predicts it; the walk resolves the tiles the prediction missed itself, so
-// the check and fix run only for pairs without a profile (a loop's first
-// groups).  Iterate m's buffer is read by the walks of the groups of m and
+// the check and fix do work only for norms without a usable profile (a
+// loop's first groups, or after a walk that resolved many tiles).  Iterate m's buffer is read by the walks of the groups of m and
 // m + 1; iterate m + R rewrites it after both.
 int Registration::run_chunked_exact(Level &L, int niter, int nb, const StepFn &step,
                                     int &final_buf, const StepFn3M &step3m) {
@@ -387,13 +387,11 @@ int Registration::run_chunked_exact(Level &L, int niter, int nb, const StepFn &s
             SeqnormBatch B;
             B.K = k;
             B.u[0] = L.est[src_of(a, t)].p;
-            bool fresh = false;  // a pair without a profile: the check and fix predict it
             for (int i = 0; i < k; i++) {
                 const int w = 3 * (g & 1) + i;
                 B.u[i + 1] = L.est[ring(a, t + i)].p;
                 B.ws[i] = d_seqws_[w].p;
                 B.use_profile[i] = walked[w] && seq_dx_[w] == L.dx && seq_dy_[w] == L.dy;
-                fresh |= !B.use_profile[i];
                 seq_dx_[w] = L.dx;
                 seq_dy_[w] = L.dy;
                 walked[w] = true;
@@ -404,7 +402,7 @@ int Registration::run_chunked_exact(Level &L, int niter, int nb, const StepFn &s
             // workspace set g & 1: group g - 2's walk has read it and left its profile
             if (g >= 2) OF2D_HIP(hipStreamWaitEvent(sn_st_, ev(ev_walk_, g - 2), 0));
             launch_seqnorm_pass(B, L.dx, L.dy, L.P, sn_st_);
-            if (fresh) launch_seqnorm_refine(B, L.dx, L.dy, L.P, sn_st_);
+            launch_seqnorm_refine(B, L.dx, L.dy, L.P, sn_st_);  // gated per norm on the device
             OF2D_HIP(hipEventRecord(ev(ev_fix_, g), sn_st_));
             hipStream_t wk = wk_st_[g & 1];
             OF2D_HIP(hipStreamWaitEvent(wk, ev(ev_fix_, g), 0));

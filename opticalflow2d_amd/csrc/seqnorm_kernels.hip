@@ -265,6 +265,7 @@ struct SnWs {
     double *bs;             // [2][nb] block sums, then block offsets (check)
     float *dr;              // [2][nt + 1] the last call's drift at each tile (check, pass 1)
     unsigned *miss;         // [2] raw segments the last walk stepped (its profile's quality)
+    unsigned *res;          // [2] tiles the last walk resolved (gates the check, below)
 };
 // The profile of the last call that predicts norm n: its own, except for
 // |prev| after a call whose prev was zero (the Logger's first update), whose
@@ -624,6 +625,16 @@ void seqnorm_tables(unsigned N, int dimx, int P, unsigned nt, SnJobs J) {
 // (A single 1024-thread block over every tile took 22 us at 4096^2 and 120
 // us at 8192^2, 600 us when it waited for CUs behind a triple launch.)
 constexpr int kSnChk = 256;  // tiles per block of the check
+// The check and fix run for a norm only when its prediction is in doubt: no
+// profile, or the last walk on the workspace resolved more than kSnResMax
+// tiles (crossings take ~15-25 per norm at 4096^2; a profile that missed
+// many tiles predicts the next call poorly too).  Otherwise the walk resolves
+// the few tiles the prediction missed itself, and the four launches return at
+// once.
+constexpr unsigned kSnResMax = 48;
+__device__ __forceinline__ bool sn_check_norm(const SnWs &ws, int use_prof, int n) {
+    return !use_prof || ws.res[n] > kSnResMax;
+}
 constexpr unsigned kSnMissMax = 256;  // raw segments of a walk whose profile still predicts
 __device__ __forceinline__ double sn_drift(const SnWs &ws, unsigned nt, int src, unsigned b) {
     const double f = ws.prof[(size_t)src * (nt + 1) + b], q = ws.Pp[(size_t)src * (nt + 1) + b];
@@ -632,6 +643,7 @@ __device__ __forceinline__ double sn_drift(const SnWs &ws, unsigned nt, int src,
 __global__ __launch_bounds__(kSnChk) void seqnorm_check_sums(unsigned nt, SnJobs J) {
     const SnWs &ws = J.ws[blockIdx.y];
     const int use_prof = J.use_prof[blockIdx.y];
+    if (!sn_check_norm(ws, use_prof, 0) && !sn_check_norm(ws, use_prof, 1)) return;
     const unsigned b = blockIdx.x * kSnChk + threadIdx.x;
     __shared__ double sh[2][kSnChk / 64];
     for (int n = 0; n < 2; n++) {
@@ -655,6 +667,8 @@ __global__ __launch_bounds__(kSnChk) void seqnorm_check_sums(unsigned nt, SnJobs
 __global__ __launch_bounds__(kSnScan) void seqnorm_check_scan(unsigned nt, unsigned nb, SnJobs J) {
     const SnWs &ws = J.ws[blockIdx.y];
     const double *p_off = J.p_off[blockIdx.y];
+    const int use_prof = J.use_prof[blockIdx.y];
+    if (!sn_check_norm(ws, use_prof, 0) && !sn_check_norm(ws, use_prof, 1)) return;
     const unsigned chunk = (nb + kSnScan - 1) / kSnScan;
     const unsigned k0 = min(nb, threadIdx.x * chunk), k1 = min(nb, k0 + chunk);
     __shared__ double sh[2][kSnScan];
@@ -709,6 +723,8 @@ __global__ __launch_bounds__(kSnScan) void seqnorm_check_scan(unsigned nt, unsig
 __global__ __launch_bounds__(kSnChk) void seqnorm_check(unsigned nt, SnJobs J) {
     const SnWs &ws = J.ws[blockIdx.y];
     const int use_prof = J.use_prof[blockIdx.y];
+    const bool chk[2] = {sn_check_norm(ws, use_prof, 0), sn_check_norm(ws, use_prof, 1)};
+    if (!chk[0] && !chk[1]) return;
     const unsigned b = blockIdx.x * kSnChk + threadIdx.x;
     const bool active = b < nt;
     const int lane = threadIdx.x & 63, w = threadIdx.x / 64;
@@ -740,7 +756,7 @@ __global__ __launch_bounds__(kSnChk) void seqnorm_check(unsigned nt, SnJobs J) {
     if (!active) return;
     bool listed = false;
     for (int n = 0; n < 2; n++) {
-        if (!(h[n] & (kHdrZero | kHdrNan)) && a[n] < INFINITY && Pb[n] < INFINITY) {
+        if (chk[n] && !(h[n] & (kHdrZero | kHdrNan)) && a[n] < INFINITY && Pb[n] < INFINITY) {
             // with a usable profile: the prefix times its drift, 1/64 either
             // side; without: the float sum below the fp64 prefix by up to a
             // factor 16 (the kSnCand binades below 1/16 above it: past 2^24
@@ -1235,6 +1251,7 @@ __global__ __launch_bounds__(64 * kSnWalkWaves) void seqnorm_walk(unsigned N, in
         ws.tot[2 * n + 1] = ws.tot[2 * n];
         ws.tot[2 * n] = S;
         ws.miss[n] = (unsigned)raw;  // segments its resolves stepped term by term
+        ws.res[n] = (unsigned)resolves;
         out[n] = S;
         if (dbg) {
             dbg[n] = resolves;
@@ -1261,7 +1278,7 @@ size_t seqnorm_workspace_bytes(int dimx, int dimy) {
            2 * (nt + 1) * (sizeof(double) + sizeof(float)) + 4 * sizeof(float) +
            4 * sizeof(unsigned) + 2 * sizeof(double) +
            2 * ((nt + 1 + kSnChk - 1) / kSnChk) * sizeof(double) + 2 * (nt + 1) * sizeof(float) +
-           2 * sizeof(unsigned) + 256;
+           4 * sizeof(unsigned) + 256;
 }
 
 namespace {
@@ -1282,6 +1299,7 @@ SnWs carve(void *ws, unsigned nt) {
     w.bs = w.tot64 + 2;
     w.dr = reinterpret_cast<float *>(w.bs + 2 * (size_t)((nt + 1 + kSnChk - 1) / kSnChk));
     w.miss = reinterpret_cast<unsigned *>(w.dr + 2 * (size_t)(nt + 1));
+    w.res = w.miss + 2;
     return w;
 }
 unsigned check_geometry(int dimx, int dimy, int P) {
@@ -1423,10 +1441,9 @@ void launch_seqnorm_walk(const float2 *cur, const float2 *prev, int dimx, int di
 
 void launch_seqnorm(const float2 *cur, const float2 *prev, int dimx, int dimy, int P, void *ws,
                     bool use_profile, float *out, int *dbg, hipStream_t st) {
-    // with a profile the walk resolves the tiles it mispredicted: no check / fix
     const SeqnormBatch B = one(cur, prev, ws, use_profile);
     launch_seqnorm_pass(B, dimx, dimy, P, st);
-    if (!use_profile) launch_seqnorm_refine(B, dimx, dimy, P, st);
+    launch_seqnorm_refine(B, dimx, dimy, P, st);
     launch_seqnorm_walk(cur, prev, dimx, dimy, P, ws, nullptr, out, dbg, st);
 }
 

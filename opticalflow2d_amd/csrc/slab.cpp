@@ -328,10 +328,10 @@ SlabGeometry slab_geometry(const of2d_slab *s) {
 // three iterates, with its 3-line halo, or single steps with 1-line halos)
 // into a ring of kExR buffers, and each group's norms are one batch of
 // seqnorm launches (seqnorm_kernels.hip) over this slab's rows:
-//   sn  the pass; for pairs without a profile (a loop's first groups) also
-//       the slab's fp64 totals, the prediction offsets chained in rank order
-//       (rank r receives r - 1's running fp64 totals and sends its own on)
-//       and the check / fix
+//   sn  the pass, the slab's fp64 totals, the prediction offsets chained in
+//       rank order (rank r receives r - 1's running fp64 totals and sends its
+//       own on), the check / fix (which work only for norms without a usable
+//       profile)
 //   wk  the walk, chained in rank order: rank r starts from rank r - 1's
 //       exact running sums after its last term and passes its own on, so the
 //       last rank's walk ends with the reference's sums bit for bit
@@ -472,13 +472,11 @@ int run_exact(of2d_slab *s, int niter) {
             B.K = k;
             B.u[0] = exbuf(s, src_of(a, t)).p;
             const double *tot[3];
-            bool fresh = false;  // a pair without a profile: offsets, check and fix
             for (int i = 0; i < k; i++) {
                 const int w = 3 * (int)(g & 1) + i;
                 B.u[i + 1] = exbuf(s, ring(a, t + i)).p;
                 B.ws[i] = E.ws[w].p;
                 B.use_profile[i] = E.walked[w];
-                fresh |= !E.walked[w];
                 E.walked[w] = true;
                 B.p_off[i] = E.poff.p + 2 * i;
                 B.out[i] = E.seq.p + 2 * (size_t)(t + i);
@@ -487,29 +485,25 @@ int run_exact(of2d_slab *s, int niter) {
             // workspace set g & 1: group g - 2's walk has read it and left its profile
             if (g >= 2) OF2D_HIP(hipStreamWaitEvent(E.sn, ev(E.ev_walk, g - 2), 0));
             of2d::launch_seqnorm_pass(B, s->dimx, s->nrows, s->P, E.sn);
-            // pairs with a profile: the walk resolves the tiles it missed, no
-            // check (the same groups on every rank: the chain stays matched)
-            if (fresh) {
-                for (int i = 0; i < k; i++)
-                    tot[i] = of2d::seqnorm_total(s->dimx, s->nrows, s->P, B.ws[i], E.sn);
-                double *nxt = E.nxt.p + 6 * (g % kExEv);
-                const double *prev_nxt = nullptr;
-                if (r > 0 && rccl) {
-                    double *in = E.nxt_in.p + 6 * (g % kExEv);
-                    OF2D_NCCL(ncclRecv(in, 2 * k, ncclDouble, r - 1, E.comm_sn, E.sn));
-                    prev_nxt = in;
-                } else if (r > 0 && grp) {
-                    wait_rank(grp->off_done[r - 1], g);
-                    OF2D_HIP(hipStreamWaitEvent(E.sn, ev(up->ex->ev_off, g), 0));
-                    prev_nxt = up->ex->nxt.p + 6 * (g % kExEv);
-                }
-                of2d::launch_seqnorm_offset_chain(prev_nxt, tot, k, E.poff.p, nxt, E.sn);
-                if (rccl && r < n - 1)
-                    OF2D_NCCL(ncclSend(nxt, 2 * k, ncclDouble, r + 1, E.comm_sn, E.sn));
-                OF2D_HIP(hipEventRecord(ev(E.ev_off, g), E.sn));
-                if (grp) grp->off_done[r].store(g + 1, std::memory_order_release);
-                of2d::launch_seqnorm_refine(B, s->dimx, s->nrows, s->P, E.sn);
+            for (int i = 0; i < k; i++)
+                tot[i] = of2d::seqnorm_total(s->dimx, s->nrows, s->P, B.ws[i], E.sn);
+            double *nxt = E.nxt.p + 6 * (g % kExEv);
+            const double *prev_nxt = nullptr;
+            if (r > 0 && rccl) {
+                double *in = E.nxt_in.p + 6 * (g % kExEv);
+                OF2D_NCCL(ncclRecv(in, 2 * k, ncclDouble, r - 1, E.comm_sn, E.sn));
+                prev_nxt = in;
+            } else if (r > 0 && grp) {
+                wait_rank(grp->off_done[r - 1], g);
+                OF2D_HIP(hipStreamWaitEvent(E.sn, ev(up->ex->ev_off, g), 0));
+                prev_nxt = up->ex->nxt.p + 6 * (g % kExEv);
             }
+            of2d::launch_seqnorm_offset_chain(prev_nxt, tot, k, E.poff.p, nxt, E.sn);
+            if (rccl && r < n - 1)
+                OF2D_NCCL(ncclSend(nxt, 2 * k, ncclDouble, r + 1, E.comm_sn, E.sn));
+            OF2D_HIP(hipEventRecord(ev(E.ev_off, g), E.sn));
+            if (grp) grp->off_done[r].store(g + 1, std::memory_order_release);
+            of2d::launch_seqnorm_refine(B, s->dimx, s->nrows, s->P, E.sn);
             OF2D_HIP(hipEventRecord(ev(E.ev_fix, g), E.sn));
             OF2D_HIP(hipStreamWaitEvent(E.wk, ev(E.ev_fix, g), 0));
             if (r > 0 && rccl) {
