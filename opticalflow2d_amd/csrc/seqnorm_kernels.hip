@@ -626,14 +626,18 @@ void seqnorm_tables(unsigned N, int dimx, int P, unsigned nt, SnJobs J) {
 // us at 8192^2, 600 us when it waited for CUs behind a triple launch.)
 constexpr int kSnChk = 256;  // tiles per block of the check
 // The check and fix run for a norm only when its prediction is in doubt: no
-// profile, or the last walk on the workspace resolved more than kSnResMax
-// tiles (crossings take ~15-25 per norm at 4096^2; a profile that missed
-// many tiles predicts the next call poorly too).  Otherwise the walk resolves
-// the few tiles the prediction missed itself, and the four launches return at
-// once.
+// profile, no trend of its totals (the pass scaled the profile by 1: the
+// first updates of a loop), or the last walk on the workspace resolved more
+// than kSnResMax tiles (crossings take ~15-25 per norm at 4096^2; a profile
+// that missed many tiles predicts the next call poorly too).  Otherwise the
+// walk resolves the few tiles the prediction missed itself, and the four
+// launches return at once.
 constexpr unsigned kSnResMax = 48;
 __device__ __forceinline__ bool sn_check_norm(const SnWs &ws, int use_prof, int n) {
-    return !use_prof || ws.res[n] > kSnResMax;
+    if (!use_prof) return true;
+    const int src = prof_src(ws, n);
+    const bool trend = src == n && ws.tot[2 * src] > 0.0f && ws.tot[2 * src + 1] > 0.0f;
+    return !trend || ws.res[n] > kSnResMax;
 }
 constexpr unsigned kSnMissMax = 256;  // raw segments of a walk whose profile still predicts
 __device__ __forceinline__ double sn_drift(const SnWs &ws, unsigned nt, int src, unsigned b) {
