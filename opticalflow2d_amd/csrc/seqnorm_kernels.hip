@@ -265,7 +265,6 @@ struct SnWs {
     double *bs;             // [2][nb] block sums, then block offsets (check)
     float *dr;              // [2][nt + 1] the last call's drift at each tile (check, pass 1)
     unsigned *miss;         // [2] raw segments the last walk stepped (its profile's quality)
-    unsigned *res;          // [2] tiles the last walk resolved (gates the check, below)
 };
 // The profile of the last call that predicts norm n: its own, except for
 // |prev| after a call whose prev was zero (the Logger's first update), whose
@@ -275,6 +274,32 @@ __device__ __forceinline__ int prof_src(const SnWs &ws, int n) {
 }
 __device__ __forceinline__ size_t g_index(unsigned b, int n, int c, int s) {
     return (((size_t)b * 2 + n) * kSnCand + c) * kSnSegs + s;
+}
+
+// The lane's term of segment `seg` of tile `b`: the vector whose magnitude it
+// is (cur - prev, Field::operator- (Field.tpp:305-334), or prev; 0 past the
+// grid), loaded ahead of the raw segment that uses it
+struct SnSegTerms {
+    float2 v;
+};
+__device__ __forceinline__ SnSegTerms sn_seg_load(const float2 *__restrict__ cur,
+                                                  const float2 *__restrict__ prev, int which,
+                                                  unsigned b, int seg, unsigned N, int dimx,
+                                                  int P) {
+    const unsigned L = b * (unsigned)kSnTile + 64u * seg + (threadIdx.x & 63);
+    SnSegTerms t{make_float2(0.0f, 0.0f)};
+    if (L < N) {
+        const unsigned j = L / (unsigned)dimx, i = L - j * (unsigned)dimx;
+        const size_t off = (size_t)j * (size_t)P + i;
+        const float2 p = prev[off];
+        if (which) {
+            t.v = p;
+        } else {
+            const float2 c = cur[off];
+            t.v = make_float2(c.x - p.x, c.y - p.y);
+        }
+    }
+    return t;
 }
 
 // ---------------------------------------------------------------- tables
@@ -476,85 +501,86 @@ __device__ __forceinline__ void sn_wave_pass(const SnJobs &J, unsigned N, int di
     }
 }
 
-// The fix's entries of one listed tile of pair j (one wave): for each norm
-// whose header is pending (new candidates) or asks for segment entries, the 64
-// segment entries G of every candidate (one DPP sum per segment; lane s holds
-// segment s's until the stores) and the tile entries T, their saturating sum.
-__device__ __forceinline__ void sn_wave_fix(const SnJobs &J, int j, unsigned N, int dimx, int P,
-                                            unsigned b) {
+// The fix's tile entries of one listed tile b of pair j, by the block's four
+// waves (16 consecutive segments each): for each norm whose header is pending
+// (the check's new candidates, up to four), each lane adds its terms'
+// increments as the pass does; the waves' saturating sums meet in LDS.  The
+// walk makes any segment entries it needs itself, so the fix makes none.
+__device__ void sn_block_fix(const SnJobs &J, int j, unsigned N, int dimx, int P, unsigned b) {
     const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / 64));
     const SnWs &ws = J.ws[j];
+    constexpr int kW = kSnThreads / 64, kSegs = kSnSegs / kW;
     unsigned hd[2];
-    int nc[2], elo[2];
+    int nc[2];
+    float sc[2][kSnCand];
 #pragma unroll
     for (int n = 0; n < 2; n++) {
-        hd[n] = ws.H[2 * (size_t)b + n];
-        nc[n] = (hd[n] & (kHdrPending | kHdrSegReq)) ? hdr_nc(hd[n]) : 0;
-        elo[n] = hdr_elo(hd[n]);
+        hd[n] = (unsigned)__builtin_amdgcn_readfirstlane((int)ws.H[2 * (size_t)b + n]);
+        nc[n] = (hd[n] & kHdrPending) ? hdr_nc(hd[n]) : 0;
+#pragma unroll
+        for (int c = 0; c < kSnCand; c++)
+            sc[n][c] = c < nc[n] ? sn_scale32(hdr_elo(hd[n]) + c) : 0.0f;
     }
-    unsigned gv[2][kSnCand];
+    unsigned tl[2][kSnCand] = {}, bl[2] = {0u, 0u};
+    SnSegTerms tv[kSegs][2];
+#pragma unroll
+    for (int k = 0; k < kSegs; k++)
+#pragma unroll
+        for (int n = 0; n < 2; n++)
+            tv[k][n] = nc[n] ? sn_seg_load(J.u[j + 1], J.u[j], n, b, w * kSegs + k, N, dimx, P)
+                             : SnSegTerms{make_float2(0.0f, 0.0f)};
+#pragma unroll
+    for (int k = 0; k < kSegs; k++)
+#pragma unroll
+        for (int n = 0; n < 2; n++) {
+            if (!nc[n]) continue;
+            const float x = tv[k][n].v.x, y = tv[k][n].v.y;
+            const SnEst v = sn_est(x, y);
+            unsigned m[kSnCand];
+            bool unc = !v.ok;
+#pragma unroll
+            for (int c = 0; c < kSnCand; c++) unc |= !sn_incr_est(v, sc[n][c], m[c]);
+            if (sn_ballot(unc)) {
+                const double dd = sn_mag(x, y);
+#pragma unroll
+                for (int c = 0; c < kSnCand; c++) {
+                    bool bad = false;
+                    m[c] = sn_incr(dd, c < nc[n] ? sn_scale(hdr_elo(hd[n]) + c) : 0.0, bad);
+                    bl[n] |= bad ? 1u << c : 0u;
+                }
+            }
+#pragma unroll
+            for (int c = 0; c < kSnCand; c++) tl[n][c] += m[c];
+        }
+    auto sat = [](unsigned p, unsigned x) {
+        return ((p | x) & kSnBad) | sn_sat(p & ~kSnBad, x & ~kSnBad);
+    };
+    __shared__ unsigned part[kW][2][kSnCand];
 #pragma unroll
     for (int n = 0; n < 2; n++)
 #pragma unroll
-        for (int c = 0; c < kSnCand; c++) gv[n][c] = 0u;
-    SnLoader<1> ld(b, (unsigned)dimx);
-    constexpr int D = sn_ring<1>();
-    float2 cv[D][2];
-#pragma unroll
-    for (int d = 0; d < D; d++) ld.next(J, j, N, (unsigned)dimx, (unsigned)P, cv[d]);
-    for (int s0 = 0; s0 < kSnSegs; s0 += D) {
-#pragma unroll
-        for (int d = 0; d < D; d++) {
-            const int s = s0 + d;
-#pragma unroll
-            for (int n = 0; n < 2; n++) {
-                if (nc[n] == 0) continue;
-                // Field::operator- (Field.tpp:305-334) for |cur - prev|
-                const float x = n ? cv[d][0].x : cv[d][1].x - cv[d][0].x;
-                const float y = n ? cv[d][0].y : cv[d][1].y - cv[d][0].y;
-                const SnEst v = sn_est(x, y);
-                unsigned m[kSnCand];
-                bool bad[kSnCand], unc = false;
-#pragma unroll
-                for (int c = 0; c < kSnCand; c++) {
-                    m[c] = 0u;
-                    bad[c] = false;
-                    if (c < nc[n]) unc |= !sn_incr_est(v, sn_scale32(elo[n] + c), m[c]);
-                }
-                if (sn_ballot(unc)) {
-                    const double dd = sn_mag(x, y);
-#pragma unroll
-                    for (int c = 0; c < kSnCand; c++)
-                        if (c < nc[n]) m[c] = sn_incr(dd, sn_scale(elo[n] + c), bad[c]);
-                }
-#pragma unroll
-                for (int c = 0; c < kSnCand; c++) {
-                    if (c >= nc[n]) continue;
-                    const unsigned t = wave_sum(m[c]);  // <= 64 2^25
-                    const bool tb = sn_ballot(bad[c]) != 0ull;
-                    const unsigned e = (t < kSnSat ? t : kSnSat) | (tb ? kSnBad : 0u);
-                    gv[n][c] = lane == s ? e : gv[n][c];
-                }
-            }
-            if (s0 + D < kSnSegs) ld.next(J, j, N, (unsigned)dimx, (unsigned)P, cv[d]);
-        }
-    }
-#pragma unroll
-    for (int n = 0; n < 2; n++) {
-        if (nc[n] == 0) continue;
-        unsigned tv = 0u;
-#pragma unroll
         for (int c = 0; c < kSnCand; c++) {
             if (c >= nc[n]) continue;
-            ws.G[g_index(b, n, c, lane)] = gv[n][c];
-            const unsigned t = wave_reduce(gv[n][c], [](unsigned p, unsigned x) {
-                return ((p | x) & kSnBad) | sn_sat(p & ~kSnBad, x & ~kSnBad);
-            });
-            if (lane == c) tv = t;
+            const bool bad = sn_ballot((bl[n] >> c) & 1u) != 0ull;
+            const unsigned l = tl[n][c];
+            const unsigned t = wave_reduce(l < kSnSat ? l : kSnSat, sat) | (bad ? kSnBad : 0u);
+            if (lane == 0) part[w][n][c] = t;
         }
-        if (lane < nc[n]) ws.T[(2 * (size_t)b + n) * kSnCand + lane] = tv;
-        if (lane == 0) ws.H[2 * (size_t)b + n] = (hd[n] & ~(kHdrPending | kHdrSegReq)) | kHdrSeg;
+    __syncthreads();
+    if (w == 0) {
+#pragma unroll
+        for (int n = 0; n < 2; n++) {
+            if (!nc[n]) continue;
+            if (lane < nc[n]) {
+                unsigned t = part[0][n][lane];
+                for (int q = 1; q < kW; q++) t = sat(t, part[q][n][lane]);
+                ws.T[(2 * (size_t)b + n) * kSnCand + lane] = t;
+            }
+            if (lane == 0) ws.H[2 * (size_t)b + n] = hd[n] & ~(kHdrPending | kHdrSegReq);
+        }
     }
+    __syncthreads();  // part is reused by the block's next tile
 }
 
 // the pass over every tile: one wave per tile, K pairs; the candidate count
@@ -625,20 +651,10 @@ void seqnorm_tables(unsigned N, int dimx, int P, unsigned nt, SnJobs J) {
 // (A single 1024-thread block over every tile took 22 us at 4096^2 and 120
 // us at 8192^2, 600 us when it waited for CUs behind a triple launch.)
 constexpr int kSnChk = 256;  // tiles per block of the check
-// The check and fix run for a norm only when its prediction is in doubt: no
-// profile, no trend of its totals (the pass scaled the profile by 1: the
-// first updates of a loop), or the last walk on the workspace resolved more
-// than kSnResMax tiles (crossings take ~15-25 per norm at 4096^2; a profile
-// that missed many tiles predicts the next call poorly too).  Otherwise the
-// walk resolves the few tiles the prediction missed itself, and the four
-// launches return at once.
-constexpr unsigned kSnResMax = 48;
-__device__ __forceinline__ bool sn_check_norm(const SnWs &ws, int use_prof, int n) {
-    if (!use_prof) return true;
-    const int src = prof_src(ws, n);
-    const bool trend = src == n && ws.tot[2 * src] > 0.0f && ws.tot[2 * src + 1] > 0.0f;
-    return !trend || ws.res[n] > kSnResMax;
-}
+// (A gate that skipped the check while the last walk on the workspace had
+// resolved few tiles was tried in round 4: one overshooting trend scaling of
+// a profile then cost a walk thousands of resolves; the check's drift-
+// corrected fp64 prefix predicts well, so it runs for every call.)
 constexpr unsigned kSnMissMax = 256;  // raw segments of a walk whose profile still predicts
 __device__ __forceinline__ double sn_drift(const SnWs &ws, unsigned nt, int src, unsigned b) {
     const double f = ws.prof[(size_t)src * (nt + 1) + b], q = ws.Pp[(size_t)src * (nt + 1) + b];
@@ -647,7 +663,6 @@ __device__ __forceinline__ double sn_drift(const SnWs &ws, unsigned nt, int src,
 __global__ __launch_bounds__(kSnChk) void seqnorm_check_sums(unsigned nt, SnJobs J) {
     const SnWs &ws = J.ws[blockIdx.y];
     const int use_prof = J.use_prof[blockIdx.y];
-    if (!sn_check_norm(ws, use_prof, 0) && !sn_check_norm(ws, use_prof, 1)) return;
     const unsigned b = blockIdx.x * kSnChk + threadIdx.x;
     __shared__ double sh[2][kSnChk / 64];
     for (int n = 0; n < 2; n++) {
@@ -671,8 +686,6 @@ __global__ __launch_bounds__(kSnChk) void seqnorm_check_sums(unsigned nt, SnJobs
 __global__ __launch_bounds__(kSnScan) void seqnorm_check_scan(unsigned nt, unsigned nb, SnJobs J) {
     const SnWs &ws = J.ws[blockIdx.y];
     const double *p_off = J.p_off[blockIdx.y];
-    const int use_prof = J.use_prof[blockIdx.y];
-    if (!sn_check_norm(ws, use_prof, 0) && !sn_check_norm(ws, use_prof, 1)) return;
     const unsigned chunk = (nb + kSnScan - 1) / kSnScan;
     const unsigned k0 = min(nb, threadIdx.x * chunk), k1 = min(nb, k0 + chunk);
     __shared__ double sh[2][kSnScan];
@@ -727,8 +740,6 @@ __global__ __launch_bounds__(kSnScan) void seqnorm_check_scan(unsigned nt, unsig
 __global__ __launch_bounds__(kSnChk) void seqnorm_check(unsigned nt, SnJobs J) {
     const SnWs &ws = J.ws[blockIdx.y];
     const int use_prof = J.use_prof[blockIdx.y];
-    const bool chk[2] = {sn_check_norm(ws, use_prof, 0), sn_check_norm(ws, use_prof, 1)};
-    if (!chk[0] && !chk[1]) return;
     const unsigned b = blockIdx.x * kSnChk + threadIdx.x;
     const bool active = b < nt;
     const int lane = threadIdx.x & 63, w = threadIdx.x / 64;
@@ -760,7 +771,7 @@ __global__ __launch_bounds__(kSnChk) void seqnorm_check(unsigned nt, SnJobs J) {
     if (!active) return;
     bool listed = false;
     for (int n = 0; n < 2; n++) {
-        if (chk[n] && !(h[n] & (kHdrZero | kHdrNan)) && a[n] < INFINITY && Pb[n] < INFINITY) {
+        if (!(h[n] & (kHdrZero | kHdrNan)) && a[n] < INFINITY && Pb[n] < INFINITY) {
             // with a usable profile: the prefix times its drift, 1/64 either
             // side; without: the float sum below the fp64 prefix by up to a
             // factor 16 (the kSnCand binades below 1/16 above it: past 2^24
@@ -813,17 +824,14 @@ __global__ void seqnorm_offset_chain(const double *__restrict__ prev_nxt, SnTota
     }
 }
 
-// the listed tiles of pair blockIdx.y: new tile and segment entries, one wave
-// per tile
+// the listed tiles of pair blockIdx.y: new tile entries, one block per tile
 __global__ __launch_bounds__(kSnThreads) void seqnorm_fix(unsigned N, int dimx, int P,
                                                          unsigned nt, SnJobs J) {
     const int j = blockIdx.y;
     const unsigned cnt = J.ws[j].cnt[0];
-    const unsigned w = (unsigned)__builtin_amdgcn_readfirstlane((int)(threadIdx.x / 64));
-    for (unsigned k = blockIdx.x * (kSnThreads / 64) + w; k < cnt;
-         k += gridDim.x * (kSnThreads / 64)) {
+    for (unsigned k = blockIdx.x; k < cnt; k += gridDim.x) {  // block-uniform
         const unsigned b = (unsigned)__builtin_amdgcn_readfirstlane((int)J.ws[j].list[k]);
-        sn_wave_fix(J, j, N, dimx, P, b);
+        sn_block_fix(J, j, N, dimx, P, b);
     }
 }
 
@@ -866,32 +874,6 @@ __device__ __forceinline__ unsigned lane_at(unsigned v, int q) {
 __device__ __forceinline__ int first_lane(unsigned long long m) { return __builtin_ctzll(m); }
 __device__ __forceinline__ unsigned long long lanes_from(int k) {
     return k >= 64 ? 0ull : (~0ull << k);
-}
-
-// The lane's term of segment `seg` of tile `b`: the vector whose magnitude it
-// is (cur - prev, Field::operator- (Field.tpp:305-334), or prev; 0 past the
-// grid), loaded ahead of the raw segment that uses it
-struct SnSegTerms {
-    float2 v;
-};
-__device__ __forceinline__ SnSegTerms sn_seg_load(const float2 *__restrict__ cur,
-                                                  const float2 *__restrict__ prev, int which,
-                                                  unsigned b, int seg, unsigned N, int dimx,
-                                                  int P) {
-    const unsigned L = b * (unsigned)kSnTile + 64u * seg + (threadIdx.x & 63);
-    SnSegTerms t{make_float2(0.0f, 0.0f)};
-    if (L < N) {
-        const unsigned j = L / (unsigned)dimx, i = L - j * (unsigned)dimx;
-        const size_t off = (size_t)j * (size_t)P + i;
-        const float2 p = prev[off];
-        if (which) {
-            t.v = p;
-        } else {
-            const float2 c = cur[off];
-            t.v = make_float2(c.x - p.x, c.y - p.y);
-        }
-    }
-    return t;
 }
 
 // The 64 terms of a segment (lane = term, `tv` its vector) from the exact
@@ -1255,7 +1237,6 @@ __global__ __launch_bounds__(64 * kSnWalkWaves) void seqnorm_walk(unsigned N, in
         ws.tot[2 * n + 1] = ws.tot[2 * n];
         ws.tot[2 * n] = S;
         ws.miss[n] = (unsigned)raw;  // segments its resolves stepped term by term
-        ws.res[n] = (unsigned)resolves;
         out[n] = S;
         if (dbg) {
             dbg[n] = resolves;
@@ -1282,7 +1263,7 @@ size_t seqnorm_workspace_bytes(int dimx, int dimy) {
            2 * (nt + 1) * (sizeof(double) + sizeof(float)) + 4 * sizeof(float) +
            4 * sizeof(unsigned) + 2 * sizeof(double) +
            2 * ((nt + 1 + kSnChk - 1) / kSnChk) * sizeof(double) + 2 * (nt + 1) * sizeof(float) +
-           4 * sizeof(unsigned) + 256;
+           2 * sizeof(unsigned) + 256;
 }
 
 namespace {
@@ -1303,7 +1284,6 @@ SnWs carve(void *ws, unsigned nt) {
     w.bs = w.tot64 + 2;
     w.dr = reinterpret_cast<float *>(w.bs + 2 * (size_t)((nt + 1 + kSnChk - 1) / kSnChk));
     w.miss = reinterpret_cast<unsigned *>(w.dr + 2 * (size_t)(nt + 1));
-    w.res = w.miss + 2;
     return w;
 }
 unsigned check_geometry(int dimx, int dimy, int P) {
@@ -1353,8 +1333,8 @@ void launch_seqnorm_refine(const SeqnormBatch &B, int dimx, int dimy, int P, hip
     hipLaunchKernelGGL(seqnorm_check_scan, dim3(1, B.K), dim3(kSnScan), 0, st, nt, nb, J);
     hipLaunchKernelGGL(seqnorm_check, dim3(nb, B.K), dim3(kSnChk), 0, st, nt, J);
     OF2D_HIP(hipGetLastError());
-    // one wave per listed tile: up to 1024 waves per pair
-    const unsigned fb = std::min((nt + kSnThreads / 64 - 1) / (kSnThreads / 64), 256u);
+    // one block per listed tile, up to 1024 blocks per pair at once
+    const unsigned fb = std::min(nt, 1024u);
     hipLaunchKernelGGL(seqnorm_fix, dim3(fb, B.K), dim3(kSnThreads), 0, st, N, dimx, P, nt, J);
     OF2D_HIP(hipGetLastError());
 }
