@@ -194,13 +194,14 @@ class Registration {
     // run_chunked with the reference's float norms: every iterate in memory,
     // groups of up to three iterations (a step3m triple or single steps) into
     // a ring of twelve buffers; each group's norms as one batch, its pass on
-    // sn_st_ and its walk on wk_st_[g & 1], workspace set g & 1 (three
+    // sn_st_ and its walk on wk_st_[g & 1], workspace set g mod 3 (three
     // workspaces): the walks of consecutive groups run at once
     int run_chunked_exact(Level &L, int niter, int nb, const StepFn &step, int &final_buf,
                           const StepFn3M &step3m = nullptr);
     hipStream_t sn_st_ = nullptr, wk_st_[2] = {};
     static constexpr int kExactEv = 16;  // event ring per group (> 4 groups in flight)
-    static constexpr int kSeqWs = 6;     // two sets of three
+    static constexpr int kSeqSets = 3;   // workspace sets: group g's walk is read by g + 3
+    static constexpr int kSeqWs = 3 * kSeqSets;
     hipEvent_t ev_step_[kExactEv] = {}, ev_fix_[kExactEv] = {}, ev_walk_[kExactEv] = {};
     DevArray<unsigned char> d_seqws_[kSeqWs];  // seqnorm workspaces (level 0 size)
     DevArray<float> d_seq_;                    // per-iteration exact sums of a chunk

@@ -338,10 +338,10 @@ void Registration::seqnorm(const Level &L, const float2 *cur, const float2 *prev
 // batch (seqnorm_kernels.hip: pair i = iterates t + i - 1, t + i): the
 // bandwidth pass on sn_st_ and the latency-bound walk on wk_st_[g & 1], so
 // group g's walk overlaps group g + 1's steps, pass and walk.  Group g works
-// on workspace set g & 1, whose last walk (group g - 2) left the profile that
-// predicts it; the walk resolves the tiles the prediction missed itself, so
-// the check and fix do work only for norms without a usable profile (a
-// loop's first groups, or after a walk that resolved many tiles).  Iterate m's buffer is read by the walks of the groups of m and
+// on workspace set g mod 3, whose last walk (group g - 3) left the profile that
+// predicts it (the check corrects the prediction with the fp64 prefix and
+// the fix remakes the few tiles it missed); the walk makes the segment
+// entries of the tiles it resolves itself.  Iterate m's buffer is read by the walks of the groups of m and
 // m + 1; iterate m + R rewrites it after both.
 int Registration::run_chunked_exact(Level &L, int niter, int nb, const StepFn &step,
                                     int &final_buf, const StepFn3M &step3m) {
@@ -388,7 +388,7 @@ int Registration::run_chunked_exact(Level &L, int niter, int nb, const StepFn &s
             B.K = k;
             B.u[0] = L.est[src_of(a, t)].p;
             for (int i = 0; i < k; i++) {
-                const int w = 3 * (g & 1) + i;
+                const int w = 3 * (g % kSeqSets) + i;
                 B.u[i + 1] = L.est[ring(a, t + i)].p;
                 B.ws[i] = d_seqws_[w].p;
                 B.use_profile[i] = walked[w] && seq_dx_[w] == L.dx && seq_dy_[w] == L.dy;
@@ -399,8 +399,9 @@ int Registration::run_chunked_exact(Level &L, int niter, int nb, const StepFn &s
                 B.dbg[i] = sn_debug ? dbg.p + kDbg * (size_t)(t + i) : nullptr;
             }
             OF2D_HIP(hipStreamWaitEvent(sn_st_, ev(ev_step_, g), 0));
-            // workspace set g & 1: group g - 2's walk has read it and left its profile
-            if (g >= 2) OF2D_HIP(hipStreamWaitEvent(sn_st_, ev(ev_walk_, g - 2), 0));
+            // workspace set g mod 3: group g - 3's walk has read it and left its
+            // profile (three sets keep a walk's latency off the pass's path)
+            if (g >= kSeqSets) OF2D_HIP(hipStreamWaitEvent(sn_st_, ev(ev_walk_, g - kSeqSets), 0));
             launch_seqnorm_pass(B, L.dx, L.dy, L.P, sn_st_);
             launch_seqnorm_refine(B, L.dx, L.dy, L.P, sn_st_);  // gated per norm on the device
             OF2D_HIP(hipEventRecord(ev(ev_fix_, g), sn_st_));
