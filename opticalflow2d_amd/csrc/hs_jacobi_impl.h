@@ -939,7 +939,11 @@ __global__ __launch_bounds__(64 * WAVES, MINB) void jacobi3_mid_kernel(
     int glo, int ghi, double *__restrict__ partial, double *__restrict__ partial2,
     double *__restrict__ partial3, unsigned *__restrict__ status, int band0, int gx, int gy,
     int rows, const unsigned *__restrict__ range_flag, int jlo, int jhi,
-    const float *__restrict__ Ia, float2 *__restrict__ m1, float2 *__restrict__ m2) {
+    const float *__restrict__ Ia, float2 *__restrict__ m1, float2 *__restrict__ m2,
+    const int *__restrict__ stop, int stop_t0) {
+    // the loop broke before this triple's first iteration (seqnorm_decide):
+    // nothing of it is read
+    if (stop && *stop < stop_t0) return;
     jacobi3_body<ROWS, WAVES, XCD, MINB, UNR, PRIO, ALT, GI, true>(
         uo, un, dI, It, P, dimx, nrows, row0, dimy, alphasq, glo, ghi, partial, partial2, partial3,
         status, band0, gx, gy, rows, range_flag, jlo, jhi, Ia, m1, m2);

@@ -74,7 +74,8 @@ void launch_hs_jacobi3(const float2 *u_old, float2 *u_new, const float2 *dI, con
                        int P, int dimx, int nrows, int row0, int dimy, float alphasq, int glo,
                        int ghi, double *partial, double *partial2, double *partial3,
                        unsigned *status, const unsigned *range_flag, hipStream_t st,
-                       int band_lo, int band_hi, const float *Ia, float2 *u1, float2 *u2) {
+                       int band_lo, int band_hi, const float *Ia, float2 *u1, float2 *u2,
+                       const int *stop, int stop_t0) {
     if (P % kHsStrip != 0 || nrows <= 0 || dimx > P || dimx < 2 || glo > -1 || ghi < nrows + 1)
         throw std::invalid_argument("launch_hs_jacobi3: bad geometry");
     if (!u1 != !u2) throw std::invalid_argument("launch_hs_jacobi3: u1 and u2 go together");
@@ -91,7 +92,8 @@ void launch_hs_jacobi3(const float2 *u_old, float2 *u_new, const float2 *dI, con
         hipLaunchKernelGGL(Ia ? kHsJacobi3IM : kHsJacobi3M, gl, dim3(64 * kHs3Waves), 0, st, u_old,
                            u_new, dI, It, P, dimx, nrows, row0, dimy, alphasq, glo, ghi, partial,
                            partial2, partial3, status, band_lo, (int)g.x, (int)g.y,
-                           hs3_rows(dimx, nrows), range_flag, -1, -1, Ia, u1, u2);
+                           hs3_rows(dimx, nrows), range_flag, -1, -1, Ia, u1, u2, stop,
+                           stop_t0);
     else
         hipLaunchKernelGGL(Ia ? kHsJacobi3I : kHsJacobi3, gl, dim3(64 * kHs3Waves), 0, st, u_old,
                            u_new, dI, It, P, dimx, nrows, row0, dimy, alphasq, glo, ghi, partial,

@@ -175,9 +175,12 @@ void launch_hs_jacobi3(const float2 *u_old, float2 *u_new, const float2 *dI, con
                        int ghi, double *partial, double *partial2, double *partial3,
                        unsigned *status, const unsigned *range_flag, hipStream_t st,
                        int band_lo = -1, int band_hi = -1, const float *Ia = nullptr,
-                       float2 *u1 = nullptr, float2 *u2 = nullptr);
+                       float2 *u1 = nullptr, float2 *u2 = nullptr, const int *stop = nullptr,
+                       int stop_t0 = 0);
 // (u1, u2 non-null: the first two iterates of the owned rows are stored there
-// too, for the reference-exact Logger; +16 B/px)
+// too, for the reference-exact Logger; +16 B/px; with stop, the launch does
+// nothing when *stop < stop_t0: the loop broke before the triple's first
+// iteration stop_t0, seqnorm_decide)
 // Once per gradient field, before the triple kernel runs on it
 // (hs_jacobi_impl.h hs_precheck_kernel): zeroes *range_flag, then sets it if
 // any gradient / denominator of the allocation [base, base + count) lies
@@ -197,6 +200,7 @@ int launch_hs_jacobi3_window(const float2 *u_old, float2 *u_new, const float2 *d
 void launch_hs_precheck(const float2 *base, size_t count, int P, int ghost, int dimx, int dimy,
                         float alphasq, unsigned *range_flag, unsigned *status, hipStream_t st);
 constexpr int kRangeFlagWord = 32;  // word of the 64-word status buffers holding range_flag
+constexpr int kStopWord = 33;  // the exact-Logger loop's break (seqnorm_decide)
 // partial-row length that fits every HS kernel (single, pair, triple)
 inline int hs_partial_blocks(int P, int dimx, int nrows) {
     int nb = hs_nblocks(P, nrows);
@@ -275,7 +279,18 @@ struct SeqnormBatch {
     const float *s_in[3] = {};    // walk: a row slab's predecessors' exact sums
     float *out[3] = {};           // walk: the sums of pair i (device float[2])
     int *dbg[3] = {};             // walk: cost counters (int[10]), optional
+    // the loop's break word (launch_seqnorm_decide): with it, every kernel of
+    // the batch returns at once when *stop < t0 (t0: the batch's first
+    // iteration)
+    const int *stop = nullptr;
+    int t0 = 0;
 };
+// the Logger errors of a walked batch (pair i's sums at seq[2i], seq[2i + 1]),
+// as logger_error does on the host: the first iteration t0 + i > 1 whose
+// error is below 0.001 into *stop (atomicMin); the sums copied to host
+// (mapped host memory, float[2K])
+void launch_seqnorm_decide(const float *seq, int K, int t0, double npx, int *stop, float *host,
+                           hipStream_t st);
 // diagnostics (tools/seqnorm_bench; synchronous): the workspace's list count
 // and profile flags (cnt[0..3]), then per norm the tiles with segment entries,
 // with more than one candidate, with none (out[12])

@@ -101,6 +101,7 @@ struct HostScratch {
     double *sums = nullptr;
     unsigned *status = nullptr;
     float *flt = nullptr;
+    float *seqh = nullptr;  // coherent, mapped: seqnorm_decide's copy of the exact sums
     FluidReport *report = nullptr;  // hipHostMallocCoherent
     int cap = 0;
     void ensure(int n);
@@ -117,7 +118,7 @@ struct Level {
     Field<float2> motion[2];
     int mcur = 0;
     Field<float2> dI;
-    Field<float2> est[14];  // [3] .. [13]: only for the exact-norm loop's ring
+    Field<float2> est[16];  // [3] .. [15]: only for the exact-norm loop's ring
     Field<float2> force, velocity, increment, corr, tmp;
     DevArray<double> cbuf[2];              // Curvature: two x|y double plane pairs (pitch P)
     DevArray<double> cC1T, cC0, cD1T, cD0;  // Curvature: REDFT10 / REDFT01 matrices
@@ -154,8 +155,9 @@ class Registration {
     using StepFn3 = std::function<void(const float2 *src, float2 *dst, double *partial,
                                        double *partial2, double *partial3)>;
     // three iterations in one pass, every iterate stored (d1, d2, d3)
+    // (t0: the triple's first iteration, for the stop word of run_exact_pipelined)
     using StepFn3M =
-        std::function<void(const float2 *src, float2 *d1, float2 *d2, float2 *d3)>;
+        std::function<void(const float2 *src, float2 *d1, float2 *d2, float2 *d3, int t0)>;
 
    private:
     // nblk[k]: block partials written by step (k = 0), step2 (1), step3 (2)
@@ -191,18 +193,27 @@ class Registration {
     // enqueue the exact norms of one Logger update into d_seq_[2t], [2t + 1]
     // (synchronous loops: Elastic, Fluid; workspace 0, on st_)
     void seqnorm(const Level &L, const float2 *cur, const float2 *prev, int t);
-    // run_chunked with the reference's float norms: every iterate in memory,
-    // groups of up to three iterations (a step3m triple or single steps) into
-    // a ring of twelve buffers; each group's norms as one batch, its pass on
-    // sn_st_ and its walk on wk_st_[g & 1], workspace set g mod 3 (three
-    // workspaces): the walks of consecutive groups run at once
+    // run_chunked with the reference's float norms (single steps in groups of
+    // up to three into a ring, each group's norms as one batch on the norm
+    // streams); with step3m, run_exact_pipelined
     int run_chunked_exact(Level &L, int niter, int nb, const StepFn &step, int &final_buf,
                           const StepFn3M &step3m = nullptr);
-    hipStream_t sn_st_ = nullptr, wk_st_[2] = {};
-    static constexpr int kExactEv = 16;  // event ring per group (> 4 groups in flight)
-    static constexpr int kSeqSets = 3;   // workspace sets: group g's walk is read by g + 3
+    // HS: triples, blocks of iterations enqueued one ahead of the host's
+    // decision, the break also taken on the device (the stop word)
+    int run_exact_pipelined(Level &L, int niter, const StepFn &step, int &final_buf,
+                            const StepFn3M &step3m);
+    // a group's norms behind its steps: pass on sn_st_, check and fix on
+    // fx_st_, walk (and with B.stop seqnorm_decide) on wk_st_[g mod 3]
+    void enqueue_norms(const SeqnormBatch &B, const Level &L, int g, double npx = 0.0,
+                       float *seqh_out = nullptr);
+    void print_sn_debug(const Level &L, const int *dbg, int k0, int lo, int hi);
+    hipStream_t sn_st_ = nullptr, fx_st_ = nullptr, wk_st_[3] = {};
+    static constexpr int kExactEv = 64;  // event ring per group (two blocks in flight)
+    static constexpr int kSeqSets = 4;   // workspace sets: group g's walk is read by g + 4
     static constexpr int kSeqWs = 3 * kSeqSets;
-    hipEvent_t ev_step_[kExactEv] = {}, ev_fix_[kExactEv] = {}, ev_walk_[kExactEv] = {};
+    static constexpr int kRing = 15;  // iterate buffers: a step waits for the walks 4-5 groups back
+    hipEvent_t ev_step_[kExactEv] = {}, ev_pass_[kExactEv] = {}, ev_fix_[kExactEv] = {},
+               ev_walk_[kExactEv] = {};
     DevArray<unsigned char> d_seqws_[kSeqWs];  // seqnorm workspaces (level 0 size)
     DevArray<float> d_seq_;                    // per-iteration exact sums of a chunk
     int seq_dx_[kSeqWs] = {}, seq_dy_[kSeqWs] = {};  // grid of each workspace's last call

@@ -37,17 +37,21 @@ void HostScratch::ensure(int n) {
     if (n <= cap) return;
     if (sums) (void)hipHostFree(sums);
     if (flt) (void)hipHostFree(flt);
+    if (seqh) (void)hipHostFree(seqh);
     if (!status) OF2D_HIP(hipHostMalloc(&status, 64 * sizeof(unsigned)));
     if (!report)
         OF2D_HIP(hipHostMalloc(&report, sizeof(FluidReport),
                                hipHostMallocCoherent | hipHostMallocMapped));
     OF2D_HIP(hipHostMalloc(&sums, sizeof(double) * 4 * n));
     OF2D_HIP(hipHostMalloc(&flt, sizeof(float) * 4 * n));
+    OF2D_HIP(hipHostMalloc(&seqh, sizeof(float) * 4 * (n + 3),
+                           hipHostMallocCoherent | hipHostMallocMapped));
     cap = n;
 }
 HostScratch::~HostScratch() {
     if (sums) (void)hipHostFree(sums);
     if (flt) (void)hipHostFree(flt);
+    if (seqh) (void)hipHostFree(seqh);
     if (status) (void)hipHostFree(status);
     if (report) (void)hipHostFree(report);
 }
@@ -150,11 +154,13 @@ Registration::~Registration() {
     if (ev_fork_) (void)hipEventDestroy(ev_fork_);
     if (ev_join_) (void)hipEventDestroy(ev_join_);
     if (sn_st_) (void)hipStreamDestroy(sn_st_);
+    if (fx_st_) (void)hipStreamDestroy(fx_st_);
     for (hipStream_t w : wk_st_)
         if (w) (void)hipStreamDestroy(w);
     for (int k = 0; k < kExactEv; k++) {
         if (ev_step_[k]) (void)hipEventDestroy(ev_step_[k]);
         if (ev_fix_[k]) (void)hipEventDestroy(ev_fix_[k]);
+        if (ev_pass_[k]) (void)hipEventDestroy(ev_pass_[k]);
         if (ev_walk_[k]) (void)hipEventDestroy(ev_walk_[k]);
     }
     if (st_) (void)hipStreamDestroy(st_);
@@ -193,10 +199,18 @@ void Registration::ensure_device() {
     OF2D_HIP(hipGetDevice(&home_));
     OF2D_HIP(hipStreamCreateWithFlags(&st_, hipStreamNonBlocking));
     OF2D_HIP(hipStreamCreateWithFlags(&sn_st_, hipStreamNonBlocking));
-    for (hipStream_t &w : wk_st_) OF2D_HIP(hipStreamCreateWithFlags(&w, hipStreamNonBlocking));
+    // the fix and the walks at high priority: they are the latency chain that
+    // gates the steps (ring) and passes (workspaces) a few groups later, and
+    // wait for CUs behind the bandwidth kernels otherwise (4096^2 procedural
+    // convergence 148 -> 128 us per iteration, profiles/r04m_exact_pipeline_ab.log)
+    int prio_lo = 0, pr = 0;
+    OF2D_HIP(hipDeviceGetStreamPriorityRange(&prio_lo, &pr));
+    OF2D_HIP(hipStreamCreateWithPriority(&fx_st_, hipStreamNonBlocking, pr));
+    for (hipStream_t &w : wk_st_) OF2D_HIP(hipStreamCreateWithPriority(&w, hipStreamNonBlocking, pr));
     for (int k = 0; k < kExactEv; k++) {
         OF2D_HIP(hipEventCreateWithFlags(&ev_step_[k], hipEventDisableTiming));
         OF2D_HIP(hipEventCreateWithFlags(&ev_fix_[k], hipEventDisableTiming));
+        OF2D_HIP(hipEventCreateWithFlags(&ev_pass_[k], hipEventDisableTiming));
         OF2D_HIP(hipEventCreateWithFlags(&ev_walk_[k], hipEventDisableTiming));
     }
     OF2D_HIP(hipEventCreateWithFlags(&ev_fork_, hipEventDisableTiming));
@@ -230,7 +244,7 @@ void Registration::ensure_device() {
     OF2D_HIP(hipDeviceSynchronize());  // null-stream memset vs the non-blocking stream
     hs_.ensure(std::max(chunk_, 64));
     for (auto &w : d_seqws_) w.alloc(seqnorm_workspace_bytes(dimx_, dimy_));
-    d_seq_.alloc(2 * (size_t)std::max(chunk_, 64));
+    d_seq_.alloc(4 * (size_t)(std::max(chunk_, 64) + 3));  // two blocks of run_exact_pipelined
     ready_ = true;
 }
 
@@ -330,24 +344,27 @@ void Registration::seqnorm(const Level &L, const float2 *cur, const float2 *prev
                    nullptr, st_);
 }
 
-// The chunked loop of run_chunked with the reference's float norms.  Every
+// The chunked loop of run_chunked with the reference's float norms for the
+// solvers without a triple (Demons, Elastic, Curvature: single steps).  Every
 // iterate must be in memory for its norms, so the iterations run in groups of
-// up to three (a step3m triple that stores all three iterates, HS; or single
-// steps) into a ring of the R buffers other than the chunk's start buffer a
-// (kept for a replay).  The norms of a group run behind its steps as one
-// batch (seqnorm_kernels.hip: pair i = iterates t + i - 1, t + i): the
-// bandwidth pass on sn_st_ and the latency-bound walk on wk_st_[g & 1], so
-// group g's walk overlaps group g + 1's steps, pass and walk.  Group g works
-// on workspace set g mod 3, whose last walk (group g - 3) left the profile that
-// predicts it (the check corrects the prediction with the fp64 prefix and
-// the fix remakes the few tiles it missed); the walk makes the segment
-// entries of the tiles it resolves itself.  Iterate m's buffer is read by the walks of the groups of m and
-// m + 1; iterate m + R rewrites it after both.
+// up to three single steps into a ring of the kRing buffers other than the
+// chunk's start buffer a (kept for a replay).  The norms of a group run behind
+// its steps as one batch (seqnorm_kernels.hip: pair i = iterates t + i - 1,
+// t + i): the bandwidth pass on sn_st_, the check and fix on fx_st_ and the
+// latency-bound walk on wk_st_[g mod 3], so group g's walk overlaps the steps,
+// passes and walks of the groups after it.  Group g works on workspace set
+// g mod kSeqSets, whose last walk (group g - kSeqSets) left the profile that
+// predicts it (the check corrects the prediction with the fp64 prefix and the
+// fix remakes the few tiles it missed); the walk makes the segment entries of
+// the tiles it resolves itself.  Iterate m's buffer is read by the walks of
+// iterations m - 1 and m; iterate m + kRing rewrites it after both.  HS takes
+// run_exact_pipelined.
 int Registration::run_chunked_exact(Level &L, int niter, int nb, const StepFn &step,
                                     int &final_buf, const StepFn3M &step3m) {
+    if (step3m) return run_exact_pipelined(L, niter, step, final_buf, step3m);
     const double npx = (double)L.dx * L.dy;
     last_err_.clear();
-    constexpr int R = 12;
+    constexpr int R = kRing;
     static_assert(R + 1 <= (int)(sizeof(L.est) / sizeof(L.est[0])), "ring");
     for (int b = 3; b <= R; b++)
         if (!L.est[b].p) L.est[b].alloc(L.dx, L.dy);
@@ -373,16 +390,15 @@ int Registration::run_chunked_exact(Level &L, int niter, int nb, const StepFn &s
         for (int t = 0; t < C; g++) {
             const int k = std::min(3, C - t);
             for (int m = t; m < t + k; m++) group_of[m] = g;
-            // the buffers of iterates t .. t + k - 1 held iterates t - R ..
-            // t + k - 1 - R, last read by the walk of iterate t + k - R's group
-            if (t + k - R >= 0) OF2D_HIP(hipStreamWaitEvent(st_, ev(ev_walk_, group_of[t + k - R]), 0));
-            if (k == 3 && step3m) {
-                step3m(L.est[src_of(a, t)].p, L.est[ring(a, t)].p, L.est[ring(a, t + 1)].p,
-                       L.est[ring(a, t + 2)].p);
-            } else {
-                for (int m = t; m < t + k; m++)
-                    step(L.est[src_of(a, m)].p, L.est[ring(a, m)].p, d_partial_ + (size_t)m * nb * 2);
-            }
+            // the buffers of iterates t + 1 .. t + k held iterates t + 1 - R ..
+            // t + k - R, read by the walks of iterations t - R .. t + k - R
+            for (int q = std::max(t - R, 0), last = -1; q <= t + k - R; q++)
+                if (group_of[q] != last) {
+                    last = group_of[q];
+                    OF2D_HIP(hipStreamWaitEvent(st_, ev(ev_walk_, last), 0));
+                }
+            for (int m = t; m < t + k; m++)
+                step(L.est[src_of(a, m)].p, L.est[ring(a, m)].p, d_partial_ + (size_t)m * nb * 2);
             OF2D_HIP(hipEventRecord(ev(ev_step_, g), st_));
             SeqnormBatch B;
             B.K = k;
@@ -398,35 +414,15 @@ int Registration::run_chunked_exact(Level &L, int niter, int nb, const StepFn &s
                 B.out[i] = d_seq_.p + 2 * (size_t)(t + i);
                 B.dbg[i] = sn_debug ? dbg.p + kDbg * (size_t)(t + i) : nullptr;
             }
-            OF2D_HIP(hipStreamWaitEvent(sn_st_, ev(ev_step_, g), 0));
-            // workspace set g mod 3: group g - 3's walk has read it and left its
-            // profile (three sets keep a walk's latency off the pass's path)
-            if (g >= kSeqSets) OF2D_HIP(hipStreamWaitEvent(sn_st_, ev(ev_walk_, g - kSeqSets), 0));
-            launch_seqnorm_pass(B, L.dx, L.dy, L.P, sn_st_);
-            launch_seqnorm_refine(B, L.dx, L.dy, L.P, sn_st_);  // gated per norm on the device
-            OF2D_HIP(hipEventRecord(ev(ev_fix_, g), sn_st_));
-            hipStream_t wk = wk_st_[g & 1];
-            OF2D_HIP(hipStreamWaitEvent(wk, ev(ev_fix_, g), 0));
-            launch_seqnorm_walk(B, L.dx, L.dy, L.P, wk);
-            OF2D_HIP(hipEventRecord(ev(ev_walk_, g), wk));
+            enqueue_norms(B, L, g);
             t += k;
         }
         // the last walk of each walk stream
-        for (int q = std::max(g - 2, g0); q < g; q++) OF2D_HIP(hipStreamWaitEvent(st_, ev(ev_walk_, q), 0));
+        for (int q = std::max(g - 3, g0); q < g; q++) OF2D_HIP(hipStreamWaitEvent(st_, ev(ev_walk_, q), 0));
         OF2D_HIP(hipMemcpyAsync(hs_.flt, d_seq_.p, sizeof(float) * 2 * C, hipMemcpyDeviceToHost,
                                 st_));
         check_status();  // synchronises st_ (and with it every norm of the chunk)
-        if (sn_debug) {
-            std::vector<int> h(kDbg * (size_t)C);
-            OF2D_HIP(hipMemcpy(h.data(), dbg.p, h.size() * sizeof(int), hipMemcpyDeviceToHost));
-            for (int t = 0; t < C; t++)
-                std::fprintf(stderr,
-                             "seqnorm %dx%d it %d: resolves %d %d raw %d %d listed %d walk %d %d "
-                             "res %d made %d %d\n",
-                             L.dx, L.dy, k0 + t, h[kDbg * t], h[kDbg * t + 1], h[kDbg * t + 2],
-                             h[kDbg * t + 3], h[kDbg * t + 4], h[kDbg * t + 5], h[kDbg * t + 6],
-                             h[kDbg * t + 7], h[kDbg * t + 8], h[kDbg * t + 9]);
-        }
+        if (sn_debug) print_sn_debug(L, dbg.p, k0, 0, C);
         for (int t = 0; t < C; t++) {
             const int k = k0 + t;
             const float err = logger_error(hs_.flt[2 * t], hs_.flt[2 * t + 1], npx);
@@ -445,6 +441,181 @@ int Registration::run_chunked_exact(Level &L, int niter, int nb, const StepFn &s
         k0 += C;
     }
     final_buf = a;
+    return niter;
+}
+
+// One group's norms behind its steps (ev_step_[g] recorded on st_): the pass
+// on sn_st_ once group g - kSeqSets's walk has left the workspaces, the check
+// and fix on fx_st_, the walk on wk_st_[g mod 3]; with B.stop, seqnorm_decide
+// after the walk (the sums' copy to seqh_out).  Records ev_walk_[g].
+void Registration::enqueue_norms(const SeqnormBatch &B, const Level &L, int g, double npx,
+                                 float *seqh_out) {
+    auto ev = [](hipEvent_t *e, int q) { return e[q % kExactEv]; };
+    OF2D_HIP(hipStreamWaitEvent(sn_st_, ev(ev_step_, g), 0));
+    if (g >= kSeqSets) OF2D_HIP(hipStreamWaitEvent(sn_st_, ev(ev_walk_, g - kSeqSets), 0));
+    launch_seqnorm_pass(B, L.dx, L.dy, L.P, sn_st_);
+    OF2D_HIP(hipEventRecord(ev(ev_pass_, g), sn_st_));
+    OF2D_HIP(hipStreamWaitEvent(fx_st_, ev(ev_pass_, g), 0));
+    launch_seqnorm_refine(B, L.dx, L.dy, L.P, fx_st_);
+    OF2D_HIP(hipEventRecord(ev(ev_fix_, g), fx_st_));
+    hipStream_t wk = wk_st_[g % 3];
+    OF2D_HIP(hipStreamWaitEvent(wk, ev(ev_fix_, g), 0));
+    launch_seqnorm_walk(B, L.dx, L.dy, L.P, wk);
+    if (B.stop)
+        launch_seqnorm_decide(B.out[0], B.K, B.t0, npx, const_cast<int *>(B.stop), seqh_out, wk);
+    OF2D_HIP(hipEventRecord(ev(ev_walk_, g), wk));
+}
+
+// OF2D_SN_DEBUG: iterations [k0 + lo, k0 + hi)'s walk counters (dbg[10 * t])
+void Registration::print_sn_debug(const Level &L, const int *dbg, int k0, int lo, int hi) {
+    constexpr int kDbg = 10;
+    std::vector<int> h(kDbg * (size_t)hi);
+    OF2D_HIP(hipMemcpy(h.data(), dbg, h.size() * sizeof(int), hipMemcpyDeviceToHost));
+    for (int t = lo; t < hi; t++)
+        std::fprintf(stderr,
+                     "seqnorm %dx%d it %d: resolves %d %d raw %d %d listed %d walk %d %d "
+                     "res %d made %d %d\n",
+                     L.dx, L.dy, k0 + t, h[kDbg * t], h[kDbg * t + 1], h[kDbg * t + 2],
+                     h[kDbg * t + 3], h[kDbg * t + 4], h[kDbg * t + 5], h[kDbg * t + 6],
+                     h[kDbg * t + 7], h[kDbg * t + 8], h[kDbg * t + 9]);
+}
+
+// HS's loop with the reference's float norms, pipelined from chunk to chunk.
+// The iterations run in triples (step3m: all three iterates stored) into the
+// ring est[1 .. kRing] (iterate j >= 1 in est[1 + (j - 1) mod kRing], iterate
+// 0 in est[0]), each triple's norms as one batch (enqueue_norms).  The break
+// is also taken on the device: after each walk seqnorm_decide applies the
+// reference's test to the batch's errors and keeps the first breaking
+// iteration in the stop word, and every later triple and norm kernel returns
+// at once.  So the host enqueues block b + 1 (chunk_ iterations, whole
+// triples) before it reads block b's sums, and the streams never drain
+// between blocks; and a break never needs a replay: the triple that would
+// overwrite the final iterate t + 1 (with iterate t + 1 + kRing) waits for
+// the walk of iteration t and then finds the stop word set.  The tail of one
+// or two single steps (niter not a multiple of three; the single step does
+// not read the stop word) is enqueued after every earlier block is decided.
+int Registration::run_exact_pipelined(Level &L, int niter, const StepFn &step, int &final_buf,
+                                      const StepFn3M &step3m) {
+    const double npx = (double)L.dx * L.dy;
+    last_err_.clear();
+    constexpr int R = kRing;
+    static_assert(R + 1 <= (int)(sizeof(L.est) / sizeof(L.est[0])), "ring");
+    for (int b = 1; b <= R; b++)
+        if (!L.est[b].p) L.est[b].alloc(L.dx, L.dy);
+    auto slot = [](int j) { return j == 0 ? 0 : 1 + (j - 1) % R; };
+    auto ev = [](hipEvent_t *e, int q) { return e[q % kExactEv]; };
+    int *stop = reinterpret_cast<int *>(d_status_ + kStopWord);
+    OF2D_HIP(hipMemsetAsync(stop, 0x7f, sizeof(int), st_));  // no break yet
+    constexpr int kNoStop = 0x7f7f7f7f;
+    // a block: whole triples, few enough groups that no event of a block being
+    // read is recorded again before it is (two blocks in flight)
+    const int blk = std::min(3 * ((chunk_ + 2) / 3), 3 * (kExactEv / 2 - 4));
+    const int ring2 = 2 * blk;  // the sums' ring: two blocks of iterations
+    hs_.ensure(std::max(chunk_, 64));
+    static const bool sn_debug = std::getenv("OF2D_SN_DEBUG") != nullptr;
+    constexpr int kDbg = 10;
+    DevArray<int> dbg;
+    if (sn_debug) dbg.alloc(kDbg * (size_t)ring2);
+    bool walked[kSeqWs] = {};  // a new loop: each workspace starts from a fresh state
+    std::vector<int> grp_of((size_t)std::max(niter, 1));
+    int g = 0;
+    // iterations [t, t + k) as group g (t a multiple of three)
+    auto enqueue_group = [&](int t, int k) {
+        for (int m = t; m < t + k; m++) grp_of[m] = g;
+        // iterates t + 1 .. t + k overwrite iterates t + 1 - R .. t + k - R,
+        // read by the walks of iterations t - R .. t + k - R
+        for (int q = std::max(t - R, 0), last = -1; q <= t + k - R; q++)
+            if (grp_of[q] != last) {
+                last = grp_of[q];
+                OF2D_HIP(hipStreamWaitEvent(st_, ev(ev_walk_, last), 0));
+            }
+        if (k == 3)
+            step3m(L.est[slot(t)].p, L.est[slot(t + 1)].p, L.est[slot(t + 2)].p,
+                   L.est[slot(t + 3)].p, t);
+        else
+            for (int m = t; m < t + k; m++) step(L.est[slot(m)].p, L.est[slot(m + 1)].p, d_partial_);
+        OF2D_HIP(hipEventRecord(ev(ev_step_, g), st_));
+        SeqnormBatch B;
+        B.K = k;
+        B.stop = stop;
+        B.t0 = t;
+        B.u[0] = L.est[slot(t)].p;
+        for (int i = 0; i < k; i++) {
+            const int w = 3 * (g % kSeqSets) + i;
+            B.u[i + 1] = L.est[slot(t + 1 + i)].p;
+            B.ws[i] = d_seqws_[w].p;
+            B.use_profile[i] = walked[w] && seq_dx_[w] == L.dx && seq_dy_[w] == L.dy;
+            seq_dx_[w] = L.dx;
+            seq_dy_[w] = L.dy;
+            walked[w] = true;
+            B.out[i] = d_seq_.p + 2 * (size_t)((t + i) % ring2);
+            B.dbg[i] = sn_debug ? dbg.p + kDbg * (size_t)((t + i) % ring2) : nullptr;
+        }
+        enqueue_norms(B, L, g, npx, hs_.seqh + 2 * (size_t)(t % ring2));
+        g++;
+    };
+    const int ntrip = niter / 3 * 3;
+    const int nbt = (ntrip + blk - 1) / blk;  // blocks of triples
+    const int nblocks = nbt + (niter > ntrip ? 1 : 0);  // and the tail
+    auto lo_of = [&](int b) { return b < nbt ? b * blk : ntrip; };
+    auto hi_of = [&](int b) { return b < nbt ? std::min((b + 1) * blk, ntrip) : niter; };
+    std::vector<int> gbeg(nblocks + 1, 0);
+    auto enqueue_block = [&](int b) {
+        gbeg[b] = g;
+        if (b < nbt)
+            for (int t = lo_of(b); t < hi_of(b); t += 3) enqueue_group(t, 3);
+        else
+            enqueue_group(ntrip, niter - ntrip);
+        gbeg[b + 1] = g;
+    };
+    // the other streams' work before st_'s next (the next loop rewrites the
+    // ring and the stop word), the status, and the device's break against the
+    // host's
+    auto finish = [&](int tbreak) {
+        for (hipStream_t s : {sn_st_, fx_st_, wk_st_[0], wk_st_[1], wk_st_[2]}) {
+            OF2D_HIP(hipEventRecord(ev_join_, s));
+            OF2D_HIP(hipStreamWaitEvent(st_, ev_join_, 0));
+        }
+        OF2D_HIP(hipMemcpyAsync(hs_.status + 1, stop, sizeof(int), hipMemcpyDeviceToHost, st_));
+        check_status();  // synchronises st_
+        const int dev = static_cast<int>(hs_.status[1]);
+        if (dev != (tbreak >= 0 ? tbreak : kNoStop))
+            throw DeviceError("internal error: the device's Logger break (" + std::to_string(dev) +
+                              ") is not the host's (" + std::to_string(tbreak) + ")");
+    };
+    if (nblocks > 0) enqueue_block(0);
+    for (int b = 0; b < nblocks; b++) {
+        if (b + 1 < nbt) enqueue_block(b + 1);  // one block ahead
+        // block b's sums: the last walk of each walk stream, then its decide
+        for (int q = std::max(gbeg[b + 1] - 3, gbeg[b]); q < gbeg[b + 1]; q++)
+            OF2D_HIP(hipEventSynchronize(ev(ev_walk_, q)));
+        if (sn_debug) {
+            for (int t = lo_of(b); t < hi_of(b); t++) {
+                std::vector<int> h(kDbg);
+                OF2D_HIP(hipMemcpy(h.data(), dbg.p + kDbg * (size_t)(t % ring2), kDbg * sizeof(int),
+                                   hipMemcpyDeviceToHost));
+                std::fprintf(stderr,
+                             "seqnorm %dx%d it %d: resolves %d %d raw %d %d listed %d walk %d %d "
+                             "res %d made %d %d\n",
+                             L.dx, L.dy, t, h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7], h[8],
+                             h[9]);
+            }
+        }
+        for (int t = lo_of(b); t < hi_of(b); t++) {
+            const float *sm = hs_.seqh + 2 * (size_t)(t % ring2);
+            const float err = logger_error(sm[0], sm[1], npx);
+            last_err_.push_back(err);
+            if (verbose_) print("Iteration: %d\tError:%.4f\n", t, (double)err);
+            if (err < 0.001f && t > 1) {  // ImageRegistrationOpticalFlow.cpp:131-134
+                finish(t);
+                final_buf = slot(t + 1);
+                return t + 1;
+            }
+        }
+        if (b + 1 == nbt && nblocks > nbt) enqueue_block(nbt);  // the tail, after the rest
+    }
+    finish(-1);
+    final_buf = slot(niter);
     return niter;
 }
 
@@ -585,7 +756,7 @@ int Registration::loop_hs(Level &L, int niter, float alpha, int &final_buf) {
         })
               : StepFn3(),
         nblk,
-        pairs ? StepFn3M([&](const float2 *src, float2 *d1, float2 *d2, float2 *d3) {
+        pairs ? StepFn3M([&](const float2 *src, float2 *d1, float2 *d2, float2 *d3, int t0) {
             // the exact Logger's triples: every iterate stored (partials unused)
             launch_hs_jacobi3(src, d3, L.dI.p, L.It.p, L.P, L.dx, L.dy, 0, L.dy, alphasq, -1,
                               L.dy + 1, d_partial_, d_partial_ + (size_t)nb * 2,
@@ -593,7 +764,7 @@ int Registration::loop_hs(Level &L, int niter, float alpha, int &final_buf) {
                               (gi_ < 0 ? hs3_gradients_from_image(L.dx, L.dy) : gi_ != 0)
                                   ? L.Iaux.p
                                   : nullptr,
-                              d1, d2);
+                              d1, d2, reinterpret_cast<const int *>(d_status_ + kStopWord), t0);
         })
               : StepFn3M());
 }

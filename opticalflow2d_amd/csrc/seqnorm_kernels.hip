@@ -317,7 +317,15 @@ struct SnJobs {
     const float *s_in[kSnMaxJobs];    // walk: a row slab's predecessors' exact sums
     float *out[kSnMaxJobs];
     int *dbg[kSnMaxJobs];
+    // a loop's break (the first iteration whose Logger error ends it, see
+    // seqnorm_decide): every kernel of a batch whose first iteration t0 lies
+    // past it returns at once (its norms are never read)
+    const int *stop;
+    int t0;
 };
+__device__ __forceinline__ bool sn_stopped(const SnJobs &J) {
+    return J.stop && *J.stop < J.t0;
+}
 
 // segments in flight per wave: a ring of D segment buffers, each reloaded
 // with the segment D ahead right after its own is consumed, so a load has
@@ -592,6 +600,7 @@ __device__ void sn_block_fix(const SnJobs &J, int j, unsigned N, int dimx, int P
 template <int K>
 __global__ __launch_bounds__(kSnThreads) __attribute__((amdgpu_waves_per_eu(OF2D_SN_WPE)))
 void seqnorm_tables(unsigned N, int dimx, int P, unsigned nt, SnJobs J) {
+    if (sn_stopped(J)) return;
     if (blockIdx.x == 0 && threadIdx.x < 4)
 #pragma unroll
         for (int i = 0; i < K; i++) J.ws[i].cnt[threadIdx.x] = 0;  // seqnorm_check's list
@@ -661,6 +670,7 @@ __device__ __forceinline__ double sn_drift(const SnWs &ws, unsigned nt, int src,
     return (q > 0.0 && f > 0.0 && f < INFINITY) ? f / q : 1.0;
 }
 __global__ __launch_bounds__(kSnChk) void seqnorm_check_sums(unsigned nt, SnJobs J) {
+    if (sn_stopped(J)) return;
     const SnWs &ws = J.ws[blockIdx.y];
     const int use_prof = J.use_prof[blockIdx.y];
     const unsigned b = blockIdx.x * kSnChk + threadIdx.x;
@@ -684,6 +694,7 @@ __global__ __launch_bounds__(kSnChk) void seqnorm_check_sums(unsigned nt, SnJobs
 // predecessors: the prediction is of the global running sum); Pp[nt] <- the
 // total
 __global__ __launch_bounds__(kSnScan) void seqnorm_check_scan(unsigned nt, unsigned nb, SnJobs J) {
+    if (sn_stopped(J)) return;
     const SnWs &ws = J.ws[blockIdx.y];
     const double *p_off = J.p_off[blockIdx.y];
     const unsigned chunk = (nb + kSnScan - 1) / kSnScan;
@@ -738,6 +749,7 @@ __global__ __launch_bounds__(kSnScan) void seqnorm_check_scan(unsigned nt, unsig
     }
 }
 __global__ __launch_bounds__(kSnChk) void seqnorm_check(unsigned nt, SnJobs J) {
+    if (sn_stopped(J)) return;
     const SnWs &ws = J.ws[blockIdx.y];
     const int use_prof = J.use_prof[blockIdx.y];
     const unsigned b = blockIdx.x * kSnChk + threadIdx.x;
@@ -827,6 +839,7 @@ __global__ void seqnorm_offset_chain(const double *__restrict__ prev_nxt, SnTota
 // the listed tiles of pair blockIdx.y: new tile entries, one block per tile
 __global__ __launch_bounds__(kSnThreads) void seqnorm_fix(unsigned N, int dimx, int P,
                                                          unsigned nt, SnJobs J) {
+    if (sn_stopped(J)) return;
     const int j = blockIdx.y;
     const unsigned cnt = J.ws[j].cnt[0];
     for (unsigned k = blockIdx.x; k < cnt; k += gridDim.x) {  // block-uniform
@@ -1126,6 +1139,7 @@ constexpr int kSnAhead = 8;  // windows loaded per step: the next step's loads h
 // resolve clocks, tiles given the walk's own segment entries (per norm).
 __global__ __launch_bounds__(64 * kSnWalkWaves) void seqnorm_walk(unsigned N, int dimx, int P,
                                                                    unsigned nt, SnJobs J) {
+    if (sn_stopped(J)) return;  // before the barrier, the whole block
     const int job = blockIdx.x >> 1;
     const int n = blockIdx.x & 1;  // 0: |cur - prev|, 1: |prev|
     const int lane = threadIdx.x & 63;
@@ -1252,6 +1266,23 @@ __global__ __launch_bounds__(64 * kSnWalkWaves) void seqnorm_walk(unsigned N, in
     }
 }
 
+// The loop's break on the device: the Logger error of each pair of a walked
+// batch, as the host's logger_error (registration.cpp; Logger.cpp:37-39 and
+// ImageRegistrationOpticalFlow.cpp:131-134: error < 0.001 and iteration > 1),
+// the first breaking iteration into *stop (atomicMin, so batches may finish
+// in any order), and the sums copied to the host's mapped mirror.
+__global__ void seqnorm_decide(const float *__restrict__ seq, int K, int t0, float npx,
+                               int *__restrict__ stop, float *__restrict__ host) {
+    const int i = threadIdx.x;
+    if (i >= K) return;
+    const float sd = seq[2 * i], sp = seq[2 * i + 1];
+    host[2 * i] = sd;
+    host[2 * i + 1] = sp;
+    const float prevnorm = sp / npx, diffnorm = sd / npx;
+    const float err = prevnorm == 0.0f ? 0.0f : diffnorm / prevnorm;
+    if (err < 0.001f && t0 + i > 1) atomicMin(stop, t0 + i);
+}
+
 }  // namespace
 
 size_t seqnorm_workspace_bytes(int dimx, int dimy) {
@@ -1307,6 +1338,8 @@ SnJobs jobs_of(const SeqnormBatch &B, unsigned nt) {
         J.out[i] = B.out[i];
         J.dbg[i] = B.dbg[i];
     }
+    J.stop = B.stop;
+    J.t0 = B.t0;
     return J;
 }
 }  // namespace
@@ -1344,6 +1377,15 @@ void launch_seqnorm_walk(const SeqnormBatch &B, int dimx, int dimy, int P, hipSt
     const unsigned N = (unsigned)((size_t)dimx * dimy);
     hipLaunchKernelGGL(seqnorm_walk, dim3(2 * B.K), dim3(64 * kSnWalkWaves), 0, st, N, dimx, P, nt,
                        jobs_of(B, nt));
+    OF2D_HIP(hipGetLastError());
+}
+
+void launch_seqnorm_decide(const float *seq, int K, int t0, double npx, int *stop, float *host,
+                           hipStream_t st) {
+    if (K < 1 || K > kSnMaxJobs || !seq || !stop || !host)
+        throw std::invalid_argument("launch_seqnorm_decide: arguments");
+    hipLaunchKernelGGL(seqnorm_decide, dim3(1), dim3(64), 0, st, seq, K, t0, (float)npx, stop,
+                       host);
     OF2D_HIP(hipGetLastError());
 }
 

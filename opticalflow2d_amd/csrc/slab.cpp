@@ -68,7 +68,12 @@ struct of2d_slab {
     hipEvent_t ev_int = nullptr, ev_edge = nullptr;
     ncclComm_t comm = nullptr;
     of2d_slab_group *grp = nullptr;  // in-process transport instead of RCCL
-    hipEvent_t ev_ready = nullptr, ev_done = nullptr;  // its exchange handshakes
+    hipEvent_t ev_ready = nullptr, ev_done = nullptr;  // its all-reduce handshakes
+    // its halo handshakes (local_exchange): a ring of event pairs, one per
+    // exchange in flight, and the exchanges it has enqueued over its life
+    static constexpr int kXr = 4;
+    hipEvent_t ev_xr[kXr] = {}, ev_xd[kXr] = {};
+    long nx = 0;
     double *d_red = nullptr;  // its all-reduce result staging
     of2d::Field<float2> u[3];
     of2d::Field<float2> dI;
@@ -120,6 +125,10 @@ struct of2d_slab_group {
     // (the next rank waits for its neighbour's count before waiting on the
     // neighbour's event); groups are counted over the slabs' lifetime
     std::unique_ptr<std::atomic<long>[]> off_done, walk_done;
+    // halo exchanges (local_exchange): per rank, the exchanges whose ready /
+    // done record it has enqueued, and the buffer it published for each slot
+    std::unique_ptr<std::atomic<long>[]> xr_ready, xr_done;
+    std::vector<const void *> xptr;  // [rank * kXr + slot]
     std::mutex m;
     std::condition_variable cv;
     int arrived = 0;
@@ -165,37 +174,60 @@ int sguard(of2d_slab *s, F &&f) {
     }
 }
 
-// in-process transport: every rank publishes `u` once its boundary lines are
-// final (ev_ready), pulls its neighbours' lines into its own ghost lines, and
-// does not run ahead until the neighbours have pulled from it (ev_done)
+// in-process group: wait until `cnt` (a rank's count of enqueued records)
+// passes x
+void wait_count(const std::atomic<long> &cnt, long x, const char *what) {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (int spin = 0; cnt.load(std::memory_order_acquire) <= x; spin++) {
+        if (spin > 64) std::this_thread::yield();
+        if ((spin & 1023) == 1023 &&
+            std::chrono::steady_clock::now() - t0 > std::chrono::seconds(60))
+            throw std::runtime_error(std::string("slab group: a rank did not reach the ") + what);
+    }
+}
+
+// in-process transport, point to point: every rank publishes `u` once its
+// boundary lines are final (its ready record of exchange x), pulls its
+// neighbours' lines into its own ghost lines, and does not run ahead until the
+// neighbours have pulled from it (their done records).  The host threads meet
+// only their neighbours and only to see an event RECORDED (enqueued), never
+// completed, so each runs ahead enqueueing whole chunks; the event pairs are a
+// ring of kXr, which is safe from x + 1 on: a rank publishes done(x) after
+// its wait on the neighbour's ready(x) was enqueued, and waits for the
+// neighbours' done(x) before its exchange x + 1.
 void local_exchange(of2d_slab *s, float2 *u, int lines, size_t cnt, hipStream_t st) {
     of2d_slab_group *g = s->grp;
+    constexpr int kXr = of2d_slab::kXr;
     const long P = s->P;
     const size_t bytes = cnt * sizeof(float);
-    OF2D_HIP(hipEventRecord(s->ev_ready, st));
-    g->ptr[s->rank] = u;
-    g->barrier();
+    const long x = s->nx++;
+    const int k = (int)(x % kXr);
     for (int r = 0; r < s->nranks; r++)
         if (!g->slabs[r]) throw std::invalid_argument("slab group: not every rank was created");
-    if (s->rank > 0) {
-        const of2d_slab *up = g->slabs[s->rank - 1];
-        const float2 *src = static_cast<const float2 *>(g->ptr[s->rank - 1]);
-        OF2D_HIP(hipStreamWaitEvent(st, up->ev_ready, 0));
-        OF2D_HIP(hipMemcpyAsync(u - lines * P, src + (long)(up->nrows - lines) * P, bytes,
-                                hipMemcpyDeviceToDevice, st));
+    OF2D_HIP(hipEventRecord(s->ev_xr[k], st));
+    g->xptr[(size_t)s->rank * kXr + k] = u;
+    g->xr_ready[s->rank].store(x + 1, std::memory_order_release);
+    const int nbr[2] = {s->rank - 1, s->rank + 1};
+    for (int q : nbr) {
+        if (q < 0 || q >= s->nranks) continue;
+        wait_count(g->xr_ready[q], x, "halo exchange");
+        const of2d_slab *o = g->slabs[q];
+        const float2 *src = static_cast<const float2 *>(g->xptr[(size_t)q * kXr + k]);
+        OF2D_HIP(hipStreamWaitEvent(st, o->ev_xr[k], 0));
+        if (q < s->rank)  // its last lines into the ghost lines above row 0
+            OF2D_HIP(hipMemcpyAsync(u - lines * P, src + (long)(o->nrows - lines) * P, bytes,
+                                    hipMemcpyDeviceToDevice, st));
+        else  // its first lines below the last row
+            OF2D_HIP(hipMemcpyAsync(u + (long)s->nrows * P, src, bytes, hipMemcpyDeviceToDevice,
+                                    st));
     }
-    if (s->rank < s->nranks - 1) {
-        const of2d_slab *dn = g->slabs[s->rank + 1];
-        const float2 *src = static_cast<const float2 *>(g->ptr[s->rank + 1]);
-        OF2D_HIP(hipStreamWaitEvent(st, dn->ev_ready, 0));
-        OF2D_HIP(hipMemcpyAsync(u + (long)s->nrows * P, src, bytes, hipMemcpyDeviceToDevice,
-                                st));
+    OF2D_HIP(hipEventRecord(s->ev_xd[k], st));
+    g->xr_done[s->rank].store(x + 1, std::memory_order_release);
+    for (int q : nbr) {
+        if (q < 0 || q >= s->nranks) continue;
+        wait_count(g->xr_done[q], x, "halo exchange");
+        OF2D_HIP(hipStreamWaitEvent(st, g->slabs[q]->ev_xd[k], 0));
     }
-    OF2D_HIP(hipEventRecord(s->ev_done, st));
-    g->barrier();
-    if (s->rank > 0) OF2D_HIP(hipStreamWaitEvent(st, g->slabs[s->rank - 1]->ev_done, 0));
-    if (s->rank < s->nranks - 1)
-        OF2D_HIP(hipStreamWaitEvent(st, g->slabs[s->rank + 1]->ev_done, 0));
 }
 
 // `lines` (1..3) boundary j-lines to each neighbour, on stream `st`
@@ -405,14 +437,7 @@ void exact_setup(of2d_slab *s) {
 }
 
 // in-process group: wait until rank r has enqueued group g's record of `done`
-void wait_rank(const std::atomic<long> &done, long g) {
-    const auto t0 = std::chrono::steady_clock::now();
-    while (done.load(std::memory_order_acquire) <= g) {
-        std::this_thread::yield();
-        if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(60))
-            throw std::runtime_error("slab group: a rank did not reach the Logger chain");
-    }
-}
+void wait_rank(const std::atomic<long> &done, long g) { wait_count(done, g, "Logger chain"); }
 
 // The convergence-on run with the reference's Logger; *done = iterations
 int run_exact(of2d_slab *s, int niter) {
@@ -627,6 +652,10 @@ static int slab_create(of2d_slab **out, int dimx, int dimy, float alpha, int ran
             if (grp->n != nranks) throw std::invalid_argument("slab: group size != nranks");
             OF2D_HIP(hipEventCreateWithFlags(&s->ev_ready, hipEventDisableTiming));
             OF2D_HIP(hipEventCreateWithFlags(&s->ev_done, hipEventDisableTiming));
+            for (int k = 0; k < of2d_slab::kXr; k++) {
+                OF2D_HIP(hipEventCreateWithFlags(&s->ev_xr[k], hipEventDisableTiming));
+                OF2D_HIP(hipEventCreateWithFlags(&s->ev_xd[k], hipEventDisableTiming));
+            }
             OF2D_HIP(hipMalloc(&s->d_red, sizeof(double) * 2 * (size_t)s->chunk_cap()));
             std::lock_guard<std::mutex> lk(grp->m);
             if (grp->slabs[rank]) throw std::invalid_argument("slab: rank already in the group");
@@ -663,9 +692,14 @@ int of2d_slab_group_create(of2d_slab_group **out, int nranks) {
     g->slabs.assign(nranks, nullptr);
     g->ptr.assign(nranks, nullptr);
     g->flag.assign(nranks, 0);
+    g->xptr.assign((size_t)nranks * of2d_slab::kXr, nullptr);
+    g->xr_ready.reset(new std::atomic<long>[nranks]);
+    g->xr_done.reset(new std::atomic<long>[nranks]);
     g->off_done.reset(new std::atomic<long>[nranks]);
     g->walk_done.reset(new std::atomic<long>[nranks]);
     for (int r = 0; r < nranks; r++) {
+        g->xr_ready[r] = 0;
+        g->xr_done[r] = 0;
         g->off_done[r] = 0;
         g->walk_done[r] = 0;
     }
@@ -1120,6 +1154,10 @@ int of2d_slab_destroy(of2d_slab *s) {
     }
     if (s->ev_ready) (void)hipEventDestroy(s->ev_ready);
     if (s->ev_done) (void)hipEventDestroy(s->ev_done);
+    for (int k = 0; k < of2d_slab::kXr; k++) {
+        if (s->ev_xr[k]) (void)hipEventDestroy(s->ev_xr[k]);
+        if (s->ev_xd[k]) (void)hipEventDestroy(s->ev_xd[k]);
+    }
     if (s->d_red) (void)hipFree(s->d_red);
     if (s->d_partial) (void)hipFree(s->d_partial);
     if (s->d_sums) (void)hipFree(s->d_sums);

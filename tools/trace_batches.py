@@ -67,3 +67,14 @@ for f, iv in sorted(by.items(), key=lambda kv: -union(kv[1])):
         print(f"  {f:16s} busy {u / nb / 1e3:7.1f} us per batch ({100 * u / span:5.1f} %), {n / nb:.2f} launches per batch")
 allb = union([(a, b) for a, b, f, q in rows])
 print(f"  {'any kernel':16s} busy {allb / nb / 1e3:7.1f} us per batch; idle {100 * (1 - allb / span):.1f} %")
+
+# a few consecutive batches in the middle of the run: each launch's start and
+# end relative to the first mid launch shown (us), by queue
+if len(sys.argv) > 2:
+    k0 = len(best) // 2
+    a0 = best[k0][0]
+    a1 = best[min(k0 + int(sys.argv[2]), len(best) - 1)][0]
+    print(f"\ntimeline from mid launch {k0} ({a0}), us:")
+    for a, b, f, q in rows:
+        if b > a0 and a < a1:
+            print(f"  q{q:>3} {f:16s} {(a - a0) / 1e3:8.1f} .. {(b - a0) / 1e3:8.1f}  ({(b - a) / 1e3:6.1f})")
