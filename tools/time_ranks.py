@@ -4,7 +4,9 @@ iterations and convergence on (the reference-exact Logger).  On a one-GPU box
 every rank runs on device 0, so the figures are the path's overhead at equal
 total work.
 
-    python tools/time_ranks.py [n] [reps]
+    python tools/time_ranks.py [n] [reps] [modes] [ngpus]
+
+modes: "fixed,conv" (default both); ngpus: comma list (default 1,2,8).
 """
 import os
 import sys
@@ -17,10 +19,14 @@ from opticalflow2d_amd import synthetic as S  # noqa: E402
 set_print_sink(lambda s: None)
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
 reps = int(sys.argv[2]) if len(sys.argv) > 2 else 3
+modes = sys.argv[3].split(",") if len(sys.argv) > 3 else ["fixed", "conv"]
+ngs = [int(v) for v in sys.argv[4].split(",")] if len(sys.argv) > 4 else [1, 2, 8]
 ref, mov = S.texture_pair(n)
 for mode, opts, niter in (("fixed 999", {"fixed_iters": 1}, 999), ("convergence", {}, 1000)):
+    if mode.split()[0][:4] not in [m[:4] for m in modes]:
+        continue
     base = None
-    for ng in (1, 2, 8):
+    for ng in ngs:
         with ImageRegistration((n, n), [niter], 0, 0, [0.1], ngpus=ng, **opts) as r:
             r.set_images(ref, mov)
             r.estimate()  # warm-up (allocations, the ranks' threads' first launches)
