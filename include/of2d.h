@@ -98,7 +98,12 @@ int of2d_last_errors(const of2d_ctx *ctx, float *out, int cap);
  *   the Logger's running sums cross the ranks by peer copies; the pyramid,
  *   warps and accumulation stay on the registration's device).  Results are
  *   the one-device results bit for bit with the default Logger norms.  Levels
- *   with fewer j-lines than ranks run on one device.
+ *   with fewer j-lines than ranks run on one device.  Ranks beyond the device
+ *   count are merged (a device runs one slab of rows; splitting it only adds
+ *   halo work) unless "ngpus_share" is set.
+ *   "ngpus_share" (0 = default / 1): ranks may share a device, (device + r)
+ *   mod count for every r < ngpus (the decomposition on fewer devices than
+ *   ranks: tests, timings of the path's overhead on one GPU).
  *   "logger_fp64" (0 = default / 1): 0 computes the Logger norms as the
  *   reference does (float running sums, of2d_motion_norms), so the break of
  *   ImageRegistrationOpticalFlow.cpp:131-134 falls on the reference's

@@ -10,6 +10,7 @@
 // iterations to take the convergence decision.
 #pragma once
 
+#include <algorithm>
 #include <cstdarg>
 #include <functional>
 #include <memory>
@@ -176,6 +177,12 @@ class Registration {
     MultiHS &multi_for(int s, float alpha);
     void multi_release();
     int ngpus_ = 1;
+    // ranks may share a device (option "ngpus_share"; tests of the
+    // decomposition on one GPU); otherwise at most one rank per device: a
+    // device's rows in one slab, as splitting them only adds halo work
+    bool share_ = false;
+    int ndev_ = 1;
+    int ranks() const { return share_ ? ngpus_ : std::min(ngpus_, ndev_); }
     std::vector<std::shared_ptr<MultiHS>> lv_multi_;
     void check_status();
     void check_reported_status(unsigned st);

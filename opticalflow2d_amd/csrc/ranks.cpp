@@ -96,7 +96,7 @@ MultiHS &Registration::multi_for(int s, float alpha) {
     m->alpha = alpha;
     int count = 0;
     OF2D_HIP(hipGetDeviceCount(&count));
-    const int n = ngpus_;
+    const int n = ranks();
     if (n > kMaxLocalRanks) throw std::invalid_argument("ngpus: at most 16 ranks");
     std::vector<int> devs;
     for (int k = 0; k < n; k++) {

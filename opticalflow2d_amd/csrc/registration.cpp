@@ -177,6 +177,10 @@ void Registration::set_option(const std::string &key, double v) {
         if ((int)v != ngpus_) multi_release();
         ngpus_ = (int)v;
     }
+    else if (key == "ngpus_share") {
+        if ((v != 0) != share_) multi_release();
+        share_ = v != 0;
+    }
     else if (key == "chunk") {
         if (ready_) throw std::invalid_argument("option 'chunk' must be set before first use");
         chunk_ = std::max(1, (int)v);
@@ -197,6 +201,7 @@ void Registration::ensure_device() {
     }
     if (device_ >= 0) OF2D_HIP(hipSetDevice(device_));
     OF2D_HIP(hipGetDevice(&home_));
+    OF2D_HIP(hipGetDeviceCount(&ndev_));
     OF2D_HIP(hipStreamCreateWithFlags(&st_, hipStreamNonBlocking));
     OF2D_HIP(hipStreamCreateWithFlags(&sn_st_, hipStreamNonBlocking));
     // the fix and the walks at high priority: they are the latency chain that
@@ -314,7 +319,8 @@ void Registration::estimate_level(int s) {
         launch_warp(L.Imov.p, L.cur_motion(), L.Iaux.p, L.dx, L.dy, L.P, st_);
         // HS over several devices: the ranks take their gradients themselves
         // (the slabs need >= 3 j-lines each: coarser levels run on one device)
-        const bool multi = reg_ == 0 && ngpus_ > 1 && L.dy >= 3 * ngpus_ && L.dx >= 3;
+        const int nr = ranks();
+        const bool multi = reg_ == 0 && nr > 1 && L.dy >= 3 * nr && L.dx >= 3;
         if (!demons && !multi)
             launch_gradients(L.Iref.p, L.Iaux.p, L.dI.p, L.It.p, L.dx, L.dy, L.P, st_);
         L.est[0].zero(st_);  // motion_est starts at zero (reset() at :141 / new Motion)

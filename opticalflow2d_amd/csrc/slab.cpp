@@ -296,9 +296,9 @@ void allreduce_sums(of2d_slab *s, double *buf, size_t count, hipStream_t st) {
         if (r != s->rank) OF2D_HIP(hipStreamWaitEvent(st, g->slabs[r]->ev_done, 0));
     OF2D_HIP(hipMemcpyAsync(buf, s->d_red, count * sizeof(double), hipMemcpyDeviceToDevice, st));
 }
-// Launch geometry of a slab's triples.  With neighbours and at least 3E
-// j-lines the launch is split (see fused in of2d_slab_run): interior j-lines
-// [E, nrows-E) with a block budget that leaves room for the two edge launches
+// Launch geometry of a slab's triples.  With neighbours on other devices (or
+// over RCCL) and at least 3E j-lines the launch is split (see fused in
+// of2d_slab_run): interior j-lines [E, nrows-E) with a block budget that leaves room for the two edge launches
 // of E = 16 j-lines (4 waves x 4 lines, one block per strip) and for the RCCL
 // send/recv kernel (kCommBlocks) to be resident beside it.  At 4096 x 4096 per
 // rank: 27 x 38-line interior bands (945 blocks) + 2 x 35 edge blocks, 104 us
@@ -333,10 +333,22 @@ void reserve_sums(of2d_slab *s, int niter) {
     s->hs.ensure((niter + 1) / 2);  // 4 doubles per unit of capacity
 }
 
+// an exchange partner of this slab is on another device, or behind RCCL (the
+// split launches hide the exchange's latency; between slabs of one device it
+// is a local copy of a few lines, cheaper than the edge launches: 16 of 11.5
+// us per triple at 8 ranks on one device, profiles/r04n_ranks8_fixed_kernel_stats.csv)
+bool remote_neighbour(const of2d_slab *s) {
+    if (!s->grp) return s->nranks > 1;
+    for (int q : {s->rank - 1, s->rank + 1})
+        if (q >= 0 && q < s->nranks && s->grp->slabs[q] && s->grp->slabs[q]->device != s->device)
+            return true;
+    return false;
+}
+
 SlabGeometry slab_geometry(const of2d_slab *s) {
     SlabGeometry g;
     const int gx = (s->dimx + of2d::kHs3Out - 1) / of2d::kHs3Out;
-    g.split = s->nranks > 1 && s->nrows >= 3 * g.E && s->dimx >= 2;
+    g.split = s->nranks > 1 && s->nrows >= 3 * g.E && s->dimx >= 2 && remote_neighbour(s);
     if (g.split) {
         const int ni = s->nrows - 2 * g.E;
         constexpr int kCommBlocks = 8;

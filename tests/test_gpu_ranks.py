@@ -1,9 +1,11 @@
 """Multi-device Horn-Schunck through the drop-in boundary (of2d_set_option
 "ngpus", the gateway's ninth init argument; opticalflow2d_amd/csrc/ranks.cpp).
 
-On a one-GPU box every rank runs on device 0 ((device + r) mod count), which
-exercises the partition, the halo copies, the prediction offsets and the
-chained Logger walks exactly as on N devices.  Bar: iterations, motion and
+By default at most one rank runs per device (ranks beyond the device count
+merge: a device's rows in one slab); with "ngpus_share" every rank r runs on
+device (device + r) mod count, so on a one-GPU box all of them share device 0,
+which exercises the partition, the halo copies, the prediction offsets and
+the chained Logger walks exactly as on N devices.  Bar: iterations, motion and
 every Logger error bit-identical to the one-rank registration with the
 default (reference-exact) Logger; with convergence on, a pyramid and refines
 (ImageRegistration.cpp:133-156, ImageRegistrationOpticalFlow.cpp:97-151).
@@ -33,7 +35,7 @@ def test_pyramid_refines_convergence_bitwise(gpu, ngpus):
     ref, mov = S.texture_pair(256, seed=4, ny=200)
     args = ((256, 200), [300, 200, 200], 2, [0.1], 2, ref, mov)
     it1, m1, e1, w1 = run(*args)
-    itn, mn, en, wn = run(*args, ngpus=ngpus)
+    itn, mn, en, wn = run(*args, ngpus=ngpus, ngpus_share=1)
     assert itn == it1
     assert np.array_equal(mn, m1)
     assert np.array_equal(wn, w1)
@@ -46,7 +48,7 @@ def test_ragged_fixed_iterations(gpu, dims, ngpus):
     ref = rng.random(dims)
     mov = np.roll(ref, 1, axis=0) * 0.9 + 0.05
     a = run(dims, [25], 0, [0.3], 1, ref, mov, fixed_iters=1)
-    b = run(dims, [25], 0, [0.3], 1, ref, mov, fixed_iters=1, ngpus=ngpus)
+    b = run(dims, [25], 0, [0.3], 1, ref, mov, fixed_iters=1, ngpus=ngpus, ngpus_share=1)
     assert np.array_equal(a[1], b[1])
 
 
@@ -55,7 +57,7 @@ def test_fp64_logger_mode_motion(gpu):
     differ from one rank's in the last bits, the iterates do not."""
     ref, mov = S.texture_pair(192, seed=8)
     a = run((192, 192), [400], 0, [0.1], 1, ref, mov, logger_fp64=1)
-    b = run((192, 192), [400], 0, [0.1], 1, ref, mov, logger_fp64=1, ngpus=3)
+    b = run((192, 192), [400], 0, [0.1], 1, ref, mov, logger_fp64=1, ngpus=3, ngpus_share=1)
     assert a[0] == b[0]
     assert np.array_equal(a[1], b[1])
     np.testing.assert_allclose(b[2], a[2], rtol=1e-5)
@@ -81,7 +83,8 @@ def test_config_scale_reference_break_8_ranks(gpu):
     (tests/golden/convergence_hs_texture4096.json)."""
     fx = json.load(open(os.path.join(GOLDEN, "convergence_hs_texture4096.json")))
     ref, mov = S.texture_pair(4096)
-    it, m, e, _ = run((4096, 4096), fx["niter"], 0, [fx["alpha"]], 1, ref, mov, ngpus=8)
+    it, m, e, _ = run((4096, 4096), fx["niter"], 0, [fx["alpha"]], 1, ref, mov, ngpus=8,
+                      ngpus_share=1)
     assert it == fx["iterations_executed"]
     f = np.asarray(m, np.float32)
     planar = np.concatenate([f[:, :, 0].reshape(-1, order="F"), f[:, :, 1].reshape(-1, order="F")])
@@ -102,6 +105,21 @@ def test_ranks_on_distinct_devices(gpu):
     args = ((256, 200), [300], 0, [0.1], 1, ref, mov)
     for opts in ({}, {"logger_fp64": 1}, {"fixed_iters": 1}):
         a = run(*args, **opts)
-        b = run(*args, ngpus=4, **opts)
+        b = run(*args, ngpus=4, ngpus_share=1, **opts)
         assert a[0] == b[0]
         assert np.array_equal(a[1], b[1])
+
+
+def test_ranks_beyond_devices_merge(gpu):
+    """Default: ngpus above the device count runs one slab per device (on a
+    one-GPU box the one-device loop), the same bits either way."""
+    import torch
+    ref, mov = S.texture_pair(256, seed=9, ny=200)
+    args = ((256, 200), [300], 0, [0.1], 1, ref, mov)
+    a = run(*args)
+    b = run(*args, ngpus=torch.cuda.device_count() + 3)
+    c = run(*args, ngpus=torch.cuda.device_count() + 3, ngpus_share=1)
+    for x in (b, c):
+        assert x[0] == a[0]
+        assert np.array_equal(x[1], a[1])
+        assert x[2].view(np.uint32).tolist() == a[2].view(np.uint32).tolist()

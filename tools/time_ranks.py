@@ -1,8 +1,9 @@
 """Wall time per iteration of the in-process multi-device HS path
 (of2d_set_option "ngpus", csrc/ranks.cpp) at 4096^2 against one rank: fixed
-iterations and convergence on (the reference-exact Logger).  On a one-GPU box
-every rank runs on device 0, so the figures are the path's overhead at equal
-total work.
+iterations and convergence on (the reference-exact Logger).  Each count runs
+with the default (ranks beyond the device count merge: on a one-GPU box the
+one-device loop) and with "ngpus_share" (every rank on device 0 of a one-GPU
+box: the decomposition's overhead at equal total work).
 
     python tools/time_ranks.py [n] [reps] [modes] [ngpus]
 
@@ -26,8 +27,9 @@ for mode, opts, niter in (("fixed 999", {"fixed_iters": 1}, 999), ("convergence"
     if mode.split()[0][:4] not in [m[:4] for m in modes]:
         continue
     base = None
-    for ng in ngs:
-        with ImageRegistration((n, n), [niter], 0, 0, [0.1], ngpus=ng, **opts) as r:
+    for ng, share in [(g, sh) for g in ngs for sh in ((0,) if g == 1 else (0, 1))]:
+        with ImageRegistration((n, n), [niter], 0, 0, [0.1], ngpus=ng, ngpus_share=share,
+                               **opts) as r:
             r.set_images(ref, mov)
             r.estimate()  # warm-up (allocations, the ranks' threads' first launches)
             ts = []
@@ -40,5 +42,5 @@ for mode, opts, niter in (("fixed 999", {"fixed_iters": 1}, 999), ("convergence"
         t = min(ts)
         us = t * 1e6 / it
         base = base or us
-        print(f"{mode:12s} {n}^2 ngpus={ng}: {it} iterations, {t*1e3:.2f} ms "
+        print(f"{mode:12s} {n}^2 ngpus={ng} share={share}: {it} iterations, {t*1e3:.2f} ms "
               f"({us:.1f} us/iteration, {us / base:.3f}x of ngpus=1)", flush=True)
