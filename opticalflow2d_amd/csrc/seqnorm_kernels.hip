@@ -322,6 +322,10 @@ struct SnJobs {
     // past it returns at once (its norms are never read)
     const int *stop;
     int t0;
+    // the pass's scale: the fp64 prefixes (Pp) of the previous batch's first
+    // and last pairs (their checks have run) and its pair count, or null
+    const double *pp_first, *pp_last;
+    int kprev;
 };
 __device__ __forceinline__ bool sn_stopped(const SnJobs &J) {
     return J.stop && *J.stop < J.t0;
@@ -379,7 +383,15 @@ struct SnLoader {
 // sqrt; the exact fp64 sequence in the waves where a lane's estimate does not
 // decide), so a tile entry is one saturating wave sum at the end.  Segment
 // entries come from the fix, for the tiles the check lists.
-template <int K, int NC>
+// a header the refill completes: listed by the check (up to kSnCand
+// candidates)
+__device__ __forceinline__ bool sn_refills(unsigned h) {
+    return (h & kHdrPending) && !(h & (kHdrZero | kHdrNan)) && hdr_nc(h) > 0;
+}
+// RF (seqnorm_refill): hd are the check's headers; only the pending norms with
+// at most NC candidates take entries (T and the header, pending cleared), the
+// others are left as they are, and A / Z (the pass's) are not written again.
+template <int K, int NC, bool RF = false>
 __device__ __forceinline__ void sn_wave_pass(const SnJobs &J, unsigned N, int dimx, int P,
                                              unsigned nt, unsigned b, const unsigned (&hd)[K][2]) {
     const int lane = threadIdx.x & 63;
@@ -389,7 +401,7 @@ __device__ __forceinline__ void sn_wave_pass(const SnJobs &J, unsigned N, int di
     for (int i = 0; i < K; i++)
 #pragma unroll
         for (int n = 0; n < 2; n++) {
-            nc[i][n] = hdr_nc(hd[i][n]);
+            nc[i][n] = (!RF || sn_refills(hd[i][n])) ? hdr_nc(hd[i][n]) : 0;
             // a candidate the header does not have gets scale 0: its
             // increments are 0 and decided, so every term computes all of them
             // without a branch
@@ -479,7 +491,8 @@ __device__ __forceinline__ void sn_wave_pass(const SnJobs &J, unsigned N, int di
         const SnWs &ws = J.ws[i];
 #pragma unroll
         for (int n = 0; n < 2; n++) {
-            unsigned hh = hd[i][n];
+            if (RF && !sn_refills(hd[i][n])) continue;
+            unsigned hh = RF ? (hd[i][n] & ~kHdrPending) : hd[i][n];
             if (NC > 0) {
                 unsigned tv = 0u;
                 bool anybad = false;
@@ -495,6 +508,10 @@ __device__ __forceinline__ void sn_wave_pass(const SnJobs &J, unsigned N, int di
                 }
                 if (lane < nc[i][n]) ws.T[(2 * (size_t)b + n) * kSnCand + lane] = tv;
                 (void)anybad;  // a tie or NaN: the entry fails in the walk, which resolves it
+            }
+            if (RF) {
+                if (lane == 0) ws.H[2 * (size_t)b + n] = hh;
+                continue;
             }
             const double a = wave_reduce((double)fs[i][n], [](double p, double x) { return p + x; });
             const unsigned long long zm = sn_ballot(zv[i][n]);
@@ -616,13 +633,30 @@ void seqnorm_tables(unsigned N, int dimx, int P, unsigned nt, SnJobs J) {
         for (int n = 0; n < 2; n++) {
             unsigned h = hdr_pack(0, 0);
             if (J.use_prof[i]) {
-                // the last call's running sums scaled by the trend of its
-                // totals (|cur - prev| shrinks from update to update)
+                // the last call's running sums (their shape across the grid
+                // moves little: > 99 % of the tiles within 5 % over twelve
+                // updates early in the 4096^2 texture loop) scaled to this
+                // pair's total: extrapolated from the previous batch's fp64
+                // totals at its rate per update, or else the trend of the
+                // workspace's own totals (|cur - prev| shrinks from update to
+                // update)
                 const int src = prof_src(ws, n);
                 const float *pr = ws.prof + (size_t)src * (nt + 1);
-                const float t0 = ws.tot[2 * src], t1 = ws.tot[2 * src + 1];
-                double r = (src == n && t1 > 0.0f && t0 > 0.0f) ? (double)t0 / t1 : 1.0;
-                r = r < 0.25 ? 0.25 : (r > 4.0 ? 4.0 : r);
+                const double told = ws.Pp[(size_t)src * (nt + 1) + nt];
+                const double tl = J.pp_last ? J.pp_last[(size_t)n * (nt + 1) + nt] : 0.0;
+                const double tf = J.pp_first ? J.pp_first[(size_t)n * (nt + 1) + nt] : 0.0;
+                double r;
+                if (tl > 0.0 && told > 0.0 && tl < INFINITY) {
+                    const double rho = (J.kprev > 1 && tf > 0.0 && tf < INFINITY)
+                                           ? pow(tl / tf, 1.0 / (J.kprev - 1))
+                                           : 1.0;
+                    r = tl * pow(rho, (double)(i + 1)) / told;
+                    r = r < 0x1p-10 ? 0x1p-10 : (r > 0x1p10 ? 0x1p10 : r);
+                } else {
+                    const float t0 = ws.tot[2 * src], t1 = ws.tot[2 * src + 1];
+                    r = (src == n && t1 > 0.0f && t0 > 0.0f) ? (double)t0 / t1 : 1.0;
+                    r = r < 0.25 ? 0.25 : (r > 4.0 ? 4.0 : r);
+                }
                 h = cand_window((double)pr[b] * r * (1.0 - kSnWin),
                                 (double)pr[b + 1] * r / (1.0 - kSnWin));
             }
@@ -646,6 +680,39 @@ void seqnorm_tables(unsigned N, int dimx, int P, unsigned nt, SnJobs J) {
     if (ncmax == 0) sn_wave_pass<K, 0>(J, N, dimx, P, nt, b, hd);
     else if (ncmax == 1) sn_wave_pass<K, 1>(J, N, dimx, P, nt, b, hd);
     else sn_wave_pass<K, 2>(J, N, dimx, P, nt, b, hd);
+}
+
+// The check's listed tiles, when there are many (a loop's first batches,
+// which have no profile, or a misprediction): one wave per tile reads the
+// batch's K + 1 iterates once and makes the entries of every pending norm,
+// as the pass does — 4 arrays per tile against the fix's 2 per listed pair,
+// and the pass's lane-sum form.  Runs only when a pair of the batch listed
+// more than kSnRefillMin tiles; the fix then finds nothing pending.
+constexpr unsigned kSnRefillMin = 512;
+template <int K>
+__global__ __launch_bounds__(kSnThreads) __attribute__((amdgpu_waves_per_eu(OF2D_SN_WPE)))
+void seqnorm_refill(unsigned N, int dimx, int P, unsigned nt, SnJobs J) {
+    if (sn_stopped(J)) return;
+    bool many = false;
+#pragma unroll
+    for (int i = 0; i < K; i++) many |= J.ws[i].cnt[0] > kSnRefillMin;
+    if (!many) return;
+    const unsigned b = (unsigned)__builtin_amdgcn_readfirstlane(
+        (int)(blockIdx.x * (kSnThreads / 64) + threadIdx.x / 64));
+    if (b >= nt) return;
+    unsigned hd[K][2];
+    int ncmax = 0;
+#pragma unroll
+    for (int i = 0; i < K; i++)
+#pragma unroll
+        for (int n = 0; n < 2; n++) {
+            hd[i][n] = (unsigned)__builtin_amdgcn_readfirstlane((int)J.ws[i].H[2 * (size_t)b + n]);
+            if (sn_refills(hd[i][n])) ncmax = max(ncmax, hdr_nc(hd[i][n]));
+        }
+    // two candidates (the usual window), or up to four (the prefix's wide
+    // window of a loop's first batches)
+    if (ncmax > 2) sn_wave_pass<K, kSnCand, true>(J, N, dimx, P, nt, b, hd);
+    else if (ncmax > 0) sn_wave_pass<K, 2, true>(J, N, dimx, P, nt, b, hd);
 }
 
 // fp64 prefix of the tile sums (a prediction: any order) -> the binades the
@@ -735,15 +802,17 @@ __global__ __launch_bounds__(kSnScan) void seqnorm_check_scan(unsigned nt, unsig
         // and while they predicted it: a walk that stepped many raw segments
         // (binades its tiles' candidates missed) leaves a profile whose drift
         // has moved on, and the next call on the workspace takes the wide window
-        // (2: totals within 1.25x, the drift +-1/64; 1: within 2.5x, as the
-        // loop's workspace sets see sums six updates apart early in a loop,
-        // +-1/32; 0: not usable)
+        // (2: totals within 1.25x, the drift +-1/64; 1: within 2.5x, +-1/32;
+        // 3: further apart, +-1/16 — the drift moves far less than the sums:
+        // early in the 4096^2 texture loop the totals of a workspace's calls
+        // twelve updates apart differ 2-5x, its drift by <= 5 %; 0: no usable
+        // profile, the prefix alone)
         for (int n = 0; n < 2; n++) {
             const int src = prof_src(ws, n);
             const double old = ws.Pp[(size_t)src * (nt + 1) + nt];
             const double q = old > 0.0 ? total[n] / old : 0.0;
             const bool ok = total[n] > 0.0 && ws.miss[src] <= kSnMissMax;
-            ws.cnt[1 + n] = !ok ? 0u : (q < 1.25 && q > 0.8) ? 2u : (q < 2.5 && q > 0.4) ? 1u : 0u;
+            ws.cnt[1 + n] = !ok ? 0u : (q < 1.25 && q > 0.8) ? 2u : (q < 2.5 && q > 0.4) ? 1u : 3u;
         }
         for (int n = 0; n < 2; n++) ws.Pp[(size_t)n * (nt + 1) + nt] = total[n];
     }
@@ -790,13 +859,16 @@ __global__ __launch_bounds__(kSnChk) void seqnorm_check(unsigned nt, SnJobs J) {
             // terms most small terms vanish below half an ulp and the float
             // sum falls well behind; a miss costs the walk term-level steps)
             const unsigned pq = use_prof ? ws.cnt[1 + n] : 0u;
-            const double wd = pq == 2 ? 1.0 / 64 : 1.0 / 32;
+            const double wd = pq == 2 ? 1.0 / 64 : (pq == 1 ? 1.0 / 32 : 1.0 / 16);
             const unsigned want =
                 pq ? cand_window(Pb[n] * d0[n] * (1.0 - wd), (Pb[n] + a[n]) * d1[n] * (1.0 + wd))
                    : cand_window(Pb[n] * (1.0 / 16), (Pb[n] + a[n]) * (1.0 + 1.0 / 16));
             const int wl = hdr_elo(want), wn = hdr_nc(want), hl = hdr_elo(h[n]), hn = hdr_nc(h[n]);
             unsigned hh = h[n];
-            if (wn > 0 && (wl < hl || wl + wn > hl + hn)) hh = want | kHdrPending;
+            // (a header the pass left pending, its window wider than two
+            // candidates, takes the check's narrower one)
+            if (wn > 0 && ((h[n] & kHdrPending) || wl < hl || wl + wn > hl + hn))
+                hh = want | kHdrPending;
             if (hh != h[n]) ws.H[2 * (size_t)b + n] = hh;
             listed |= (hh & kHdrPending) != 0;
         }
@@ -841,6 +913,10 @@ __global__ __launch_bounds__(kSnThreads) void seqnorm_fix(unsigned N, int dimx, 
                                                          unsigned nt, SnJobs J) {
     if (sn_stopped(J)) return;
     const int j = blockIdx.y;
+    // many listed: seqnorm_refill has made every pending entry of the batch
+    bool many = false;
+    for (int i = 0; i < (int)gridDim.y; i++) many |= J.ws[i].cnt[0] > kSnRefillMin;
+    if (many) return;
     const unsigned cnt = J.ws[j].cnt[0];
     for (unsigned k = blockIdx.x; k < cnt; k += gridDim.x) {  // block-uniform
         const unsigned b = (unsigned)__builtin_amdgcn_readfirstlane((int)J.ws[j].list[k]);
@@ -1340,6 +1416,9 @@ SnJobs jobs_of(const SeqnormBatch &B, unsigned nt) {
     }
     J.stop = B.stop;
     J.t0 = B.t0;
+    J.pp_first = B.prev_ws[0] ? carve(const_cast<void *>(B.prev_ws[0]), nt).Pp : nullptr;
+    J.pp_last = B.prev_ws[1] ? carve(const_cast<void *>(B.prev_ws[1]), nt).Pp : nullptr;
+    J.kprev = B.kprev;
     return J;
 }
 }  // namespace
@@ -1357,19 +1436,36 @@ void launch_seqnorm_pass(const SeqnormBatch &B, int dimx, int dimy, int P, hipSt
     OF2D_HIP(hipGetLastError());
 }
 
-void launch_seqnorm_refine(const SeqnormBatch &B, int dimx, int dimy, int P, hipStream_t st) {
+void launch_seqnorm_check(const SeqnormBatch &B, int dimx, int dimy, int P, hipStream_t st) {
     const unsigned nt = check_geometry(dimx, dimy, P);
-    const unsigned N = (unsigned)((size_t)dimx * dimy);
     const SnJobs J = jobs_of(B, nt);
     const unsigned nb = (nt + 1 + kSnChk - 1) / kSnChk;  // blocks over tiles 0 .. nt
     hipLaunchKernelGGL(seqnorm_check_sums, dim3(nb, B.K), dim3(kSnChk), 0, st, nt, J);
     hipLaunchKernelGGL(seqnorm_check_scan, dim3(1, B.K), dim3(kSnScan), 0, st, nt, nb, J);
     hipLaunchKernelGGL(seqnorm_check, dim3(nb, B.K), dim3(kSnChk), 0, st, nt, J);
     OF2D_HIP(hipGetLastError());
+}
+
+void launch_seqnorm_entries(const SeqnormBatch &B, int dimx, int dimy, int P, hipStream_t st) {
+    const unsigned nt = check_geometry(dimx, dimy, P);
+    const unsigned N = (unsigned)((size_t)dimx * dimy);
+    const SnJobs J = jobs_of(B, nt);
+    const dim3 rg((nt + kSnThreads / 64 - 1) / (kSnThreads / 64));
+    switch (B.K) {
+        case 1: hipLaunchKernelGGL(seqnorm_refill<1>, rg, dim3(kSnThreads), 0, st, N, dimx, P, nt, J); break;
+        case 2: hipLaunchKernelGGL(seqnorm_refill<2>, rg, dim3(kSnThreads), 0, st, N, dimx, P, nt, J); break;
+        default: hipLaunchKernelGGL(seqnorm_refill<3>, rg, dim3(kSnThreads), 0, st, N, dimx, P, nt, J); break;
+    }
+    OF2D_HIP(hipGetLastError());
     // one block per listed tile, up to 1024 blocks per pair at once
     const unsigned fb = std::min(nt, 1024u);
     hipLaunchKernelGGL(seqnorm_fix, dim3(fb, B.K), dim3(kSnThreads), 0, st, N, dimx, P, nt, J);
     OF2D_HIP(hipGetLastError());
+}
+
+void launch_seqnorm_refine(const SeqnormBatch &B, int dimx, int dimy, int P, hipStream_t st) {
+    launch_seqnorm_check(B, dimx, dimy, P, st);
+    launch_seqnorm_entries(B, dimx, dimy, P, st);
 }
 
 void launch_seqnorm_walk(const SeqnormBatch &B, int dimx, int dimy, int P, hipStream_t st) {
