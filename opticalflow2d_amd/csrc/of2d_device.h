@@ -284,10 +284,6 @@ struct SeqnormBatch {
     // iteration)
     const int *stop = nullptr;
     int t0 = 0;
-    // the pass's prediction: the workspaces of the previous batch's first and
-    // last pairs (whose checks have run: their fp64 totals) and its pair count
-    const void *prev_ws[2] = {};
-    int kprev = 0;
 };
 // the Logger errors of a walked batch (pair i's sums at seq[2i], seq[2i + 1]),
 // as logger_error does on the host: the first iteration t0 + i > 1 whose
@@ -301,10 +297,6 @@ void launch_seqnorm_decide(const float *seq, int K, int t0, double npx, int *sto
 void seqnorm_ws_stats(const void *ws, int dimx, int dimy, unsigned *out);
 void launch_seqnorm_pass(const SeqnormBatch &b, int dimx, int dimy, int P, hipStream_t st);
 void launch_seqnorm_refine(const SeqnormBatch &b, int dimx, int dimy, int P, hipStream_t st);
-// refine = check (three launches: the tiles whose entries miss the fp64
-// prefix's binades, listed) + entries (refill when many are listed, fix)
-void launch_seqnorm_check(const SeqnormBatch &b, int dimx, int dimy, int P, hipStream_t st);
-void launch_seqnorm_entries(const SeqnormBatch &b, int dimx, int dimy, int P, hipStream_t st);
 void launch_seqnorm_walk(const SeqnormBatch &b, int dimx, int dimy, int P, hipStream_t st);
 
 // ---------------------------------------------------------------- fields

@@ -219,8 +219,8 @@ class Registration {
     static constexpr int kSeqSets = 4;   // workspace sets: group g's walk is read by g + 4
     static constexpr int kSeqWs = 3 * kSeqSets;
     static constexpr int kRing = 15;  // iterate buffers: a step waits for the walks 4-5 groups back
-    hipEvent_t ev_step_[kExactEv] = {}, ev_pass_[kExactEv] = {}, ev_chk_[kExactEv] = {},
-               ev_fix_[kExactEv] = {}, ev_walk_[kExactEv] = {};
+    hipEvent_t ev_step_[kExactEv] = {}, ev_pass_[kExactEv] = {}, ev_fix_[kExactEv] = {},
+               ev_walk_[kExactEv] = {};
     DevArray<unsigned char> d_seqws_[kSeqWs];  // seqnorm workspaces (level 0 size)
     DevArray<float> d_seq_;                    // per-iteration exact sums of a chunk
     int seq_dx_[kSeqWs] = {}, seq_dy_[kSeqWs] = {};  // grid of each workspace's last call

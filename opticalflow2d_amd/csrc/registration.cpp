@@ -161,7 +161,6 @@ Registration::~Registration() {
         if (ev_step_[k]) (void)hipEventDestroy(ev_step_[k]);
         if (ev_fix_[k]) (void)hipEventDestroy(ev_fix_[k]);
         if (ev_pass_[k]) (void)hipEventDestroy(ev_pass_[k]);
-        if (ev_chk_[k]) (void)hipEventDestroy(ev_chk_[k]);
         if (ev_walk_[k]) (void)hipEventDestroy(ev_walk_[k]);
     }
     if (st_) (void)hipStreamDestroy(st_);
@@ -217,7 +216,6 @@ void Registration::ensure_device() {
         OF2D_HIP(hipEventCreateWithFlags(&ev_step_[k], hipEventDisableTiming));
         OF2D_HIP(hipEventCreateWithFlags(&ev_fix_[k], hipEventDisableTiming));
         OF2D_HIP(hipEventCreateWithFlags(&ev_pass_[k], hipEventDisableTiming));
-        OF2D_HIP(hipEventCreateWithFlags(&ev_chk_[k], hipEventDisableTiming));
         OF2D_HIP(hipEventCreateWithFlags(&ev_walk_[k], hipEventDisableTiming));
     }
     OF2D_HIP(hipEventCreateWithFlags(&ev_fork_, hipEventDisableTiming));
@@ -468,14 +466,10 @@ void Registration::enqueue_norms(const SeqnormBatch &B, const Level &L, int g, d
     auto ev = [](hipEvent_t *e, int q) { return e[q % kExactEv]; };
     OF2D_HIP(hipStreamWaitEvent(sn_st_, ev(ev_step_, g), 0));
     if (g >= kSeqSets) OF2D_HIP(hipStreamWaitEvent(sn_st_, ev(ev_walk_, g - kSeqSets), 0));
-    // the pass scales its prediction by the previous batch's totals (its check)
-    if (B.prev_ws[0] && g >= 1) OF2D_HIP(hipStreamWaitEvent(sn_st_, ev(ev_chk_, g - 1), 0));
     launch_seqnorm_pass(B, L.dx, L.dy, L.P, sn_st_);
     OF2D_HIP(hipEventRecord(ev(ev_pass_, g), sn_st_));
     OF2D_HIP(hipStreamWaitEvent(fx_st_, ev(ev_pass_, g), 0));
-    launch_seqnorm_check(B, L.dx, L.dy, L.P, fx_st_);
-    OF2D_HIP(hipEventRecord(ev(ev_chk_, g), fx_st_));
-    launch_seqnorm_entries(B, L.dx, L.dy, L.P, fx_st_);
+    launch_seqnorm_refine(B, L.dx, L.dy, L.P, fx_st_);
     OF2D_HIP(hipEventRecord(ev(ev_fix_, g), fx_st_));
     hipStream_t wk = wk_st_[g % 3];
     OF2D_HIP(hipStreamWaitEvent(wk, ev(ev_fix_, g), 0));
@@ -537,7 +531,7 @@ int Registration::run_exact_pipelined(Level &L, int niter, const StepFn &step, i
     if (sn_debug) dbg.alloc(kDbg * (size_t)ring2);
     bool walked[kSeqWs] = {};  // a new loop: each workspace starts from a fresh state
     std::vector<int> grp_of((size_t)std::max(niter, 1));
-    int g = 0, grp_start = 0;  // the group being enqueued, the previous one's first iteration
+    int g = 0;
     // iterations [t, t + k) as group g (t a multiple of three)
     auto enqueue_group = [&](int t, int k) {
         for (int m = t; m < t + k; m++) grp_of[m] = g;
@@ -570,13 +564,6 @@ int Registration::run_exact_pipelined(Level &L, int niter, const StepFn &step, i
             B.out[i] = d_seq_.p + 2 * (size_t)((t + i) % ring2);
             B.dbg[i] = sn_debug ? dbg.p + kDbg * (size_t)((t + i) % ring2) : nullptr;
         }
-        if (g > 0) {  // the previous group's first and last pairs (same grid)
-            const int kp = t - grp_start;
-            B.prev_ws[0] = d_seqws_[3 * ((g - 1) % kSeqSets)].p;
-            B.prev_ws[1] = d_seqws_[3 * ((g - 1) % kSeqSets) + kp - 1].p;
-            B.kprev = kp;
-        }
-        grp_start = t;
         enqueue_norms(B, L, g, npx, hs_.seqh + 2 * (size_t)(t % ring2));
         g++;
     };

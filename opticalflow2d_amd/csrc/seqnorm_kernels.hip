@@ -322,10 +322,6 @@ struct SnJobs {
     // past it returns at once (its norms are never read)
     const int *stop;
     int t0;
-    // the pass's scale: the fp64 prefixes (Pp) of the previous batch's first
-    // and last pairs (their checks have run) and its pair count, or null
-    const double *pp_first, *pp_last;
-    int kprev;
 };
 __device__ __forceinline__ bool sn_stopped(const SnJobs &J) {
     return J.stop && *J.stop < J.t0;
@@ -388,7 +384,7 @@ struct SnLoader {
 __device__ __forceinline__ bool sn_refills(unsigned h) {
     return (h & kHdrPending) && !(h & (kHdrZero | kHdrNan)) && hdr_nc(h) > 0;
 }
-// RF (seqnorm_refill): hd are the check's headers; only the pending norms with
+// RF (sn_refill_tile): hd are the check's headers; only the pending norms with
 // at most NC candidates take entries (T and the header, pending cleared), the
 // others are left as they are, and A / Z (the pass's) are not written again.
 template <int K, int NC, bool RF = false>
@@ -633,30 +629,13 @@ void seqnorm_tables(unsigned N, int dimx, int P, unsigned nt, SnJobs J) {
         for (int n = 0; n < 2; n++) {
             unsigned h = hdr_pack(0, 0);
             if (J.use_prof[i]) {
-                // the last call's running sums (their shape across the grid
-                // moves little: > 99 % of the tiles within 5 % over twelve
-                // updates early in the 4096^2 texture loop) scaled to this
-                // pair's total: extrapolated from the previous batch's fp64
-                // totals at its rate per update, or else the trend of the
-                // workspace's own totals (|cur - prev| shrinks from update to
-                // update)
+                // the last call's running sums scaled by the trend of its
+                // totals (|cur - prev| shrinks from update to update)
                 const int src = prof_src(ws, n);
                 const float *pr = ws.prof + (size_t)src * (nt + 1);
-                const double told = ws.Pp[(size_t)src * (nt + 1) + nt];
-                const double tl = J.pp_last ? J.pp_last[(size_t)n * (nt + 1) + nt] : 0.0;
-                const double tf = J.pp_first ? J.pp_first[(size_t)n * (nt + 1) + nt] : 0.0;
-                double r;
-                if (tl > 0.0 && told > 0.0 && tl < INFINITY) {
-                    const double rho = (J.kprev > 1 && tf > 0.0 && tf < INFINITY)
-                                           ? pow(tl / tf, 1.0 / (J.kprev - 1))
-                                           : 1.0;
-                    r = tl * pow(rho, (double)(i + 1)) / told;
-                    r = r < 0x1p-10 ? 0x1p-10 : (r > 0x1p10 ? 0x1p10 : r);
-                } else {
-                    const float t0 = ws.tot[2 * src], t1 = ws.tot[2 * src + 1];
-                    r = (src == n && t1 > 0.0f && t0 > 0.0f) ? (double)t0 / t1 : 1.0;
-                    r = r < 0.25 ? 0.25 : (r > 4.0 ? 4.0 : r);
-                }
+                const float t0 = ws.tot[2 * src], t1 = ws.tot[2 * src + 1];
+                double r = (src == n && t1 > 0.0f && t0 > 0.0f) ? (double)t0 / t1 : 1.0;
+                r = r < 0.25 ? 0.25 : (r > 4.0 ? 4.0 : r);
                 h = cand_window((double)pr[b] * r * (1.0 - kSnWin),
                                 (double)pr[b + 1] * r / (1.0 - kSnWin));
             }
@@ -686,20 +665,12 @@ void seqnorm_tables(unsigned N, int dimx, int P, unsigned nt, SnJobs J) {
 // which have no profile, or a misprediction): one wave per tile reads the
 // batch's K + 1 iterates once and makes the entries of every pending norm,
 // as the pass does — 4 arrays per tile against the fix's 2 per listed pair,
-// and the pass's lane-sum form.  Runs only when a pair of the batch listed
-// more than kSnRefillMin tiles; the fix then finds nothing pending.
+// and the pass's lane-sum form (seqnorm_entries, when a pair of the batch
+// listed more than kSnRefillMin tiles).
 constexpr unsigned kSnRefillMin = 512;
 template <int K>
-__global__ __launch_bounds__(kSnThreads) __attribute__((amdgpu_waves_per_eu(OF2D_SN_WPE)))
-void seqnorm_refill(unsigned N, int dimx, int P, unsigned nt, SnJobs J) {
-    if (sn_stopped(J)) return;
-    bool many = false;
-#pragma unroll
-    for (int i = 0; i < K; i++) many |= J.ws[i].cnt[0] > kSnRefillMin;
-    if (!many) return;
-    const unsigned b = (unsigned)__builtin_amdgcn_readfirstlane(
-        (int)(blockIdx.x * (kSnThreads / 64) + threadIdx.x / 64));
-    if (b >= nt) return;
+__device__ __forceinline__ void sn_refill_tile(const SnJobs &J, unsigned N, int dimx, int P,
+                                               unsigned nt, unsigned b) {
     unsigned hd[K][2];
     int ncmax = 0;
 #pragma unroll
@@ -908,15 +879,28 @@ __global__ void seqnorm_offset_chain(const double *__restrict__ prev_nxt, SnTota
     }
 }
 
-// the listed tiles of pair blockIdx.y: new tile entries, one block per tile
-__global__ __launch_bounds__(kSnThreads) void seqnorm_fix(unsigned N, int dimx, int P,
-                                                         unsigned nt, SnJobs J) {
+// The listed tiles' new entries, one launch: with many listed (a pair of the
+// batch over kSnRefillMin) the blocks of row 0 refill every tile, a wave per
+// tile; otherwise the fix — pair blockIdx.y's listed tiles, one block per
+// tile (sn_block_fix).  (Two launches cost the latency chain check -> walk a
+// launch more per batch: 4096^2 procedural 139-142 -> 148-149 us per
+// iteration, profiles/r04za_predict_ab.log.)
+template <int K>
+__global__ __launch_bounds__(kSnThreads) void seqnorm_entries(unsigned N, int dimx, int P,
+                                                              unsigned nt, SnJobs J) {
     if (sn_stopped(J)) return;
-    const int j = blockIdx.y;
-    // many listed: seqnorm_refill has made every pending entry of the batch
     bool many = false;
-    for (int i = 0; i < (int)gridDim.y; i++) many |= J.ws[i].cnt[0] > kSnRefillMin;
-    if (many) return;
+#pragma unroll
+    for (int i = 0; i < K; i++) many |= J.ws[i].cnt[0] > kSnRefillMin;
+    if (many) {
+        if (blockIdx.y != 0) return;
+        const unsigned w = (unsigned)__builtin_amdgcn_readfirstlane((int)(threadIdx.x / 64));
+        for (unsigned b = blockIdx.x * (kSnThreads / 64) + w; b < nt;
+             b += gridDim.x * (kSnThreads / 64))
+            sn_refill_tile<K>(J, N, dimx, P, nt, b);
+        return;
+    }
+    const int j = blockIdx.y;
     const unsigned cnt = J.ws[j].cnt[0];
     for (unsigned k = blockIdx.x; k < cnt; k += gridDim.x) {  // block-uniform
         const unsigned b = (unsigned)__builtin_amdgcn_readfirstlane((int)J.ws[j].list[k]);
@@ -1416,9 +1400,6 @@ SnJobs jobs_of(const SeqnormBatch &B, unsigned nt) {
     }
     J.stop = B.stop;
     J.t0 = B.t0;
-    J.pp_first = B.prev_ws[0] ? carve(const_cast<void *>(B.prev_ws[0]), nt).Pp : nullptr;
-    J.pp_last = B.prev_ws[1] ? carve(const_cast<void *>(B.prev_ws[1]), nt).Pp : nullptr;
-    J.kprev = B.kprev;
     return J;
 }
 }  // namespace
@@ -1436,36 +1417,23 @@ void launch_seqnorm_pass(const SeqnormBatch &B, int dimx, int dimy, int P, hipSt
     OF2D_HIP(hipGetLastError());
 }
 
-void launch_seqnorm_check(const SeqnormBatch &B, int dimx, int dimy, int P, hipStream_t st) {
+void launch_seqnorm_refine(const SeqnormBatch &B, int dimx, int dimy, int P, hipStream_t st) {
     const unsigned nt = check_geometry(dimx, dimy, P);
+    const unsigned N = (unsigned)((size_t)dimx * dimy);
     const SnJobs J = jobs_of(B, nt);
     const unsigned nb = (nt + 1 + kSnChk - 1) / kSnChk;  // blocks over tiles 0 .. nt
     hipLaunchKernelGGL(seqnorm_check_sums, dim3(nb, B.K), dim3(kSnChk), 0, st, nt, J);
     hipLaunchKernelGGL(seqnorm_check_scan, dim3(1, B.K), dim3(kSnScan), 0, st, nt, nb, J);
     hipLaunchKernelGGL(seqnorm_check, dim3(nb, B.K), dim3(kSnChk), 0, st, nt, J);
     OF2D_HIP(hipGetLastError());
-}
-
-void launch_seqnorm_entries(const SeqnormBatch &B, int dimx, int dimy, int P, hipStream_t st) {
-    const unsigned nt = check_geometry(dimx, dimy, P);
-    const unsigned N = (unsigned)((size_t)dimx * dimy);
-    const SnJobs J = jobs_of(B, nt);
-    const dim3 rg((nt + kSnThreads / 64 - 1) / (kSnThreads / 64));
+    // one block per listed tile (up to 1024 per pair at once), or the refill
+    const dim3 eg(std::min(nt, 1024u), B.K);
     switch (B.K) {
-        case 1: hipLaunchKernelGGL(seqnorm_refill<1>, rg, dim3(kSnThreads), 0, st, N, dimx, P, nt, J); break;
-        case 2: hipLaunchKernelGGL(seqnorm_refill<2>, rg, dim3(kSnThreads), 0, st, N, dimx, P, nt, J); break;
-        default: hipLaunchKernelGGL(seqnorm_refill<3>, rg, dim3(kSnThreads), 0, st, N, dimx, P, nt, J); break;
+        case 1: hipLaunchKernelGGL(seqnorm_entries<1>, eg, dim3(kSnThreads), 0, st, N, dimx, P, nt, J); break;
+        case 2: hipLaunchKernelGGL(seqnorm_entries<2>, eg, dim3(kSnThreads), 0, st, N, dimx, P, nt, J); break;
+        default: hipLaunchKernelGGL(seqnorm_entries<3>, eg, dim3(kSnThreads), 0, st, N, dimx, P, nt, J); break;
     }
     OF2D_HIP(hipGetLastError());
-    // one block per listed tile, up to 1024 blocks per pair at once
-    const unsigned fb = std::min(nt, 1024u);
-    hipLaunchKernelGGL(seqnorm_fix, dim3(fb, B.K), dim3(kSnThreads), 0, st, N, dimx, P, nt, J);
-    OF2D_HIP(hipGetLastError());
-}
-
-void launch_seqnorm_refine(const SeqnormBatch &B, int dimx, int dimy, int P, hipStream_t st) {
-    launch_seqnorm_check(B, dimx, dimy, P, st);
-    launch_seqnorm_entries(B, dimx, dimy, P, st);
 }
 
 void launch_seqnorm_walk(const SeqnormBatch &B, int dimx, int dimy, int P, hipStream_t st) {

@@ -11,7 +11,7 @@ from collections import defaultdict
 
 
 def fam(name):
-    for k in ("jacobi3_mid", "seqnorm_tables", "seqnorm_walk", "seqnorm_fix", "seqnorm_check",
+    for k in ("jacobi3_mid", "seqnorm_tables", "seqnorm_walk", "seqnorm_fix", "seqnorm_entries", "seqnorm_check",
               "jacobi3_kernel", "jacobi_kernel"):
         if k in name:
             return k
