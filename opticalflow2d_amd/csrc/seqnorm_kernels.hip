@@ -667,7 +667,10 @@ void seqnorm_tables(unsigned N, int dimx, int P, unsigned nt, SnJobs J) {
 // as the pass does — 4 arrays per tile against the fix's 2 per listed pair,
 // and the pass's lane-sum form (seqnorm_entries, when a pair of the batch
 // listed more than kSnRefillMin tiles).
-constexpr unsigned kSnRefillMin = 512;
+#ifndef OF2D_SN_REFILL_MIN
+#define OF2D_SN_REFILL_MIN 512  // A/B build knob
+#endif
+constexpr unsigned kSnRefillMin = OF2D_SN_REFILL_MIN;
 template <int K>
 __device__ __forceinline__ void sn_refill_tile(const SnJobs &J, unsigned N, int dimx, int P,
                                                unsigned nt, unsigned b) {
