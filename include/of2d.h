@@ -104,6 +104,8 @@ int of2d_last_errors(const of2d_ctx *ctx, float *out, int cap);
  *   "ngpus_share" (0 = default / 1): ranks may share a device, (device + r)
  *   mod count for every r < ngpus (the decomposition on fewer devices than
  *   ranks: tests, timings of the path's overhead on one GPU).
+ *   "slab_split" (-1 auto = default, 0, 1): the ranks' slab option "split"
+ *   (of2d_slab_set_option).
  *   "logger_fp64" (0 = default / 1): 0 computes the Logger norms as the
  *   reference does (float running sums, of2d_motion_norms), so the break of
  *   ImageRegistrationOpticalFlow.cpp:131-134 falls on the reference's
@@ -188,11 +190,19 @@ int of2d_slab_last_run_kernel_us(const of2d_slab *s, double *avg_us, int *nlaunc
  *   derives dI from Iaux in the kernel (24 B/px per launch) instead of reading
  *   dI (28); auto does so when dI + It (12 B/px) exceed the 256 MB MALL;
  *   bit-identical either way
- *   "logger_fp64" (0 = default / 1): as of2d_set_option's; 0 takes the
- *   convergence-on Logger norms as the reference does (one float running sum
- *   over the slabs in rank order, so the break falls on the one-grid
+ *   "logger_fp64" (-1 auto = default, 0, 1): as of2d_set_option's; 0 takes
+ *   the convergence-on Logger norms as the reference does (one float running
+ *   sum over the slabs in rank order, so the break falls on the one-grid
  *   reference's iteration), 1 sums the fused fp64 partials (fixed_iters runs
- *   always do) */
+ *   always do); auto is 0 except on an RCCL communicator of two or more
+ *   ranks, where the rank-to-rank chain of the running sums (two more
+ *   communicators on two more streams) has not run on hardware: 1 there,
+ *   unless 0 is set
+ *   "split" (-1 auto = default, 0, 1): triples as an interior launch beside
+ *   the halo exchange and two edge launches (auto: when a neighbour is on
+ *   another device or behind RCCL), never, or whenever the slab has >= 48
+ *   j-lines (tests of the multi-device launch order on one device);
+ *   bit-identical either way */
 int of2d_slab_set_option(of2d_slab *s, const char *key, double value);
 int of2d_slab_destroy(of2d_slab *s);
 const char *of2d_slab_last_error(const of2d_slab *s);
@@ -228,9 +238,12 @@ int of2d_motion_norms(const float *cur, const float *prev, int dimx, int dimy, i
 /* The Logger norms of a chain of iterates u[0 .. niter] (niter + 1 fields of
  * dimx*dimy*2 floats): sums[2k], sums[2k + 1] are those of the update from
  * u[k] to u[k + 1], as of2d_motion_norms gives them, computed the way the
- * registration loop does: in batches of `batch` (1..3) consecutive updates
- * whose pass reads each iterate once, alternating between two sets of
- * workspaces.  stats as of2d_motion_norms, per update.  Not in the
+ * registration loop batches them: `batch` (1..3) consecutive updates per
+ * batch, whose pass reads each iterate once, on four sets of workspaces in
+ * rotation (batch g's profile is batch g - 4's, Registration::kSeqSets).  The
+ * launches run in order on one stream: the sums match the registration's,
+ * its stream schedule (walks on three streams, the stop word) is not
+ * reproduced.  stats as of2d_motion_norms, per update.  Not in the
  * reference: a test entry for the batched device norms. */
 int of2d_motion_norms_chain(const float *u, int dimx, int dimy, int niter, int batch,
                             float *sums, int *stats);

@@ -202,9 +202,11 @@ int of2d_motion_norms_chain(const float *u, int dimx, int dimy, int niter, int b
             const size_t row = (size_t)dimx * sizeof(float2), pitch = (size_t)f[k].P * sizeof(float2);
             OF2D_HIP(hipMemcpy2D(f[k].p, pitch, u + k * n, row, row, dimy, hipMemcpyHostToDevice));
         }
-        // two sets of three workspaces, as Registration::run_chunked_exact
-        of2d::DevArray<unsigned char> ws[6];
-        bool used[6] = {};
+        // four sets of three workspaces rotated per batch, as the registration
+        // loops (Registration::kSeqSets): batch g's profile is batch g - 4's
+        constexpr int kSets = 4;
+        of2d::DevArray<unsigned char> ws[3 * kSets];
+        bool used[3 * kSets] = {};
         for (auto &w : ws) w.alloc(of2d::seqnorm_workspace_bytes(dimx, dimy));
         of2d::DevArray<float> out;
         out.alloc(2 * (size_t)niter);
@@ -216,7 +218,7 @@ int of2d_motion_norms_chain(const float *u, int dimx, int dimy, int niter, int b
             B.K = std::min(batch, niter - t);
             for (int i = 0; i <= B.K; i++) B.u[i] = f[(size_t)t + i].p;
             for (int i = 0; i < B.K; i++) {
-                const int w = 3 * (g & 1) + i;
+                const int w = 3 * (g % kSets) + i;
                 B.ws[i] = ws[w].p;
                 B.use_profile[i] = used[w];
                 used[w] = true;

@@ -226,6 +226,7 @@ class Registration {
     int seq_dx_[kSeqWs] = {}, seq_dy_[kSeqWs] = {};  // grid of each workspace's last call
     int chunk_ = 33;  // eleven fused triples per chunk
     int gi_ = -1;     // triple kernel: dI from Iaux (1), from dI (0), by size (-1)
+    int split_ = -1;  // ranks' triples: interior / edge split (slab option "split")
     int device_ = -1;  // option "device" (-1: the current device at first use)
     int home_ = -1;    // the registration's device, fixed at first use
     bool ready_ = false;

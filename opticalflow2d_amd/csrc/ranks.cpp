@@ -137,6 +137,7 @@ int Registration::loop_hs_multi(int s, float alpha, int &final_buf) {
         };
         opt("logger_fp64", logger_fp64_ ? 1.0 : 0.0);
         opt("hs_gradients_from_image", gi_);
+        opt("split", split_);
         slab_set_images_device(sl, L.Iref.p, L.Iaux.p, L.P, M.home);
     }
     // every rank's loop from a thread of its own (each enqueues whole chunks
@@ -154,7 +155,15 @@ int Registration::loop_hs_multi(int s, float alpha, int &final_buf) {
     }
     OF2D_HIP(hipSetDevice(M.home));
     for (int k = 0; k < n; k++)
-        if (rc[k] != OF2D_OK) rethrow(rc[k], msg[k]);
+        if (rc[k] != OF2D_OK) {
+            // a rank that threw left the group's per-rank counters (halo
+            // exchanges, Logger-chain groups) out of step with the others':
+            // the next run starts from new slabs
+            const int code = rc[k];
+            const std::string m = msg[k];
+            multi_release();
+            rethrow(code, m);
+        }
     // the Logger errors are global: every rank holds the same
     const int ne = of2d_slab_last_errors(M.slabs[0], nullptr, 0);
     last_err_.assign(std::max(ne, 0), 0.0f);

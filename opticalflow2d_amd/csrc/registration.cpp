@@ -24,6 +24,13 @@
 #include "of2d_host.h"
 #include "of2d_solvers.h"
 
+// the walks' cost counters per iteration to stderr (resolves, raw segments,
+// listed tiles, walk clocks; tools/seqnorm_diag.py): a diagnostic build only,
+// tools/build_variant.sh sndebug registration.cpp -DOF2D_SN_DEBUG=1
+#ifndef OF2D_SN_DEBUG
+#define OF2D_SN_DEBUG 0
+#endif
+
 namespace of2d {
 
 float logger_error(double sum_diff, double sum_prev, double npx) {
@@ -187,6 +194,8 @@ void Registration::set_option(const std::string &key, double v) {
     }
     else if (key == "hs_gradients_from_image")
         gi_ = v < 0 ? -1 : (v != 0 ? 1 : 0);
+    else if (key == "slab_split")
+        split_ = v < 0 ? -1 : (v != 0 ? 1 : 0);
     else if (key == "device") {
         if (ready_) throw std::invalid_argument("option 'device' must be set before first use");
         device_ = (int)v;
@@ -387,9 +396,7 @@ int Registration::run_chunked_exact(Level &L, int niter, int nb, const StepFn &s
     };
     auto src_of = [&](int a, int t) { return t == 0 ? a : ring(a, t - 1); };
     auto ev = [](hipEvent_t *e, int g) { return e[g % kExactEv]; };
-    // OF2D_SN_DEBUG: the walks' cost counters per iteration to stderr
-    // (resolves, raw segments, listed tiles, walk clocks; tools/ diagnostics)
-    static const bool sn_debug = std::getenv("OF2D_SN_DEBUG") != nullptr;
+    constexpr bool sn_debug = OF2D_SN_DEBUG != 0;
     constexpr int kDbg = 10;
     DevArray<int> dbg;
     if (sn_debug) dbg.alloc(kDbg * (size_t)chunk_);
@@ -479,7 +486,7 @@ void Registration::enqueue_norms(const SeqnormBatch &B, const Level &L, int g, d
     OF2D_HIP(hipEventRecord(ev(ev_walk_, g), wk));
 }
 
-// OF2D_SN_DEBUG: iterations [k0 + lo, k0 + hi)'s walk counters (dbg[10 * t])
+// OF2D_SN_DEBUG builds: iterations [k0 + lo, k0 + hi)'s walk counters (dbg[10 * t])
 void Registration::print_sn_debug(const Level &L, const int *dbg, int k0, int lo, int hi) {
     constexpr int kDbg = 10;
     std::vector<int> h(kDbg * (size_t)hi);
@@ -525,7 +532,7 @@ int Registration::run_exact_pipelined(Level &L, int niter, const StepFn &step, i
     const int blk = std::min(3 * ((chunk_ + 2) / 3), 3 * (kExactEv / 2 - 4));
     const int ring2 = 2 * blk;  // the sums' ring: two blocks of iterations
     hs_.ensure(std::max(chunk_, 64));
-    static const bool sn_debug = std::getenv("OF2D_SN_DEBUG") != nullptr;
+    constexpr bool sn_debug = OF2D_SN_DEBUG != 0;
     constexpr int kDbg = 10;
     DevArray<int> dbg;
     if (sn_debug) dbg.alloc(kDbg * (size_t)ring2);

@@ -24,25 +24,45 @@
 // with the reference's own two roundings; inside the walk's term-level scans
 // ties are composed exactly (a run of terms is M -> M + (M even ? a : b)).
 //
-// Pipeline for the pair of norms of one Logger update (|cur - prev| and
-// |prev|), in tiles of kSnTile consecutive terms, segments of 64:
-//   seqnorm_tables<true>   one pass over cur / prev: fp64 tile sums, the
-//                          nonzero-segment masks, and per candidate binade
-//                          (predicted from the previous update's exact
-//                          running sums, the "profile") the ulp sums of each
-//                          segment and of the tile
-//   seqnorm_check(_sums, _scan)  fp64 prefix over the tiles -> the binades the float
-//                          sum can be in across each tile (the fp64 sum +-1/8);
-//                          tiles whose candidates miss one are marked pending
-//   seqnorm_tables<false>  the pending tiles again, with those binades
-//   seqnorm_walk           one wave per norm walks the tiles in order, 64 per
-//                          step (saturating wave scan of their entries for the
-//                          current binade); at a tile whose entry does not
-//                          apply (a crossing, a tie, a binade outside its
-//                          candidates) it scans the tile's segment entries,
-//                          and the one segment that holds the crossing term by
-//                          term.  It writes the profile of the next update.
-// Predictions only decide how much work the walk and the pending pass do: the
+// Pipeline (round 4).  The norms of a batch of K <= 3 consecutive Logger
+// updates (a Jacobi triple's: pair i = iterates u[i], u[i + 1] on workspace
+// ws[i]) run as one launch per stage, in tiles of kSnTile consecutive terms
+// and segments of 64:
+//   seqnorm_tables<K>   the pass: one wave per tile reads the K + 1 iterates
+//                       once and writes per norm the fp64 tile sum (a
+//                       prediction), the nonzero-segment mask, the header and,
+//                       for the <= 2 binades the workspace's profile predicts
+//                       (its last walk's running sums scaled by the trend of
+//                       its totals), the tile entries: each lane adds its
+//                       terms' ulp increments, decided from an fp32 estimate
+//                       of the magnitude wherever it lies clear of a
+//                       half-integer (sn_incr_est), the exact fp64 sequence in
+//                       the waves where one lane's estimate does not decide
+//   seqnorm_check       (three launches: block sums, scan, check) the fp64
+//                       prefix of the tile sums times the drift window of the
+//                       last walk gives each tile the binades its float sum
+//                       can be in; tiles whose entries miss one are listed
+//   seqnorm_entries     the listed tiles' entries: a refill (one wave per tile
+//                       over the batch's iterates, every listed norm) when a
+//                       pair listed more than kSnRefillMin tiles, otherwise the
+//                       fix (one block of four waves per listed tile and pair)
+//   seqnorm_walk        one block per norm and pair: wave 0 walks the tiles 64
+//                       per step (saturating DPP scan of their entries for S's
+//                       binade); at a tile whose entry does not apply (a
+//                       crossing, a tie, a binade outside its candidates) the
+//                       block's other waves make the segment entries of its
+//                       remaining segments for binades e, e + 1 on request
+//                       (sn_help / sn_helper) and leave the terms in LDS, and
+//                       the walker steps the crossing segment term by term
+//                       with the reference's two roundings.  It writes the
+//                       profile the workspace's next batch predicts from.
+//   seqnorm_decide      (HS's pipelined loop) the batch's Logger errors as the
+//                       host computes them; the first breaking iteration into
+//                       the stop word, after which every kernel of a later
+//                       batch returns at once (sn_block_stopped)
+// The registration runs the pass on one stream, check and entries on a
+// second, the walks on three more (registration.cpp enqueue_norms).
+// Predictions only decide how much work the walk and the entries do: the
 // walk's result is the reference's float sum whatever they predicted.
 #include <hip/hip_runtime.h>
 
@@ -324,7 +344,19 @@ struct SnJobs {
     int t0;
 };
 __device__ __forceinline__ bool sn_stopped(const SnJobs &J) {
-    return J.stop && *J.stop < J.t0;
+    return J.stop &&
+           __hip_atomic_load(J.stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < J.t0;
+}
+// The stop word read ONCE per block and shared through LDS: seqnorm_decide
+// (another stream) may set it while the block's waves start, and a block
+// whose waves decided apart would run its barriers and inter-wave protocols
+// (the walk's helper waves) with some waves gone.  Every kernel that tests the
+// word calls this first, in all of its threads.
+__device__ __forceinline__ bool sn_block_stopped(const SnJobs &J) {
+    __shared__ int stopped;
+    if (threadIdx.x == 0) stopped = sn_stopped(J) ? 1 : 0;
+    __syncthreads();
+    return stopped != 0;
 }
 
 // segments in flight per wave: a ring of D segment buffers, each reloaded
@@ -613,7 +645,7 @@ __device__ void sn_block_fix(const SnJobs &J, int j, unsigned N, int dimx, int P
 template <int K>
 __global__ __launch_bounds__(kSnThreads) __attribute__((amdgpu_waves_per_eu(OF2D_SN_WPE)))
 void seqnorm_tables(unsigned N, int dimx, int P, unsigned nt, SnJobs J) {
-    if (sn_stopped(J)) return;
+    if (sn_block_stopped(J)) return;
     if (blockIdx.x == 0 && threadIdx.x < 4)
 #pragma unroll
         for (int i = 0; i < K; i++) J.ws[i].cnt[threadIdx.x] = 0;  // seqnorm_check's list
@@ -711,7 +743,7 @@ __device__ __forceinline__ double sn_drift(const SnWs &ws, unsigned nt, int src,
     return (q > 0.0 && f > 0.0 && f < INFINITY) ? f / q : 1.0;
 }
 __global__ __launch_bounds__(kSnChk) void seqnorm_check_sums(unsigned nt, SnJobs J) {
-    if (sn_stopped(J)) return;
+    if (sn_block_stopped(J)) return;
     const SnWs &ws = J.ws[blockIdx.y];
     const int use_prof = J.use_prof[blockIdx.y];
     const unsigned b = blockIdx.x * kSnChk + threadIdx.x;
@@ -735,7 +767,7 @@ __global__ __launch_bounds__(kSnChk) void seqnorm_check_sums(unsigned nt, SnJobs
 // predecessors: the prediction is of the global running sum); Pp[nt] <- the
 // total
 __global__ __launch_bounds__(kSnScan) void seqnorm_check_scan(unsigned nt, unsigned nb, SnJobs J) {
-    if (sn_stopped(J)) return;
+    if (sn_block_stopped(J)) return;
     const SnWs &ws = J.ws[blockIdx.y];
     const double *p_off = J.p_off[blockIdx.y];
     const unsigned chunk = (nb + kSnScan - 1) / kSnScan;
@@ -792,7 +824,7 @@ __global__ __launch_bounds__(kSnScan) void seqnorm_check_scan(unsigned nt, unsig
     }
 }
 __global__ __launch_bounds__(kSnChk) void seqnorm_check(unsigned nt, SnJobs J) {
-    if (sn_stopped(J)) return;
+    if (sn_block_stopped(J)) return;
     const SnWs &ws = J.ws[blockIdx.y];
     const int use_prof = J.use_prof[blockIdx.y];
     const unsigned b = blockIdx.x * kSnChk + threadIdx.x;
@@ -891,7 +923,7 @@ __global__ void seqnorm_offset_chain(const double *__restrict__ prev_nxt, SnTota
 template <int K>
 __global__ __launch_bounds__(kSnThreads) void seqnorm_entries(unsigned N, int dimx, int P,
                                                               unsigned nt, SnJobs J) {
-    if (sn_stopped(J)) return;
+    if (sn_block_stopped(J)) return;
     bool many = false;
 #pragma unroll
     for (int i = 0; i < K; i++) many |= J.ws[i].cnt[0] > kSnRefillMin;
@@ -1202,7 +1234,7 @@ constexpr int kSnAhead = 8;  // windows loaded per step: the next step's loads h
 // resolve clocks, tiles given the walk's own segment entries (per norm).
 __global__ __launch_bounds__(64 * kSnWalkWaves) void seqnorm_walk(unsigned N, int dimx, int P,
                                                                    unsigned nt, SnJobs J) {
-    if (sn_stopped(J)) return;  // before the barrier, the whole block
+    if (sn_block_stopped(J)) return;  // one decision for the whole block
     const int job = blockIdx.x >> 1;
     const int n = blockIdx.x & 1;  // 0: |cur - prev|, 1: |prev|
     const int lane = threadIdx.x & 63;

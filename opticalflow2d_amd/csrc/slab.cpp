@@ -55,8 +55,17 @@ struct of2d_slab {
     // convergence-on runs: the Logger's norms as the reference takes them
     // (float running sums in linear order across the slabs, SlabExact), or
     // fp64 sums of the fused partials ("logger_fp64"); fixed_iters runs take
-    // no break and always use the fp64 sums
-    bool logger_fp64 = false;
+    // no break and always use the fp64 sums.  -1 (auto): the reference's norms
+    // except over RCCL with two or more ranks, whose chained walks (ncclSend /
+    // ncclRecv on two communicators split from the halo one, beside it on
+    // other streams) have not run on hardware: there the fp64 sums unless the
+    // caller sets 0
+    int logger_fp64 = -1;
+    // triples split into interior / edge launches (slab_geometry): -1 when a
+    // neighbour is on another device or behind RCCL, 0 never, 1 whenever the
+    // slab is tall enough (option "split": tests run the multi-device launch
+    // order on co-located slabs)
+    int split = -1;
     of2d::SlabExact *ex = nullptr;
     int device = 0;
     float alpha = 0.0f;
@@ -345,10 +354,15 @@ bool remote_neighbour(const of2d_slab *s) {
     return false;
 }
 
-SlabGeometry slab_geometry(const of2d_slab *s) {
+// the slab is tall enough for the interior / edge split (two E-line edges and
+// an interior of at least E lines)
+bool can_split(const of2d_slab *s) {
+    return s->nranks > 1 && s->nrows >= 3 * SlabGeometry().E && s->dimx >= 2;
+}
+SlabGeometry slab_geometry_as(const of2d_slab *s, bool split) {
     SlabGeometry g;
     const int gx = (s->dimx + of2d::kHs3Out - 1) / of2d::kHs3Out;
-    g.split = s->nranks > 1 && s->nrows >= 3 * g.E && s->dimx >= 2 && remote_neighbour(s);
+    g.split = split && can_split(s);
     if (g.split) {
         const int ni = s->nrows - 2 * g.E;
         constexpr int kCommBlocks = 8;
@@ -360,6 +374,19 @@ SlabGeometry slab_geometry(const of2d_slab *s) {
     }
     g.nb = std::max(of2d::hs_partial_blocks(s->P, s->dimx, s->nrows), g.n3);
     return g;
+}
+SlabGeometry slab_geometry(const of2d_slab *s) {
+    return slab_geometry_as(s, s->split > 0 || (s->split < 0 && remote_neighbour(s)));
+}
+// partial-row length for either geometry: the allocation at create, before the
+// group's other slabs (whose devices decide the split) or the option are known
+int partial_blocks_cap(const of2d_slab *s) {
+    return std::max(slab_geometry_as(s, false).nb, slab_geometry_as(s, true).nb);
+}
+// convergence-on runs take the reference's float running sums (run_exact)
+bool exact_logger(const of2d_slab *s) {
+    if (s->logger_fp64 >= 0) return s->logger_fp64 == 0;
+    return !(s->comm && s->nranks > 1);
 }
 }  // namespace
 
@@ -651,7 +678,7 @@ static int slab_create(of2d_slab **out, int dimx, int dimy, float alpha, int ran
         s->It.alloc(dimx, s->nrows, 2);
         s->Iref.alloc(dimx, s->nrows, 3);
         s->Imov.alloc(dimx, s->nrows, 3);
-        const int nb = slab_geometry(s).nb;
+        const int nb = partial_blocks_cap(s);
         OF2D_HIP(hipMalloc(&s->d_partial, sizeof(double) * 2 * (size_t)nb * s->chunk_cap()));
         OF2D_HIP(hipMalloc(&s->d_sums, sizeof(double) * 2 * s->chunk));
         OF2D_HIP(hipMalloc(&s->d_status, 64 * sizeof(unsigned)));
@@ -928,7 +955,7 @@ int of2d_slab_run(of2d_slab *s, int niter, int fixed_iters, int *iters_done) {
         if (s->start_dirty) s->u[s->start].zero(s->st);
         s->start_dirty = true;
         int a = s->start, k0 = 0, done = -1;
-        if (!fixed_iters && !s->logger_fp64) {
+        if (!fixed_iters && exact_logger(s)) {
             done = run_exact(s, niter);
             if (s->fin >= 3) {  // into a buffer of u[] (get_motion, the next run's start)
                 const int x = (s->start + 1) % 3;
@@ -1119,7 +1146,11 @@ int of2d_slab_info(const of2d_slab *s, int *info, int n) {
 int of2d_slab_set_option(of2d_slab *s, const char *key, double value) {
     if (!s || !key) return OF2D_ERR_INVALID_ARGUMENT;
     if (std::strcmp(key, "logger_fp64") == 0) {
-        s->logger_fp64 = value != 0.0;
+        s->logger_fp64 = value < 0.0 ? -1 : (value != 0.0 ? 1 : 0);
+        return OF2D_OK;
+    }
+    if (std::strcmp(key, "split") == 0) {
+        s->split = value < 0.0 ? -1 : (value != 0.0 ? 1 : 0);
         return OF2D_OK;
     }
     if (std::strcmp(key, "hs_gradients_from_image") == 0) {

@@ -52,6 +52,22 @@ def test_ragged_fixed_iterations(gpu, dims, ngpus):
     assert np.array_equal(a[1], b[1])
 
 
+@pytest.mark.parametrize("opts", [{"fixed_iters": 1}, {"logger_fp64": 1}])
+def test_ranks_split_launches(gpu, opts):
+    """The ranks' triples as interior + edge launches (option "slab_split" = 1:
+    the launch order of ranks on distinct devices) on 2 and 4 ranks sharing
+    device 0, with a pyramid whose coarse levels are too short to split:
+    iterations and motion bit-identical to one rank."""
+    ref, mov = S.texture_pair(256, seed=11, ny=400)
+    args = ((256, 400), [150, 100], 1, [0.1], 2, ref, mov)
+    a = run(*args, **opts)
+    for n in (2, 4):
+        b = run(*args, ngpus=n, ngpus_share=1, slab_split=1, **opts)
+        assert b[0] == a[0]
+        assert np.array_equal(b[1], a[1])
+        assert np.array_equal(b[3], a[3])
+
+
 def test_fp64_logger_mode_motion(gpu):
     """logger_fp64: per-rank partial sums added in rank order — the errors
     differ from one rank's in the last bits, the iterates do not."""

@@ -39,7 +39,7 @@ for s in "$@"; do
         ranks) run ranks 600 python -u tools/time_ranks.py ;;
         snbench) run snbench 300 bash -c "tools/seqnorm_bench 4096 12 3 0.95 && tools/seqnorm_bench 4096 12 1 0.95 && tools/seqnorm_bench 4096 12 3 0.8" ;;
         snws) run snws 300 env SNB_WS=1 tools/seqnorm_bench 4096 12 3 0.95 ;;
-        sndebug) run sndebug 300 env OF2D_SN_DEBUG=1 python -u tools/time_convergence.py 4096 1 ;;
+        sndebug) run sndebug 300 env OF2D_LIB_PATH=tools/ab/sndebug/libof2d.so python -u tools/time_convergence.py 4096 1 ;;  # tools/build_variant.sh sndebug registration.cpp -DOF2D_SN_DEBUG=1
         snprof) run snprof 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/$O/${tag}_snprof" -o k -- "$R/tools/seqnorm_bench" 4096 24 3 ;;
         *) echo "unknown step $s"; exit 2 ;;
     esac || exit $?
