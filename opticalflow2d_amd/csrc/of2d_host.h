@@ -113,13 +113,26 @@ struct HostScratch {
 // (Logger.cpp:37-39, Motion.cpp:47) applied to fp64 sums.
 float logger_error(double sum_diff, double sum_prev, double npx);
 
+// The reference-exact Logger's pipeline depth (Registration, below): iterate
+// ring buffers, workspace sets and walk streams (build knobs for A/B runs)
+#ifndef OF2D_SN_RING
+#define OF2D_SN_RING 15
+#endif
+#ifndef OF2D_SN_SETS
+#define OF2D_SN_SETS 4
+#endif
+#ifndef OF2D_SN_WALKERS
+#define OF2D_SN_WALKERS 3
+#endif
+constexpr int kMaxEst = OF2D_SN_RING + 1 > 16 ? OF2D_SN_RING + 1 : 16;
+
 struct Level {
     int dx = 0, dy = 0, P = 0;
     Field<float> Iref, Imov, Iaux, It, Iwar, jac;
     Field<float2> motion[2];
     int mcur = 0;
     Field<float2> dI;
-    Field<float2> est[16];  // [3] .. [15]: only for the exact-norm loop's ring
+    Field<float2> est[kMaxEst];  // [3] .. [kRing]: only for the exact-norm loop's ring
     Field<float2> force, velocity, increment, corr, tmp;
     DevArray<double> cbuf[2];              // Curvature: two x|y double plane pairs (pitch P)
     DevArray<double> cC1T, cC0, cD1T, cD0;  // Curvature: REDFT10 / REDFT01 matrices
@@ -159,12 +172,17 @@ class Registration {
     // (t0: the triple's first iteration, for the stop word of run_exact_pipelined)
     using StepFn3M =
         std::function<void(const float2 *src, float2 *d1, float2 *d2, float2 *d3, int t0)>;
+    // the same with the batch's tile entries taken inside the triple
+    // (launch_hs_jacobi3_fused: B.u = {src, d1, d2, d3}; rec: its records)
+    using StepFn3F = std::function<void(const float2 *src, float2 *d1, float2 *d2, float2 *d3,
+                                        int t0, const SeqnormBatch &B, unsigned *rec)>;
 
    private:
     // nblk[k]: block partials written by step (k = 0), step2 (1), step3 (2)
     int run_chunked(Level &L, int niter, int nb, const StepFn &step, int &final_buf,
                     const StepFn2 &step2 = nullptr, const StepFn3 &step3 = nullptr,
-                    const int *nblk = nullptr, const StepFn3M &step3m = nullptr);
+                    const int *nblk = nullptr, const StepFn3M &step3m = nullptr,
+                    const StepFn3F &step3f = nullptr);
     void ensure_device();
     void estimate_level(int s);
     int loop_hs(Level &L, int niter, float alpha, int &final_buf);
@@ -204,21 +222,28 @@ class Registration {
     // up to three into a ring, each group's norms as one batch on the norm
     // streams); with step3m, run_exact_pipelined
     int run_chunked_exact(Level &L, int niter, int nb, const StepFn &step, int &final_buf,
-                          const StepFn3M &step3m = nullptr);
+                          const StepFn3M &step3m = nullptr, const StepFn3F &step3f = nullptr);
     // HS: triples, blocks of iterations enqueued one ahead of the host's
     // decision, the break also taken on the device (the stop word)
     int run_exact_pipelined(Level &L, int niter, const StepFn &step, int &final_buf,
-                            const StepFn3M &step3m);
+                            const StepFn3M &step3m, const StepFn3F &step3f);
     // a group's norms behind its steps: pass on sn_st_, check and fix on
     // fx_st_, walk (and with B.stop seqnorm_decide) on wk_st_[g mod 3]
+    // (fused: the batch's pass ran inside its triple, ev_step_[g] follows it)
     void enqueue_norms(const SeqnormBatch &B, const Level &L, int g, double npx = 0.0,
-                       float *seqh_out = nullptr);
+                       float *seqh_out = nullptr, bool fused = false);
+    DevArray<unsigned char> d_snrec_;  // the fused triple's records (seqnorm_rec_bytes)
     void print_sn_debug(const Level &L, const int *dbg, int k0, int lo, int hi);
-    hipStream_t sn_st_ = nullptr, fx_st_ = nullptr, wk_st_[3] = {};
+    hipStream_t sn_st_ = nullptr, fx_st_ = nullptr, wk_st_[OF2D_SN_WALKERS] = {};
     static constexpr int kExactEv = 64;  // event ring per group (two blocks in flight)
-    static constexpr int kSeqSets = 4;   // workspace sets: group g's walk is read by g + 4
+    // workspace sets: group g's walk is read (its profile) by group g + kSeqSets
+    static constexpr int kSeqSets = OF2D_SN_SETS;
     static constexpr int kSeqWs = 3 * kSeqSets;
-    static constexpr int kRing = 15;  // iterate buffers: a step waits for the walks 4-5 groups back
+    // iterate buffers: a step waits for the walks kRing / 3 groups back, so
+    // kRing / 3 groups of steps, passes and walks are in flight
+    static constexpr int kRing = OF2D_SN_RING;
+    static_assert(kRing + 1 <= kMaxEst, "Level::est holds the ring");
+    static constexpr int kWalkers = OF2D_SN_WALKERS;  // walk streams
     hipEvent_t ev_step_[kExactEv] = {}, ev_pass_[kExactEv] = {}, ev_fix_[kExactEv] = {},
                ev_walk_[kExactEv] = {};
     DevArray<unsigned char> d_seqws_[kSeqWs];  // seqnorm workspaces (level 0 size)

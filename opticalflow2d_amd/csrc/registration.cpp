@@ -382,8 +382,9 @@ void Registration::seqnorm(const Level &L, const float2 *cur, const float2 *prev
 // iterations m - 1 and m; iterate m + kRing rewrites it after both.  HS takes
 // run_exact_pipelined.
 int Registration::run_chunked_exact(Level &L, int niter, int nb, const StepFn &step,
-                                    int &final_buf, const StepFn3M &step3m) {
-    if (step3m) return run_exact_pipelined(L, niter, step, final_buf, step3m);
+                                    int &final_buf, const StepFn3M &step3m,
+                                    const StepFn3F &step3f) {
+    if (step3m) return run_exact_pipelined(L, niter, step, final_buf, step3m, step3f);
     const double npx = (double)L.dx * L.dy;
     last_err_.clear();
     constexpr int R = kRing;
@@ -438,7 +439,8 @@ int Registration::run_chunked_exact(Level &L, int niter, int nb, const StepFn &s
             t += k;
         }
         // the last walk of each walk stream
-        for (int q = std::max(g - 3, g0); q < g; q++) OF2D_HIP(hipStreamWaitEvent(st_, ev(ev_walk_, q), 0));
+        for (int q = std::max(g - kWalkers, g0); q < g; q++)
+            OF2D_HIP(hipStreamWaitEvent(st_, ev(ev_walk_, q), 0));
         OF2D_HIP(hipMemcpyAsync(hs_.flt, d_seq_.p, sizeof(float) * 2 * C, hipMemcpyDeviceToHost,
                                 st_));
         check_status();  // synchronises st_ (and with it every norm of the chunk)
@@ -469,16 +471,20 @@ int Registration::run_chunked_exact(Level &L, int niter, int nb, const StepFn &s
 // and fix on fx_st_, the walk on wk_st_[g mod 3]; with B.stop, seqnorm_decide
 // after the walk (the sums' copy to seqh_out).  Records ev_walk_[g].
 void Registration::enqueue_norms(const SeqnormBatch &B, const Level &L, int g, double npx,
-                                 float *seqh_out) {
+                                 float *seqh_out, bool fused) {
     auto ev = [](hipEvent_t *e, int q) { return e[q % kExactEv]; };
-    OF2D_HIP(hipStreamWaitEvent(sn_st_, ev(ev_step_, g), 0));
-    if (g >= kSeqSets) OF2D_HIP(hipStreamWaitEvent(sn_st_, ev(ev_walk_, g - kSeqSets), 0));
-    launch_seqnorm_pass(B, L.dx, L.dy, L.P, sn_st_);
-    OF2D_HIP(hipEventRecord(ev(ev_pass_, g), sn_st_));
-    OF2D_HIP(hipStreamWaitEvent(fx_st_, ev(ev_pass_, g), 0));
+    if (fused) {
+        OF2D_HIP(hipStreamWaitEvent(fx_st_, ev(ev_step_, g), 0));
+    } else {
+        OF2D_HIP(hipStreamWaitEvent(sn_st_, ev(ev_step_, g), 0));
+        if (g >= kSeqSets) OF2D_HIP(hipStreamWaitEvent(sn_st_, ev(ev_walk_, g - kSeqSets), 0));
+        launch_seqnorm_pass(B, L.dx, L.dy, L.P, sn_st_);
+        OF2D_HIP(hipEventRecord(ev(ev_pass_, g), sn_st_));
+        OF2D_HIP(hipStreamWaitEvent(fx_st_, ev(ev_pass_, g), 0));
+    }
     launch_seqnorm_refine(B, L.dx, L.dy, L.P, fx_st_);
     OF2D_HIP(hipEventRecord(ev(ev_fix_, g), fx_st_));
-    hipStream_t wk = wk_st_[g % 3];
+    hipStream_t wk = wk_st_[g % kWalkers];
     OF2D_HIP(hipStreamWaitEvent(wk, ev(ev_fix_, g), 0));
     launch_seqnorm_walk(B, L.dx, L.dy, L.P, wk);
     if (B.stop)
@@ -515,7 +521,7 @@ void Registration::print_sn_debug(const Level &L, const int *dbg, int k0, int lo
 // or two single steps (niter not a multiple of three; the single step does
 // not read the stop word) is enqueued after every earlier block is decided.
 int Registration::run_exact_pipelined(Level &L, int niter, const StepFn &step, int &final_buf,
-                                      const StepFn3M &step3m) {
+                                      const StepFn3M &step3m, const StepFn3F &step3f) {
     const double npx = (double)L.dx * L.dy;
     last_err_.clear();
     constexpr int R = kRing;
@@ -539,6 +545,11 @@ int Registration::run_exact_pipelined(Level &L, int niter, const StepFn &step, i
     bool walked[kSeqWs] = {};  // a new loop: each workspace starts from a fresh state
     std::vector<int> grp_of((size_t)std::max(niter, 1));
     int g = 0;
+    // the triples take their batch's tile entries themselves where the tiles
+    // hold whole j-lines (seqnorm_fusable: 4096^2 and its pyramid levels)
+    const bool fuse = bool(step3f) && seqnorm_fusable(L.dx, L.dy);
+    if (fuse && d_snrec_.n < seqnorm_rec_bytes(L.dx, L.dy))
+        d_snrec_.alloc(seqnorm_rec_bytes(L.dx, L.dy));
     // iterations [t, t + k) as group g (t a multiple of three)
     auto enqueue_group = [&](int t, int k) {
         for (int m = t; m < t + k; m++) grp_of[m] = g;
@@ -549,12 +560,7 @@ int Registration::run_exact_pipelined(Level &L, int niter, const StepFn &step, i
                 last = grp_of[q];
                 OF2D_HIP(hipStreamWaitEvent(st_, ev(ev_walk_, last), 0));
             }
-        if (k == 3)
-            step3m(L.est[slot(t)].p, L.est[slot(t + 1)].p, L.est[slot(t + 2)].p,
-                   L.est[slot(t + 3)].p, t);
-        else
-            for (int m = t; m < t + k; m++) step(L.est[slot(m)].p, L.est[slot(m + 1)].p, d_partial_);
-        OF2D_HIP(hipEventRecord(ev(ev_step_, g), st_));
+        const bool fused = fuse && k == 3;
         SeqnormBatch B;
         B.K = k;
         B.stop = stop;
@@ -571,7 +577,21 @@ int Registration::run_exact_pipelined(Level &L, int niter, const StepFn &step, i
             B.out[i] = d_seq_.p + 2 * (size_t)((t + i) % ring2);
             B.dbg[i] = sn_debug ? dbg.p + kDbg * (size_t)((t + i) % ring2) : nullptr;
         }
-        enqueue_norms(B, L, g, npx, hs_.seqh + 2 * (size_t)(t % ring2));
+        if (fused) {
+            // the headers and the merge write workspace set g mod kSeqSets,
+            // which group g - kSeqSets's walk read last (its profile)
+            if (g >= kSeqSets) OF2D_HIP(hipStreamWaitEvent(st_, ev(ev_walk_, g - kSeqSets), 0));
+            launch_seqnorm_headers(B, L.dx, L.dy, L.P, st_);
+            step3f(L.est[slot(t)].p, L.est[slot(t + 1)].p, L.est[slot(t + 2)].p,
+                   L.est[slot(t + 3)].p, t, B, reinterpret_cast<unsigned *>(d_snrec_.p));
+        } else if (k == 3) {
+            step3m(L.est[slot(t)].p, L.est[slot(t + 1)].p, L.est[slot(t + 2)].p,
+                   L.est[slot(t + 3)].p, t);
+        } else {
+            for (int m = t; m < t + k; m++) step(L.est[slot(m)].p, L.est[slot(m + 1)].p, d_partial_);
+        }
+        OF2D_HIP(hipEventRecord(ev(ev_step_, g), st_));
+        enqueue_norms(B, L, g, npx, hs_.seqh + 2 * (size_t)(t % ring2), fused);
         g++;
     };
     const int ntrip = niter / 3 * 3;
@@ -592,7 +612,9 @@ int Registration::run_exact_pipelined(Level &L, int niter, const StepFn &step, i
     // ring and the stop word), the status, and the device's break against the
     // host's
     auto finish = [&](int tbreak) {
-        for (hipStream_t s : {sn_st_, fx_st_, wk_st_[0], wk_st_[1], wk_st_[2]}) {
+        std::vector<hipStream_t> side = {sn_st_, fx_st_};
+        for (hipStream_t w : wk_st_) side.push_back(w);
+        for (hipStream_t s : side) {
             OF2D_HIP(hipEventRecord(ev_join_, s));
             OF2D_HIP(hipStreamWaitEvent(st_, ev_join_, 0));
         }
@@ -607,7 +629,7 @@ int Registration::run_exact_pipelined(Level &L, int niter, const StepFn &step, i
     for (int b = 0; b < nblocks; b++) {
         if (b + 1 < nbt) enqueue_block(b + 1);  // one block ahead
         // block b's sums: the last walk of each walk stream, then its decide
-        for (int q = std::max(gbeg[b + 1] - 3, gbeg[b]); q < gbeg[b + 1]; q++)
+        for (int q = std::max(gbeg[b + 1] - kWalkers, gbeg[b]); q < gbeg[b + 1]; q++)
             OF2D_HIP(hipEventSynchronize(ev(ev_walk_, q)));
         if (sn_debug) {
             for (int t = lo_of(b); t < hi_of(b); t++) {
@@ -650,8 +672,8 @@ int Registration::run_exact_pipelined(Level &L, int niter, const StepFn &step, i
 // src_of(a, t) and writes dst_of(a, t)).
 int Registration::run_chunked(Level &L, int niter, int nb, const StepFn &step, int &final_buf,
                               const StepFn2 &step2, const StepFn3 &step3, const int *nblk,
-                              const StepFn3M &step3m) {
-    if (exact_norms()) return run_chunked_exact(L, niter, nb, step, final_buf, step3m);
+                              const StepFn3M &step3m, const StepFn3F &step3f) {
+    if (exact_norms()) return run_chunked_exact(L, niter, nb, step, final_buf, step3m, step3f);
     const double npx = (double)L.dx * L.dy;
     last_err_.clear();
     if (fixed_ && d_all_.n < 2 * (size_t)niter) {
@@ -786,7 +808,18 @@ int Registration::loop_hs(Level &L, int niter, float alpha, int &final_buf) {
                                   : nullptr,
                               d1, d2, reinterpret_cast<const int *>(d_status_ + kStopWord), t0);
         })
-              : StepFn3M());
+              : StepFn3M(),
+        pairs ? StepFn3F([&](const float2 *src, float2 *d1, float2 *d2, float2 *d3, int t0,
+                             const SeqnormBatch &B, unsigned *rec) {
+            launch_hs_jacobi3_fused(src, d1, d2, d3, L.dI.p, L.It.p, L.P, L.dx, L.dy, alphasq,
+                                    d_status_, range_flag,
+                                    (gi_ < 0 ? hs3_gradients_from_image(L.dx, L.dy) : gi_ != 0)
+                                        ? L.Iaux.p
+                                        : nullptr,
+                                    reinterpret_cast<const int *>(d_status_ + kStopWord), t0, B,
+                                    rec, st_);
+        })
+              : StepFn3F());
 }
 
 // WrapperOpticalFlow2d.cpp:105-117 -> Motion::copy_motion_to_input

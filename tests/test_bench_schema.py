@@ -9,7 +9,7 @@ import bench
 
 CONTRACT = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
             "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config",
-            "roofline", "cpu_baseline"}
+            "roofline", "cpu_baseline", "default_semantics"}
 
 
 def test_default_workloads():
@@ -70,6 +70,12 @@ def test_record_schema(world):
     assert rf["frac"] == pytest.approx(rf["achieved"] / 8000.0, rel=1e-3)
     assert rf["traffic"] is None and rf["traffic_source"] is None
     assert rf["kernel"].startswith("of2d::hs::jacobi3_kernel")
+    assert r["default_semantics"] is None  # measured on a GPU only, outside `value`
+
+
+def test_default_semantics_flag():
+    assert bench.parse_args(["--no-default-semantics"]).no_default_semantics
+    assert not bench.parse_args([]).no_default_semantics
 
 
 def test_traffic_only_for_its_grid_and_kernel():

@@ -11,7 +11,8 @@ from collections import defaultdict
 
 
 def fam(name):
-    for k in ("jacobi3_mid", "seqnorm_tables", "seqnorm_walk", "seqnorm_fix", "seqnorm_entries", "seqnorm_check",
+    for k in ("jacobi3_mid", "jacobi3_fused", "seqnorm_headers", "seqnorm_merge", "seqnorm_tables",
+              "seqnorm_walk", "seqnorm_fix", "seqnorm_entries", "seqnorm_check",
               "jacobi3_kernel", "jacobi_kernel"):
         if k in name:
             return k
@@ -23,7 +24,7 @@ for r in csv.DictReader(open(sys.argv[1])):
     rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), fam(r["Kernel_Name"]),
                  r["Queue_Id"]))
 rows.sort()
-mids = [r for r in rows if r[2] == "jacobi3_mid"]
+mids = [r for r in rows if r[2] in ("jacobi3_mid", "jacobi3_fused")]
 # the longest run of mid launches less than 2 ms apart
 best, cur = [], [mids[0]]
 for a, b in zip(mids, mids[1:]):

@@ -9,7 +9,8 @@ import sys
 
 
 def short(name):
-    for k in ("jacobi3_mid", "seqnorm_tables", "seqnorm_walk", "seqnorm_entries",
+    for k in ("jacobi3_mid", "jacobi3_fused", "seqnorm_headers", "seqnorm_merge",
+              "seqnorm_tables", "seqnorm_walk", "seqnorm_entries",
               "seqnorm_check_sums", "seqnorm_check_scan", "seqnorm_check", "seqnorm_decide",
               "seqnorm_offset", "reduce_partials", "fillBuffer", "copyBuffer",
               "jacobi3_kernel", "jacobi_kernel"):
@@ -25,7 +26,7 @@ for r in csv.DictReader(open(sys.argv[1])):
 rows.sort()
 first = int(sys.argv[2]) if len(sys.argv) > 2 else 40
 nb = int(sys.argv[3]) if len(sys.argv) > 3 else 3
-mids = [r for r in rows if r[2] == "jacobi3_mid"]
+mids = [r for r in rows if r[2] in ("jacobi3_mid", "jacobi3_fused")]
 t0 = mids[first][0]
 t1 = mids[first + nb][0]
 last_end = {}
