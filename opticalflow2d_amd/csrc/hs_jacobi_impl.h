@@ -580,26 +580,15 @@ __device__ __forceinline__ void progress_prio(int done, int total) {
 // MID: the two intermediate iterates u1, u2 of the owned rows are stored too
 // (to m1, m2): the reference-exact Logger needs every iterate in memory
 // (registration.cpp run_chunked_exact), 16 B/px more per launch.
-// HOOK: called once per owned row step with the four iterates of that j-line
-// (u0 = the input, u1, u2, u3 = the output) — the reference-exact Logger's
-// tile entries taken where the iterates sit in registers (seqnorm_kernels.hip
-// SnFuseHook); NoRowHook compiles to nothing.
-struct NoRowHook {
-    static constexpr bool kActive = false;
-    template <class R>
-    __device__ __forceinline__ void row(int, int, int, bool, bool, const R &, const R &,
-                                        const R &, const R &) const {}
-};
 template <int ROWS, int WAVES, bool XCD, int MINB, int UNR, int PRIO, bool ALT, bool GI,
-          bool MID, class HOOK = NoRowHook>
+          bool MID>
 __device__ __forceinline__ void jacobi3_body(
     const float2 *__restrict__ uo, float2 *__restrict__ un, const float2 *__restrict__ dI,
     const float *__restrict__ It, int P, int dimx, int nrows, int row0, int dimy, float alphasq,
     int glo, int ghi, double *__restrict__ partial, double *__restrict__ partial2,
     double *__restrict__ partial3, unsigned *__restrict__ status, int band0, int gx, int gy,
     int rows, const unsigned *__restrict__ range_flag, int jlo, int jhi,
-    const float *__restrict__ Ia, float2 *__restrict__ m1, float2 *__restrict__ m2,
-    const HOOK &hook = HOOK{}) {
+    const float *__restrict__ Ia, float2 *__restrict__ m1, float2 *__restrict__ m2) {
     int bx = (int)blockIdx.x, by = (int)blockIdx.y;
     if constexpr (XCD) {
         if (!xcd_block(gx, gy, bx, by)) return;
@@ -855,7 +844,6 @@ __device__ __forceinline__ void jacobi3_body(
                 if (sp + 2 < n) stmid(m1, sp + 2, vj2);
                 if (sp + 1 < n) stmid(m2, sp + 1, wj1);
             }
-            if constexpr (HOOK::kActive) hook.row(J(sp), bx, x, own, in1, uj, vj, wj, z);
             if (own) {
                 if constexpr (!MID) {  // MID: the exact Logger takes its own norms
                     norms(vj, uj, s1d, s1p);

@@ -296,21 +296,6 @@ void launch_seqnorm_decide(const float *seq, int K, int t0, double npx, int *sto
 // with more than one candidate, with none (out[12])
 void seqnorm_ws_stats(const void *ws, int dimx, int dimy, unsigned *out);
 void launch_seqnorm_pass(const SeqnormBatch &b, int dimx, int dimy, int P, hipStream_t st);
-// The pass of a triple's batch fused into the triple kernel (round 5), for
-// grids whose tiles hold whole j-lines (kSnTile % dimx == 0): launch_seqnorm_
-// headers (the batch's candidate binades, before the triple), then
-// launch_hs_jacobi3_fused: the MID triple u_old -> u1, u2, u3 (B.u = {u_old,
-// u1, u2, u3}) whose row steps add the batch's tile entries into `rec`
-// (seqnorm_rec_bytes), and the merge of the records into the batch's
-// workspaces — what launch_seqnorm_pass would write, entries bit for bit.
-bool seqnorm_fusable(int dimx, int dimy);
-size_t seqnorm_rec_bytes(int dimx, int dimy);
-void launch_seqnorm_headers(const SeqnormBatch &b, int dimx, int dimy, int P, hipStream_t st);
-void launch_hs_jacobi3_fused(const float2 *u_old, float2 *u1, float2 *u2, float2 *u3,
-                             const float2 *dI, const float *It, int P, int dimx, int dimy,
-                             float alphasq, unsigned *status, const unsigned *range_flag,
-                             const float *Ia, const int *stop, int stop_t0,
-                             const SeqnormBatch &B, unsigned *rec, hipStream_t st);
 void launch_seqnorm_refine(const SeqnormBatch &b, int dimx, int dimy, int P, hipStream_t st);
 void launch_seqnorm_walk(const SeqnormBatch &b, int dimx, int dimy, int P, hipStream_t st);
 

@@ -172,17 +172,12 @@ class Registration {
     // (t0: the triple's first iteration, for the stop word of run_exact_pipelined)
     using StepFn3M =
         std::function<void(const float2 *src, float2 *d1, float2 *d2, float2 *d3, int t0)>;
-    // the same with the batch's tile entries taken inside the triple
-    // (launch_hs_jacobi3_fused: B.u = {src, d1, d2, d3}; rec: its records)
-    using StepFn3F = std::function<void(const float2 *src, float2 *d1, float2 *d2, float2 *d3,
-                                        int t0, const SeqnormBatch &B, unsigned *rec)>;
 
    private:
     // nblk[k]: block partials written by step (k = 0), step2 (1), step3 (2)
     int run_chunked(Level &L, int niter, int nb, const StepFn &step, int &final_buf,
                     const StepFn2 &step2 = nullptr, const StepFn3 &step3 = nullptr,
-                    const int *nblk = nullptr, const StepFn3M &step3m = nullptr,
-                    const StepFn3F &step3f = nullptr);
+                    const int *nblk = nullptr, const StepFn3M &step3m = nullptr);
     void ensure_device();
     void estimate_level(int s);
     int loop_hs(Level &L, int niter, float alpha, int &final_buf);
@@ -222,17 +217,15 @@ class Registration {
     // up to three into a ring, each group's norms as one batch on the norm
     // streams); with step3m, run_exact_pipelined
     int run_chunked_exact(Level &L, int niter, int nb, const StepFn &step, int &final_buf,
-                          const StepFn3M &step3m = nullptr, const StepFn3F &step3f = nullptr);
+                          const StepFn3M &step3m = nullptr);
     // HS: triples, blocks of iterations enqueued one ahead of the host's
     // decision, the break also taken on the device (the stop word)
     int run_exact_pipelined(Level &L, int niter, const StepFn &step, int &final_buf,
-                            const StepFn3M &step3m, const StepFn3F &step3f);
+                            const StepFn3M &step3m);
     // a group's norms behind its steps: pass on sn_st_, check and fix on
     // fx_st_, walk (and with B.stop seqnorm_decide) on wk_st_[g mod 3]
-    // (fused: the batch's pass ran inside its triple, ev_step_[g] follows it)
     void enqueue_norms(const SeqnormBatch &B, const Level &L, int g, double npx = 0.0,
-                       float *seqh_out = nullptr, bool fused = false);
-    DevArray<unsigned char> d_snrec_;  // the fused triple's records (seqnorm_rec_bytes)
+                       float *seqh_out = nullptr);
     void print_sn_debug(const Level &L, const int *dbg, int k0, int lo, int hi);
     hipStream_t sn_st_ = nullptr, fx_st_ = nullptr, wk_st_[OF2D_SN_WALKERS] = {};
     static constexpr int kExactEv = 64;  // event ring per group (two blocks in flight)

@@ -382,9 +382,8 @@ void Registration::seqnorm(const Level &L, const float2 *cur, const float2 *prev
 // iterations m - 1 and m; iterate m + kRing rewrites it after both.  HS takes
 // run_exact_pipelined.
 int Registration::run_chunked_exact(Level &L, int niter, int nb, const StepFn &step,
-                                    int &final_buf, const StepFn3M &step3m,
-                                    const StepFn3F &step3f) {
-    if (step3m) return run_exact_pipelined(L, niter, step, final_buf, step3m, step3f);
+                                    int &final_buf, const StepFn3M &step3m) {
+    if (step3m) return run_exact_pipelined(L, niter, step, final_buf, step3m);
     const double npx = (double)L.dx * L.dy;
     last_err_.clear();
     constexpr int R = kRing;
@@ -471,17 +470,13 @@ int Registration::run_chunked_exact(Level &L, int niter, int nb, const StepFn &s
 // and fix on fx_st_, the walk on wk_st_[g mod 3]; with B.stop, seqnorm_decide
 // after the walk (the sums' copy to seqh_out).  Records ev_walk_[g].
 void Registration::enqueue_norms(const SeqnormBatch &B, const Level &L, int g, double npx,
-                                 float *seqh_out, bool fused) {
+                                 float *seqh_out) {
     auto ev = [](hipEvent_t *e, int q) { return e[q % kExactEv]; };
-    if (fused) {
-        OF2D_HIP(hipStreamWaitEvent(fx_st_, ev(ev_step_, g), 0));
-    } else {
-        OF2D_HIP(hipStreamWaitEvent(sn_st_, ev(ev_step_, g), 0));
-        if (g >= kSeqSets) OF2D_HIP(hipStreamWaitEvent(sn_st_, ev(ev_walk_, g - kSeqSets), 0));
-        launch_seqnorm_pass(B, L.dx, L.dy, L.P, sn_st_);
-        OF2D_HIP(hipEventRecord(ev(ev_pass_, g), sn_st_));
-        OF2D_HIP(hipStreamWaitEvent(fx_st_, ev(ev_pass_, g), 0));
-    }
+    OF2D_HIP(hipStreamWaitEvent(sn_st_, ev(ev_step_, g), 0));
+    if (g >= kSeqSets) OF2D_HIP(hipStreamWaitEvent(sn_st_, ev(ev_walk_, g - kSeqSets), 0));
+    launch_seqnorm_pass(B, L.dx, L.dy, L.P, sn_st_);
+    OF2D_HIP(hipEventRecord(ev(ev_pass_, g), sn_st_));
+    OF2D_HIP(hipStreamWaitEvent(fx_st_, ev(ev_pass_, g), 0));
     launch_seqnorm_refine(B, L.dx, L.dy, L.P, fx_st_);
     OF2D_HIP(hipEventRecord(ev(ev_fix_, g), fx_st_));
     hipStream_t wk = wk_st_[g % kWalkers];
@@ -521,7 +516,7 @@ void Registration::print_sn_debug(const Level &L, const int *dbg, int k0, int lo
 // or two single steps (niter not a multiple of three; the single step does
 // not read the stop word) is enqueued after every earlier block is decided.
 int Registration::run_exact_pipelined(Level &L, int niter, const StepFn &step, int &final_buf,
-                                      const StepFn3M &step3m, const StepFn3F &step3f) {
+                                      const StepFn3M &step3m) {
     const double npx = (double)L.dx * L.dy;
     last_err_.clear();
     constexpr int R = kRing;
@@ -545,11 +540,6 @@ int Registration::run_exact_pipelined(Level &L, int niter, const StepFn &step, i
     bool walked[kSeqWs] = {};  // a new loop: each workspace starts from a fresh state
     std::vector<int> grp_of((size_t)std::max(niter, 1));
     int g = 0;
-    // the triples take their batch's tile entries themselves where the tiles
-    // hold whole j-lines (seqnorm_fusable: 4096^2 and its pyramid levels)
-    const bool fuse = bool(step3f) && seqnorm_fusable(L.dx, L.dy);
-    if (fuse && d_snrec_.n < seqnorm_rec_bytes(L.dx, L.dy))
-        d_snrec_.alloc(seqnorm_rec_bytes(L.dx, L.dy));
     // iterations [t, t + k) as group g (t a multiple of three)
     auto enqueue_group = [&](int t, int k) {
         for (int m = t; m < t + k; m++) grp_of[m] = g;
@@ -560,7 +550,12 @@ int Registration::run_exact_pipelined(Level &L, int niter, const StepFn &step, i
                 last = grp_of[q];
                 OF2D_HIP(hipStreamWaitEvent(st_, ev(ev_walk_, last), 0));
             }
-        const bool fused = fuse && k == 3;
+        if (k == 3)
+            step3m(L.est[slot(t)].p, L.est[slot(t + 1)].p, L.est[slot(t + 2)].p,
+                   L.est[slot(t + 3)].p, t);
+        else
+            for (int m = t; m < t + k; m++) step(L.est[slot(m)].p, L.est[slot(m + 1)].p, d_partial_);
+        OF2D_HIP(hipEventRecord(ev(ev_step_, g), st_));
         SeqnormBatch B;
         B.K = k;
         B.stop = stop;
@@ -577,21 +572,7 @@ int Registration::run_exact_pipelined(Level &L, int niter, const StepFn &step, i
             B.out[i] = d_seq_.p + 2 * (size_t)((t + i) % ring2);
             B.dbg[i] = sn_debug ? dbg.p + kDbg * (size_t)((t + i) % ring2) : nullptr;
         }
-        if (fused) {
-            // the headers and the merge write workspace set g mod kSeqSets,
-            // which group g - kSeqSets's walk read last (its profile)
-            if (g >= kSeqSets) OF2D_HIP(hipStreamWaitEvent(st_, ev(ev_walk_, g - kSeqSets), 0));
-            launch_seqnorm_headers(B, L.dx, L.dy, L.P, st_);
-            step3f(L.est[slot(t)].p, L.est[slot(t + 1)].p, L.est[slot(t + 2)].p,
-                   L.est[slot(t + 3)].p, t, B, reinterpret_cast<unsigned *>(d_snrec_.p));
-        } else if (k == 3) {
-            step3m(L.est[slot(t)].p, L.est[slot(t + 1)].p, L.est[slot(t + 2)].p,
-                   L.est[slot(t + 3)].p, t);
-        } else {
-            for (int m = t; m < t + k; m++) step(L.est[slot(m)].p, L.est[slot(m + 1)].p, d_partial_);
-        }
-        OF2D_HIP(hipEventRecord(ev(ev_step_, g), st_));
-        enqueue_norms(B, L, g, npx, hs_.seqh + 2 * (size_t)(t % ring2), fused);
+        enqueue_norms(B, L, g, npx, hs_.seqh + 2 * (size_t)(t % ring2));
         g++;
     };
     const int ntrip = niter / 3 * 3;
@@ -672,8 +653,8 @@ int Registration::run_exact_pipelined(Level &L, int niter, const StepFn &step, i
 // src_of(a, t) and writes dst_of(a, t)).
 int Registration::run_chunked(Level &L, int niter, int nb, const StepFn &step, int &final_buf,
                               const StepFn2 &step2, const StepFn3 &step3, const int *nblk,
-                              const StepFn3M &step3m, const StepFn3F &step3f) {
-    if (exact_norms()) return run_chunked_exact(L, niter, nb, step, final_buf, step3m, step3f);
+                              const StepFn3M &step3m) {
+    if (exact_norms()) return run_chunked_exact(L, niter, nb, step, final_buf, step3m);
     const double npx = (double)L.dx * L.dy;
     last_err_.clear();
     if (fixed_ && d_all_.n < 2 * (size_t)niter) {
@@ -808,18 +789,7 @@ int Registration::loop_hs(Level &L, int niter, float alpha, int &final_buf) {
                                   : nullptr,
                               d1, d2, reinterpret_cast<const int *>(d_status_ + kStopWord), t0);
         })
-              : StepFn3M(),
-        pairs ? StepFn3F([&](const float2 *src, float2 *d1, float2 *d2, float2 *d3, int t0,
-                             const SeqnormBatch &B, unsigned *rec) {
-            launch_hs_jacobi3_fused(src, d1, d2, d3, L.dI.p, L.It.p, L.P, L.dx, L.dy, alphasq,
-                                    d_status_, range_flag,
-                                    (gi_ < 0 ? hs3_gradients_from_image(L.dx, L.dy) : gi_ != 0)
-                                        ? L.Iaux.p
-                                        : nullptr,
-                                    reinterpret_cast<const int *>(d_status_ + kStopWord), t0, B,
-                                    rec, st_);
-        })
-              : StepFn3F());
+              : StepFn3M());
 }
 
 // WrapperOpticalFlow2d.cpp:105-117 -> Motion::copy_motion_to_input

@@ -71,7 +71,6 @@
 #include <vector>
 
 #include "of2d_device.h"
-#include "hs_jacobi_impl.h"
 
 namespace of2d {
 namespace {
@@ -1379,284 +1378,6 @@ __global__ void seqnorm_decide(const float *__restrict__ seq, int K, int t0, flo
     if (err < 0.001f && t0 + i > 1) atomicMin(stop, t0 + i);
 }
 
-
-// ---------------------------------------------------------------- fused pass
-// The pass of a triple's batch taken inside the triple kernel (round 5).
-// jacobi3_mid holds all four iterates of a j-line in registers at one row step
-// (u0 the input, u1, u2, u3 = its output); seqnorm_tables read them back from
-// HBM afterwards (4 arrays, 32 B/px, 537 MB per batch at 4096^2).  With tiles
-// of whole j-lines or of several (kSnTile % dimx == 0: 4096^2, its pyramid
-// levels) every (j-line, strip) of the triple kernel lies in one tile, so the
-// row step can add its terms' increments itself:
-//   seqnorm_headers   before the triple: every tile's candidate binades from
-//                     the profile, exactly as seqnorm_tables takes them
-//   the triple        (SnFuseHook, per row step and wave) per norm of the
-//                     batch: the fp32 magnitude sum, the nonzero lanes and the
-//                     increments for the tile's <= 2 candidates (fp32
-//                     estimate, the exact fp64 sequence in waves where a lane
-//                     is undecided: sn_wave_pass's arithmetic), reduced over
-//                     the wave into one 128-B record per (j-line, strip)
-//   seqnorm_merge     one wave per tile: its records' saturating sums, fp64
-//                     tile sums, nonzero-segment masks and headers, written
-//                     as seqnorm_tables writes them
-// so the check, entries and walk run unchanged on the same workspace
-// contents.  The increments of a term are a function of the term and the
-// candidate only (the estimate decides exactly when it decides), so the
-// entries equal the pass's bit for bit; the fp64 tile sums are predictions
-// (their summation order differs and only moves work).
-constexpr int kSnRec = 32;  // dwords per (j-line, strip) record
-// record word of norm k = 2 i + n: [k] fp32 magnitude sum, [6 + k] / [12 + k]
-// entries of candidates 0 / 1 (kSnBad on a tie or NaN), [18 + 2k] / [19 + 2k]
-// the 64-bit ballot of lanes with a nonzero magnitude
-
-// the tile's candidates of one norm, as seqnorm_tables takes them
-__device__ __forceinline__ unsigned sn_predict_header(const SnWs &ws, int use_prof, int n,
-                                                      unsigned nt, unsigned b) {
-    if (!use_prof) return hdr_pack(0, 0);
-    const int src = prof_src(ws, n);
-    const float *pr = ws.prof + (size_t)src * (nt + 1);
-    const float t0 = ws.tot[2 * src], t1 = ws.tot[2 * src + 1];
-    double r = (src == n && t1 > 0.0f && t0 > 0.0f) ? (double)t0 / t1 : 1.0;
-    r = r < 0.25 ? 0.25 : (r > 4.0 ? 4.0 : r);
-    return cand_window((double)pr[b] * r * (1.0 - kSnWin), (double)pr[b + 1] * r / (1.0 - kSnWin));
-}
-
-// one thread per tile: the headers of the batch's 2K norms (more than two
-// candidates on any norm: all pending, left to the entries kernel), the
-// check's list counters reset
-template <int K>
-__global__ __launch_bounds__(256) void seqnorm_headers(unsigned nt, SnJobs J) {
-    if (sn_block_stopped(J)) return;
-    if (blockIdx.x == 0 && threadIdx.x < 4)
-#pragma unroll
-        for (int i = 0; i < K; i++) J.ws[i].cnt[threadIdx.x] = 0;
-    const unsigned b = blockIdx.x * 256 + threadIdx.x;
-    if (b >= nt) return;
-    unsigned hd[K][2];
-    int ncmax = 0;
-#pragma unroll
-    for (int i = 0; i < K; i++)
-#pragma unroll
-        for (int n = 0; n < 2; n++) {
-            hd[i][n] = sn_predict_header(J.ws[i], J.use_prof[i], n, nt, b);
-            ncmax = max(ncmax, hdr_nc(hd[i][n]));
-        }
-#pragma unroll
-    for (int i = 0; i < K; i++)
-#pragma unroll
-        for (int n = 0; n < 2; n++) {
-            unsigned h = hd[i][n];
-            if (ncmax > 2 && hdr_nc(h)) h |= kHdrPending;
-            J.ws[i].H[2 * (size_t)b + n] = h;
-        }
-}
-
-// wave sum of a float (a prediction: any order), in every lane's result
-__device__ __forceinline__ float wave_fsum(float v) {
-    auto dpp = [](float x, auto ctrl, auto rows) {
-        return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), decltype(ctrl)::value,
-                                                          decltype(rows)::value, 0xF, true));
-    };
-    using I = std::integral_constant<int, 0>;
-    (void)I{};
-    v += dpp(v, std::integral_constant<int, 0x111>{}, std::integral_constant<int, 0xF>{});
-    v += dpp(v, std::integral_constant<int, 0x112>{}, std::integral_constant<int, 0xF>{});
-    v += dpp(v, std::integral_constant<int, 0x114>{}, std::integral_constant<int, 0xF>{});
-    v += dpp(v, std::integral_constant<int, 0x118>{}, std::integral_constant<int, 0xF>{});
-    v += dpp(v, std::integral_constant<int, 0x142>{}, std::integral_constant<int, 0xA>{});
-    v += dpp(v, std::integral_constant<int, 0x143>{}, std::integral_constant<int, 0xC>{});
-    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
-}
-
-// rv with lane L set to the wave-uniform v (v_writelane_b32: one VALU op)
-template <int L>
-__device__ __forceinline__ unsigned sn_writelane(unsigned rv, unsigned v) {
-    const int s = __builtin_amdgcn_readfirstlane((int)v);
-    asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(rv) : "s"(s), "n"(L));
-    return rv;
-}
-
-struct SnFuseHook {
-    static constexpr bool kActive = true;
-    unsigned *rec;          // [rows][gx][kSnRec]
-    const unsigned *H[3];   // the batch's headers (seqnorm_headers)
-    int dimx, gx, rlog;     // rlog: log2(j-lines per tile)
-    // j-line j (wave-uniform), strip bx; the lane's px x, x + 1 (own: lanes
-    // 2..61 inside the grid; in1: x + 1 too); u0..u3 the iterates there
-    template <class R>
-    __device__ __forceinline__ void row(int j, int bx, int x, bool own, bool in1, const R &u0,
-                                        const R &u1, const R &u2, const R &u3) const {
-        const int lane = threadIdx.x & 63;
-        const unsigned b = (unsigned)j >> rlog;
-        const R *u[4] = {&u0, &u1, &u2, &u3};
-        unsigned rv = 0u;  // lane w: record word w
-        auto put = [&](int k, unsigned a, unsigned T0, unsigned T1, unsigned long long zb)
-            __attribute__((always_inline)) {
-            // k is a constant after unrolling: one v_writelane each
-            const unsigned w[5] = {a, T0, T1, (unsigned)zb, (unsigned)(zb >> 32)};
-            const int at[5] = {k, 6 + k, 12 + k, 18 + 2 * k, 19 + 2 * k};
-#pragma unroll
-            for (int q = 0; q < 5; q++) rv = (lane == at[q]) ? w[q] : rv;
-        };
-#pragma unroll
-        for (int i = 0; i < 3; i++) {
-#pragma unroll
-            for (int n = 0; n < 2; n++) {
-                const int k = 2 * i + n;
-                const unsigned h = (unsigned)__builtin_amdgcn_readfirstlane((int)H[i][2 * (size_t)b + n]);
-                const int nc = (h & kHdrPending) ? 0 : hdr_nc(h);
-                const int e0 = hdr_elo(h);
-                const float sc0 = nc > 0 ? sn_scale32(e0) : 0.0f;
-                const float sc1 = nc > 1 ? sn_scale32(e0 + 1) : 0.0f;
-                float fs = 0.0f;
-                unsigned t0 = 0u, t1 = 0u, bl = 0u;
-                bool nzl = false;
-#pragma unroll
-                for (int q = 0; q < 2; q++) {
-                    const bool valid = own && (q == 0 || in1);
-                    // Field::operator- (Field.tpp:305-334) for |cur - prev|
-                    const float2 pv = u[i]->v[q], cv = u[i + 1]->v[q];
-                    float vx = n ? pv.x : cv.x - pv.x, vy = n ? pv.y : cv.y - pv.y;
-                    vx = valid ? vx : 0.0f;
-                    vy = valid ? vy : 0.0f;
-                    const SnEst v = sn_est(vx, vy);
-                    nzl |= v.nz;
-                    unsigned m0 = 0u, m1 = 0u;
-                    bool unc = !v.ok;
-                    if (nc > 0) unc |= !sn_incr_est(v, sc0, m0);
-                    if (nc > 1) unc |= !sn_incr_est(v, sc1, m1);
-                    float dv = v.d;
-                    if (sn_ballot(unc)) {
-                        float xx = vx, yy = vy;
-                        asm volatile("" : "+v"(xx), "+v"(yy));
-                        const double dd = sn_mag(xx, yy);
-                        dv = v.ok ? dv : (float)dd;
-                        bool bad0 = false, bad1 = false;
-                        m0 = sn_incr(dd, nc > 0 ? sn_scale(e0) : 0.0, bad0);
-                        m1 = sn_incr(dd, nc > 1 ? sn_scale(e0 + 1) : 0.0, bad1);
-                        bl |= (bad0 ? 1u : 0u) | (bad1 ? 2u : 0u);
-                    }
-                    fs += dv;
-                    t0 += m0;
-                    t1 += m1;
-                }
-                const float a = wave_fsum(fs);
-                const unsigned long long zb = sn_ballot(nzl);
-                unsigned T0 = 0u, T1 = 0u;
-                if (nc > 0) {
-                    const unsigned s = wave_sum(t0 < kSnSat ? t0 : kSnSat);  // <= 64 2^25
-                    T0 = (s < kSnSat ? s : kSnSat) | (sn_ballot(bl & 1u) ? kSnBad : 0u);
-                }
-                if (nc > 1) {
-                    const unsigned s = wave_sum(t1 < kSnSat ? t1 : kSnSat);
-                    T1 = (s < kSnSat ? s : kSnSat) | (sn_ballot(bl & 2u) ? kSnBad : 0u);
-                }
-                put(k, __float_as_uint(a), T0, T1, zb);
-
-            }
-        }
-        if (lane < 30) rec[((size_t)j * gx + bx) * kSnRec + lane] = rv;
-    }
-};
-
-#ifndef OF2D_SN_FUSE_MINB
-#define OF2D_SN_FUSE_MINB 4  // resident 4-wave blocks per CU the fused triple is compiled for
-#endif
-#ifndef OF2D_SN_FUSE_UNR
-#define OF2D_SN_FUSE_UNR 4  // row steps per trip of its march loop
-#endif
-template <bool GI>
-__global__ __launch_bounds__(64 * kHs3Waves, OF2D_SN_FUSE_MINB) void jacobi3_fused_kernel(
-    const float2 *__restrict__ uo, float2 *__restrict__ un, const float2 *__restrict__ dI,
-    const float *__restrict__ It, int P, int dimx, int nrows, int dimy, float alphasq, int glo,
-    int ghi, unsigned *__restrict__ status, int gx, int gy, int rows,
-    const unsigned *__restrict__ range_flag, const float *__restrict__ Ia, float2 *__restrict__ m1,
-    float2 *__restrict__ m2, const int *__restrict__ stop, int stop_t0, SnFuseHook hook) {
-    // the loop broke before this triple's first iteration (seqnorm_decide)
-    if (stop && __hip_atomic_load(stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < stop_t0)
-        return;
-    hs::jacobi3_body<0, kHs3Waves, true, OF2D_SN_FUSE_MINB, OF2D_SN_FUSE_UNR, 1, true, GI, true,
-                     SnFuseHook>(
-        uo, un, dI, It, P, dimx, nrows, 0, dimy, alphasq, glo, ghi, nullptr, nullptr, nullptr,
-        status, 0, gx, gy, rows, range_flag, -1, -1, Ia, m1, m2, hook);
-}
-
-// one wave per tile: its records (j-lines j0 .. j0 + 2^rlog - 1, strips
-// 0 .. gx - 1) into the workspace words seqnorm_tables writes: A (fp64 sum of
-// the records' sums), Z (segment s of the tile: a record lane with a nonzero
-// magnitude among its two px), T of the header's candidates (saturating
-// sums, kSnBad ORed), H (kHdrZero / kHdrNan as the pass sets them)
-template <int K>
-__global__ __launch_bounds__(256) void seqnorm_merge(unsigned nt, int dimx, int dimy, int gx, int rlog,
-                                                     const unsigned *__restrict__ rec, SnJobs J) {
-    if (sn_block_stopped(J)) return;
-    const unsigned b = (unsigned)__builtin_amdgcn_readfirstlane(
-        (int)(blockIdx.x * 4 + threadIdx.x / 64));
-    if (b >= nt) return;
-    const int lane = threadIdx.x & 63;
-    const int j0 = (int)(b << rlog), j1 = min(j0 + (1 << rlog), dimy);
-    const int nrec = (j1 - j0) * gx;
-    double A[6] = {};
-    unsigned T0[6] = {}, T1[6] = {};
-    unsigned long long Z[6] = {};
-    for (int r0 = 0; r0 < nrec; r0 += 64) {
-        const int r = r0 + lane;
-        if (r >= nrec) continue;
-        const int j = j0 + r / gx, bx = r % gx;
-        const unsigned *w = rec + ((size_t)j * gx + bx) * kSnRec;
-        // the record's own lanes 2..61 cover columns c0 + 2 (l - 2) (two px
-        // each, never across a 64-term segment: c0 and the tile start are even)
-        const int c0 = kHs3Out * bx;
-        const long o0 = (long)j * dimx + c0 - (long)b * kSnTile;  // offset of lane 2's px in the tile
-        const int cend = min(c0 + kHs3Out, dimx);
-        const int lend = 2 + (cend - c0 + 1) / 2;  // own lanes [2, lend)
-#pragma unroll
-        for (int k = 0; k < 6; k++) {
-            A[k] += (double)__uint_as_float(w[k]);
-            T0[k] = ((T0[k] | w[6 + k]) & kSnBad) | sn_sat(T0[k] & ~kSnBad, w[6 + k] & ~kSnBad);
-            T1[k] = ((T1[k] | w[12 + k]) & kSnBad) | sn_sat(T1[k] & ~kSnBad, w[12 + k] & ~kSnBad);
-            const unsigned long long zb =
-                (unsigned long long)w[18 + 2 * k] | ((unsigned long long)w[19 + 2 * k] << 32);
-            if (!zb) continue;
-            for (int l = 2; l < lend;) {  // segment by segment
-                const long o = o0 + 2 * (l - 2);
-                const int s = (int)(o >> 6);
-                const int lnext = min(lend, l + (int)((((long)(s + 1) << 6) - o) + 1) / 2);
-                const unsigned long long m = (lnext >= 64 ? ~0ull : ((1ull << lnext) - 1)) & ~((1ull << l) - 1);
-                if (zb & m) Z[k] |= 1ull << s;
-                l = lnext;
-            }
-        }
-    }
-    auto sat = [](unsigned p, unsigned x) {
-        return ((p | x) & kSnBad) | sn_sat(p & ~kSnBad, x & ~kSnBad);
-    };
-#pragma unroll
-    for (int k = 0; k < 6; k++) {
-        A[k] = wave_reduce(A[k], [](double p, double x) { return p + x; });
-        T0[k] = wave_reduce(T0[k], sat);
-        T1[k] = wave_reduce(T1[k], sat);
-        Z[k] = wave_reduce(Z[k], [](unsigned long long p, unsigned long long x) { return p | x; });
-    }
-    if (lane != 0) return;
-#pragma unroll
-    for (int i = 0; i < K; i++) {
-        const SnWs &ws = J.ws[i];
-#pragma unroll
-        for (int n = 0; n < 2; n++) {
-            const int k = 2 * i + n;
-            unsigned hh = ws.H[2 * (size_t)b + n];
-            const int nc = (hh & kHdrPending) ? 0 : hdr_nc(hh);
-            if (nc > 0) ws.T[(2 * (size_t)b + n) * kSnCand] = T0[k];
-            if (nc > 1) ws.T[(2 * (size_t)b + n) * kSnCand + 1] = T1[k];
-            if (Z[k] == 0ull) hh = kHdrZero;
-            else if (A[k] != A[k]) hh = hdr_pack(0, 0) | kHdrNan;
-            ws.A[2 * (size_t)b + n] = A[k];
-            ws.Z[2 * (size_t)b + n] = Z[k];
-            ws.H[2 * (size_t)b + n] = hh;
-        }
-    }
-}
 }  // namespace
 
 size_t seqnorm_workspace_bytes(int dimx, int dimy) {
@@ -1764,64 +1485,6 @@ void launch_seqnorm_decide(const float *seq, int K, int t0, double npx, int *sto
         throw std::invalid_argument("launch_seqnorm_decide: arguments");
     hipLaunchKernelGGL(seqnorm_decide, dim3(1), dim3(64), 0, st, seq, K, t0, (float)npx, stop,
                        host);
-    OF2D_HIP(hipGetLastError());
-}
-
-bool seqnorm_fusable(int dimx, int dimy) {
-#ifdef OF2D_SN_NOFUSE  // A/B builds: the separate pass everywhere
-    return false;
-#endif
-    return dimx >= 2 && dimy >= 1 && kSnTile % dimx == 0;
-}
-size_t seqnorm_rec_bytes(int dimx, int dimy) {
-    return (size_t)dimy * (size_t)((dimx + kHs3Out - 1) / kHs3Out) * kSnRec * sizeof(unsigned);
-}
-void launch_seqnorm_headers(const SeqnormBatch &B, int dimx, int dimy, int P, hipStream_t st) {
-    const unsigned nt = check_geometry(dimx, dimy, P);
-    if (B.K != 3 || !seqnorm_fusable(dimx, dimy))
-        throw std::invalid_argument("launch_seqnorm_headers: a triple's batch on a fusable grid");
-    hipLaunchKernelGGL(seqnorm_headers<3>, dim3((nt + 255) / 256), dim3(256), 0, st, nt,
-                       jobs_of(B, nt));
-    OF2D_HIP(hipGetLastError());
-}
-namespace {
-int log2_exact(int v) {
-    int r = 0;
-    while ((1 << r) < v) r++;
-    return r;
-}
-}  // namespace
-void launch_hs_jacobi3_fused(const float2 *u_old, float2 *u1, float2 *u2, float2 *u3,
-                             const float2 *dI, const float *It, int P, int dimx, int dimy,
-                             float alphasq, unsigned *status, const unsigned *range_flag,
-                             const float *Ia, const int *stop, int stop_t0,
-                             const SeqnormBatch &B, unsigned *rec, hipStream_t st) {
-    const unsigned nt = check_geometry(dimx, dimy, P);
-    if (P % kHsStrip != 0 || dimx < 2 || !seqnorm_fusable(dimx, dimy) || B.K != 3 || !rec ||
-        !range_flag || !u1 || !u2)
-        throw std::invalid_argument("launch_hs_jacobi3_fused: bad arguments");
-    const SnJobs J = jobs_of(B, nt);
-    SnFuseHook hook;
-    hook.rec = rec;
-    for (int i = 0; i < 3; i++) hook.H[i] = J.ws[i].H;
-    hook.dimx = dimx;
-    hook.gx = (dimx + kHs3Out - 1) / kHs3Out;
-    hook.rlog = log2_exact(kSnTile / dimx);
-    // j-lines per wave for the rounds of resident blocks this build allows
-    const int rows = hs3_rows(dimx, dimy, 256 * OF2D_SN_FUSE_MINB);
-    const int gy = (dimy + kHs3Waves * rows - 1) / (kHs3Waves * rows);
-    const dim3 gl(8 * ((hook.gx * gy + 7) / 8));
-    if (Ia)
-        hipLaunchKernelGGL(jacobi3_fused_kernel<true>, gl, dim3(64 * kHs3Waves), 0, st, u_old, u3,
-                           dI, It, P, dimx, dimy, dimy, alphasq, -1, dimy + 1, status, hook.gx, gy,
-                           rows, range_flag, Ia, u1, u2, stop, stop_t0, hook);
-    else
-        hipLaunchKernelGGL(jacobi3_fused_kernel<false>, gl, dim3(64 * kHs3Waves), 0, st, u_old,
-                           u3, dI, It, P, dimx, dimy, dimy, alphasq, -1, dimy + 1, status, hook.gx,
-                           gy, rows, range_flag, Ia, u1, u2, stop, stop_t0, hook);
-    OF2D_HIP(hipGetLastError());
-    hipLaunchKernelGGL(seqnorm_merge<3>, dim3((nt + 3) / 4), dim3(256), 0, st, nt, dimx, dimy,
-                       hook.gx, hook.rlog, (const unsigned *)rec, J);
     OF2D_HIP(hipGetLastError());
 }
 
