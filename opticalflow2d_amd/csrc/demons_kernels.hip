@@ -148,6 +148,43 @@ __device__ __forceinline__ float2 demons_corr(float gx, float gy, float it, floa
     return make_float2(((gx * it) / den) * -1.0f, ((gy * it) / den) * -1.0f);
 }
 
+// The same with the two components' divisions by the one denominator as the
+// unscaled exact sequence with a shared refined reciprocal (hs_jacobi_impl.h
+// div2_unscaled: bit-identical to the compiler's IEEE quotient while den is in
+// [2^-40, 2^40) and each numerator in [2^-80, 2^50)), taken when every lane
+// of the wave is in that range (one ballot), the IEEE divisions otherwise.
+// An A/B build knob (OF2D_DEMONS_DIVU, round 5).
+#ifndef OF2D_DEMONS_DIVU
+#define OF2D_DEMONS_DIVU 0
+#endif
+__device__ __forceinline__ float dm_rcp_refined(float b) {
+    const float r0 = __builtin_amdgcn_rcpf(b);
+    return __builtin_fmaf(__builtin_fmaf(-b, r0, 1.0f), r0, r0);
+}
+template <bool SXP = false>
+__device__ __forceinline__ float2 demons_corr_u(float gx, float gy, float it, float sigma_isq,
+                                                float sxq, bool &zero) {
+    const float t = (it * it) * sigma_isq;
+    const float den = (gx * gx + gy * gy) + (SXP ? t * sxq : t / sxq);
+    zero |= den == 0.0f;
+    const float ax = gx * it, ay = gy * it;
+    const float mn = fminf(fabsf(ax), fabsf(ay)), mx = fmaxf(fabsf(ax), fabsf(ay));
+    const bool ok = den >= 0x1p-40f && den < 0x1p40f && mn >= 0x1p-80f && mx < 0x1p50f;
+    if (__builtin_amdgcn_ballot_w64(!ok) == 0) {
+        typedef float v2f_ __attribute__((ext_vector_type(2)));
+        const float r = dm_rcp_refined(den);
+        const v2f_ a = {ax, ay}, nb = {-den, -den}, rr = {r, r};
+        v2f_ q = a * rr;
+        v2f_ e = __builtin_elementwise_fma(nb, q, a);
+        q = __builtin_elementwise_fma(e, rr, q);
+        e = __builtin_elementwise_fma(nb, q, a);
+        q = __builtin_elementwise_fma(e, rr, q);
+        return make_float2(__builtin_amdgcn_div_fixupf(q.x, den, ax) * -1.0f,
+                           __builtin_amdgcn_div_fixupf(q.y, den, ay) * -1.0f);
+    }
+    return make_float2((ax / den) * -1.0f, (ay / den) * -1.0f);
+}
+
 // x tile of a launch over a subset of the tile columns: block columns
 // [0, ntl) are tiles [0, ntl), the others the last tiles of a gxt-tile row
 __device__ __forceinline__ int tile_x(int ntl, int gxt) {
@@ -641,6 +678,9 @@ __global__ __launch_bounds__(256) OF2D_DEMONS_FUSED_ATTR void demons_fused_kerne
                     const float gx = (w[1] - w[-1]) / 2.0f, gy = (w[WW] - w[-WW]) / 2.0f;
                     ct[r * CW + cc] = OF2D_DEMONS_ABL == 2
                                           ? make_float2(gx, gy + (w[0] - iref[q]))
+                                      : OF2D_DEMONS_DIVU
+                                          ? demons_corr_u<FAST>(gx, gy, w[0] - iref[q], sigma_isq,
+                                                                sxq, zero)
                                           : demons_corr<FAST>(gx, gy, w[0] - iref[q], sigma_isq,
                                                               sxq, zero);
                 }

@@ -75,30 +75,30 @@ void launch_hs_jacobi3(const float2 *u_old, float2 *u_new, const float2 *dI, con
                        int ghi, double *partial, double *partial2, double *partial3,
                        unsigned *status, const unsigned *range_flag, hipStream_t st,
                        int band_lo, int band_hi, const float *Ia, float2 *u1, float2 *u2,
-                       const int *stop, int stop_t0) {
+                       const int *stop, int stop_t0, int slots) {
     if (P % kHsStrip != 0 || nrows <= 0 || dimx > P || dimx < 2 || glo > -1 || ghi < nrows + 1)
         throw std::invalid_argument("launch_hs_jacobi3: bad geometry");
     if (!u1 != !u2) throw std::invalid_argument("launch_hs_jacobi3: u1 and u2 go together");
     if (!range_flag) throw std::invalid_argument("launch_hs_jacobi3: no range flag");
-    const int nb = hs3_nbands(dimx, nrows);
+    const int rows = hs3_rows(dimx, nrows, slots);
+    const int nb = (nrows + kHs3Waves * rows - 1) / (kHs3Waves * rows);
     if (band_lo < 0) band_lo = 0;
     if (band_hi < 0) band_hi = nb;
     if (band_lo > band_hi || band_hi > nb) throw std::invalid_argument("launch_hs_jacobi3: bands");
     if (band_lo == band_hi) return;
-    dim3 g = hs3_grid(dimx, nrows);
+    dim3 g((dimx + kHs3Out - 1) / kHs3Out, nb);
     g.y = band_hi - band_lo;
     const dim3 gl(8 * ((g.x * g.y + 7) / 8));
     if (u1)
         hipLaunchKernelGGL(Ia ? kHsJacobi3IM : kHsJacobi3M, gl, dim3(64 * kHs3Waves), 0, st, u_old,
                            u_new, dI, It, P, dimx, nrows, row0, dimy, alphasq, glo, ghi, partial,
-                           partial2, partial3, status, band_lo, (int)g.x, (int)g.y,
-                           hs3_rows(dimx, nrows), range_flag, -1, -1, Ia, u1, u2, stop,
-                           stop_t0);
+                           partial2, partial3, status, band_lo, (int)g.x, (int)g.y, rows,
+                           range_flag, -1, -1, Ia, u1, u2, stop, stop_t0);
     else
         hipLaunchKernelGGL(Ia ? kHsJacobi3I : kHsJacobi3, gl, dim3(64 * kHs3Waves), 0, st, u_old,
                            u_new, dI, It, P, dimx, nrows, row0, dimy, alphasq, glo, ghi, partial,
-                           partial2, partial3, status, band_lo, (int)g.x, (int)g.y,
-                           hs3_rows(dimx, nrows), range_flag, -1, -1, Ia);
+                           partial2, partial3, status, band_lo, (int)g.x, (int)g.y, rows,
+                           range_flag, -1, -1, Ia);
     OF2D_HIP(hipGetLastError());
 }
 

@@ -176,7 +176,9 @@ void launch_hs_jacobi3(const float2 *u_old, float2 *u_new, const float2 *dI, con
                        unsigned *status, const unsigned *range_flag, hipStream_t st,
                        int band_lo = -1, int band_hi = -1, const float *Ia = nullptr,
                        float2 *u1 = nullptr, float2 *u2 = nullptr, const int *stop = nullptr,
-                       int stop_t0 = 0);
+                       int stop_t0 = 0, int slots = 1024);
+// (slots: resident 4-wave blocks the launch may have, for its j-lines per
+// wave, hs3_rows; 1024 = every CU of the device)
 // (u1, u2 non-null: the first two iterates of the owned rows are stored there
 // too, for the reference-exact Logger; +16 B/px; with stop, the launch does
 // nothing when *stop < stop_t0: the loop broke before the triple's first

@@ -125,6 +125,16 @@ float logger_error(double sum_diff, double sum_prev, double npx);
 #define OF2D_SN_WALKERS 3
 #endif
 constexpr int kMaxEst = OF2D_SN_RING + 1 > 16 ? OF2D_SN_RING + 1 : 16;
+// CUs kept from the bandwidth kernels of the exact loop (the triples and the
+// pass run on streams with a CU mask without them), so that its latency chain
+// (check, entries, walks) finds free slots; OF2D_SN_CUMASK_CHAIN 1 also keeps
+// the chain's streams on those CUs only (build knobs for A/B runs; 0 = off)
+#ifndef OF2D_SN_CUMASK
+#define OF2D_SN_CUMASK 0
+#endif
+#ifndef OF2D_SN_CUMASK_CHAIN
+#define OF2D_SN_CUMASK_CHAIN 0
+#endif
 
 struct Level {
     int dx = 0, dy = 0, P = 0;
@@ -228,6 +238,8 @@ class Registration {
                        float *seqh_out = nullptr);
     void print_sn_debug(const Level &L, const int *dbg, int k0, int lo, int hi);
     hipStream_t sn_st_ = nullptr, fx_st_ = nullptr, wk_st_[OF2D_SN_WALKERS] = {};
+    int ncu_ = 256;        // compute units of the device
+    int tri_slots_ = 1024;  // resident triple blocks st_ may have (CU mask)
     static constexpr int kExactEv = 64;  // event ring per group (two blocks in flight)
     // workspace sets: group g's walk is read (its profile) by group g + kSeqSets
     static constexpr int kSeqSets = OF2D_SN_SETS;

@@ -20,6 +20,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <hip/hip_ext.h>
 
 #include "of2d_host.h"
 #include "of2d_solvers.h"
@@ -211,16 +212,35 @@ void Registration::ensure_device() {
     if (device_ >= 0) OF2D_HIP(hipSetDevice(device_));
     OF2D_HIP(hipGetDevice(&home_));
     OF2D_HIP(hipGetDeviceCount(&ndev_));
-    OF2D_HIP(hipStreamCreateWithFlags(&st_, hipStreamNonBlocking));
-    OF2D_HIP(hipStreamCreateWithFlags(&sn_st_, hipStreamNonBlocking));
-    // the fix and the walks at high priority: they are the latency chain that
-    // gates the steps (ring) and passes (workspaces) a few groups later, and
-    // wait for CUs behind the bandwidth kernels otherwise (4096^2 procedural
-    // convergence 148 -> 128 us per iteration, profiles/r04m_exact_pipeline_ab.log)
+    OF2D_HIP(hipDeviceGetAttribute(&ncu_, hipDeviceAttributeMultiprocessorCount, home_));
     int prio_lo = 0, pr = 0;
     OF2D_HIP(hipDeviceGetStreamPriorityRange(&prio_lo, &pr));
-    OF2D_HIP(hipStreamCreateWithPriority(&fx_st_, hipStreamNonBlocking, pr));
-    for (hipStream_t &w : wk_st_) OF2D_HIP(hipStreamCreateWithPriority(&w, hipStreamNonBlocking, pr));
+    if (OF2D_SN_CUMASK > 0 && OF2D_SN_CUMASK < ncu_) {
+        std::vector<uint32_t> big((ncu_ + 31) / 32, 0u), small(big.size(), 0u);
+        for (int c = 0; c < ncu_; c++) (c < OF2D_SN_CUMASK ? small : big)[c / 32] |= 1u << (c % 32);
+        OF2D_HIP(hipExtStreamCreateWithCUMask(&st_, (uint32_t)big.size(), big.data()));
+        OF2D_HIP(hipExtStreamCreateWithCUMask(&sn_st_, (uint32_t)big.size(), big.data()));
+        tri_slots_ = 4 * (ncu_ - OF2D_SN_CUMASK);
+        if (OF2D_SN_CUMASK_CHAIN) {
+            OF2D_HIP(hipExtStreamCreateWithCUMask(&fx_st_, (uint32_t)small.size(), small.data()));
+            for (hipStream_t &w : wk_st_)
+                OF2D_HIP(hipExtStreamCreateWithCUMask(&w, (uint32_t)small.size(), small.data()));
+        } else {
+            OF2D_HIP(hipStreamCreateWithPriority(&fx_st_, hipStreamNonBlocking, pr));
+            for (hipStream_t &w : wk_st_)
+                OF2D_HIP(hipStreamCreateWithPriority(&w, hipStreamNonBlocking, pr));
+        }
+    } else {
+        OF2D_HIP(hipStreamCreateWithFlags(&st_, hipStreamNonBlocking));
+        OF2D_HIP(hipStreamCreateWithFlags(&sn_st_, hipStreamNonBlocking));
+        // the fix and the walks at high priority: they are the latency chain that
+        // gates the steps (ring) and passes (workspaces) a few groups later, and
+        // wait for CUs behind the bandwidth kernels otherwise (4096^2 procedural
+        // convergence 148 -> 128 us per iteration, profiles/r04m_exact_pipeline_ab.log)
+        OF2D_HIP(hipStreamCreateWithPriority(&fx_st_, hipStreamNonBlocking, pr));
+        for (hipStream_t &w : wk_st_)
+            OF2D_HIP(hipStreamCreateWithPriority(&w, hipStreamNonBlocking, pr));
+    }
     for (int k = 0; k < kExactEv; k++) {
         OF2D_HIP(hipEventCreateWithFlags(&ev_step_[k], hipEventDisableTiming));
         OF2D_HIP(hipEventCreateWithFlags(&ev_fix_[k], hipEventDisableTiming));
@@ -787,7 +807,8 @@ int Registration::loop_hs(Level &L, int niter, float alpha, int &final_buf) {
                               (gi_ < 0 ? hs3_gradients_from_image(L.dx, L.dy) : gi_ != 0)
                                   ? L.Iaux.p
                                   : nullptr,
-                              d1, d2, reinterpret_cast<const int *>(d_status_ + kStopWord), t0);
+                              d1, d2, reinterpret_cast<const int *>(d_status_ + kStopWord), t0,
+                              tri_slots_);
         })
               : StepFn3M());
 }
