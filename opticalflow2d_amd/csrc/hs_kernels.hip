@@ -210,6 +210,26 @@ void launch_sum_ranks(const double *const *src, int n, size_t count, double *out
     OF2D_HIP(hipGetLastError());
 }
 
+// halo j-lines between slabs of one device (slab.cpp local_exchange): 16-B
+// words, a few blocks, so that the copy finds CU slots beside the triples at
+// once (the runtime's copy kernel is 256 blocks: 24 us per 98 KB copy beside
+// 8 ranks' triples, profiles/r05f_ranks_attribution.txt)
+__global__ __launch_bounds__(256) void copy_lines_kernel(const float2 *__restrict__ src,
+                                                         float2 *__restrict__ dst, long n) {
+    for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256)
+        dst[i] = src[i];
+}
+void launch_copy_lines(void *dst, const void *src, size_t bytes, hipStream_t st) {
+    if (bytes % 8 != 0 || (reinterpret_cast<uintptr_t>(dst) | reinterpret_cast<uintptr_t>(src)) % 8)
+        throw std::invalid_argument("launch_copy_lines: 8-B aligned whole float2s");
+    const long n = (long)(bytes / 8);
+    if (n == 0) return;
+    const unsigned blocks = (unsigned)std::min<long>(16, (n + 255) / 256);
+    hipLaunchKernelGGL(copy_lines_kernel, dim3(blocks), dim3(256), 0, st,
+                       static_cast<const float2 *>(src), static_cast<float2 *>(dst), n);
+    OF2D_HIP(hipGetLastError());
+}
+
 void PartialRuns::add(int t, int len, int nblocks) {
     if (!runs.empty() && runs.back().t0 + runs.back().len == t && runs.back().nblocks == nblocks)
         runs.back().len += len;

@@ -214,6 +214,8 @@ inline int hs_partial_blocks(int P, int dimx, int nrows) {
 // out[i] = sum over r < n of src[r][i], added in rank order (the in-process
 // slab group's all-reduce, slab.cpp); n <= kMaxLocalRanks
 constexpr int kMaxLocalRanks = 16;
+// device-to-device copy of whole float2s on one device, by a few blocks
+void launch_copy_lines(void *dst, const void *src, size_t bytes, hipStream_t st);
 void launch_sum_ranks(const double *const *src, int n, size_t count, double *out, hipStream_t st);
 // Row t of `partial` starts at t * stride * 2 doubles (stride = nblocks if < 0).
 void launch_reduce_partials(const double *partial, int nblocks, int C, double *sums,

@@ -125,12 +125,17 @@ float logger_error(double sum_diff, double sum_prev, double npx);
 #define OF2D_SN_WALKERS 3
 #endif
 constexpr int kMaxEst = OF2D_SN_RING + 1 > 16 ? OF2D_SN_RING + 1 : 16;
-// CUs kept from the bandwidth kernels of the exact loop (the triples and the
-// pass run on streams with a CU mask without them), so that its latency chain
-// (check, entries, walks) finds free slots; OF2D_SN_CUMASK_CHAIN 1 also keeps
-// the chain's streams on those CUs only (build knobs for A/B runs; 0 = off)
+// CUs kept from the bandwidth kernels of HS's exact loop (its triples and
+// passes run on streams with a CU mask without them), so that the loop's
+// latency chain (check, entries, walks) finds free slots: 4096^2 procedural
+// 141-142 -> 128-131 us per iteration with 8-32 CUs kept, texture unchanged
+// (profiles/r05e_conv_cumask_ab.log); OF2D_SN_CUMASK_CHAIN 1 also keeps the
+// chain's streams on those CUs only (slower: r05d).  0 = no mask.
 #ifndef OF2D_SN_CUMASK
-#define OF2D_SN_CUMASK 0
+#define OF2D_SN_CUMASK 16
+#endif
+#ifndef OF2D_SN_PASS_SERIAL
+#define OF2D_SN_PASS_SERIAL 0
 #endif
 #ifndef OF2D_SN_CUMASK_CHAIN
 #define OF2D_SN_CUMASK_CHAIN 0
@@ -232,6 +237,8 @@ class Registration {
     // decision, the break also taken on the device (the stop word)
     int run_exact_pipelined(Level &L, int niter, const StepFn &step, int &final_buf,
                             const StepFn3M &step3m);
+    int run_exact_pipelined_on(Level &L, int niter, const StepFn &step, int &final_buf,
+                               const StepFn3M &step3m);
     // a group's norms behind its steps: pass on sn_st_, check and fix on
     // fx_st_, walk (and with B.stop seqnorm_decide) on wk_st_[g mod 3]
     void enqueue_norms(const SeqnormBatch &B, const Level &L, int g, double npx = 0.0,
@@ -239,7 +246,11 @@ class Registration {
     void print_sn_debug(const Level &L, const int *dbg, int k0, int lo, int hi);
     hipStream_t sn_st_ = nullptr, fx_st_ = nullptr, wk_st_[OF2D_SN_WALKERS] = {};
     int ncu_ = 256;        // compute units of the device
-    int tri_slots_ = 1024;  // resident triple blocks st_ may have (CU mask)
+    // HS's exact loop runs its triples on hs_st_ (in place of st_ for the
+    // loop) and its passes on sn_st_, both masked (OF2D_SN_CUMASK; null: no
+    // mask), with tri_slots_ resident triple blocks
+    hipStream_t hs_st_ = nullptr;
+    int tri_slots_ = 1024;
     static constexpr int kExactEv = 64;  // event ring per group (two blocks in flight)
     // workspace sets: group g's walk is read (its profile) by group g + kSeqSets
     static constexpr int kSeqSets = OF2D_SN_SETS;

@@ -171,6 +171,7 @@ Registration::~Registration() {
         if (ev_pass_[k]) (void)hipEventDestroy(ev_pass_[k]);
         if (ev_walk_[k]) (void)hipEventDestroy(ev_walk_[k]);
     }
+    if (hs_st_) (void)hipStreamDestroy(hs_st_);
     if (st_) (void)hipStreamDestroy(st_);
 }
 
@@ -215,10 +216,11 @@ void Registration::ensure_device() {
     OF2D_HIP(hipDeviceGetAttribute(&ncu_, hipDeviceAttributeMultiprocessorCount, home_));
     int prio_lo = 0, pr = 0;
     OF2D_HIP(hipDeviceGetStreamPriorityRange(&prio_lo, &pr));
+    OF2D_HIP(hipStreamCreateWithFlags(&st_, hipStreamNonBlocking));
     if (OF2D_SN_CUMASK > 0 && OF2D_SN_CUMASK < ncu_) {
         std::vector<uint32_t> big((ncu_ + 31) / 32, 0u), small(big.size(), 0u);
         for (int c = 0; c < ncu_; c++) (c < OF2D_SN_CUMASK ? small : big)[c / 32] |= 1u << (c % 32);
-        OF2D_HIP(hipExtStreamCreateWithCUMask(&st_, (uint32_t)big.size(), big.data()));
+        OF2D_HIP(hipExtStreamCreateWithCUMask(&hs_st_, (uint32_t)big.size(), big.data()));
         OF2D_HIP(hipExtStreamCreateWithCUMask(&sn_st_, (uint32_t)big.size(), big.data()));
         tri_slots_ = 4 * (ncu_ - OF2D_SN_CUMASK);
         if (OF2D_SN_CUMASK_CHAIN) {
@@ -231,7 +233,6 @@ void Registration::ensure_device() {
                 OF2D_HIP(hipStreamCreateWithPriority(&w, hipStreamNonBlocking, pr));
         }
     } else {
-        OF2D_HIP(hipStreamCreateWithFlags(&st_, hipStreamNonBlocking));
         OF2D_HIP(hipStreamCreateWithFlags(&sn_st_, hipStreamNonBlocking));
         // the fix and the walks at high priority: they are the latency chain that
         // gates the steps (ring) and passes (workspaces) a few groups later, and
@@ -492,10 +493,13 @@ int Registration::run_chunked_exact(Level &L, int niter, int nb, const StepFn &s
 void Registration::enqueue_norms(const SeqnormBatch &B, const Level &L, int g, double npx,
                                  float *seqh_out) {
     auto ev = [](hipEvent_t *e, int q) { return e[q % kExactEv]; };
-    OF2D_HIP(hipStreamWaitEvent(sn_st_, ev(ev_step_, g), 0));
-    if (g >= kSeqSets) OF2D_HIP(hipStreamWaitEvent(sn_st_, ev(ev_walk_, g - kSeqSets), 0));
-    launch_seqnorm_pass(B, L.dx, L.dy, L.P, sn_st_);
-    OF2D_HIP(hipEventRecord(ev(ev_pass_, g), sn_st_));
+    // OF2D_SN_PASS_SERIAL (A/B knob): the pass right behind the triple on
+    // its stream instead of beside the next triples on sn_st_
+    hipStream_t ps = OF2D_SN_PASS_SERIAL ? st_ : sn_st_;
+    OF2D_HIP(hipStreamWaitEvent(ps, ev(ev_step_, g), 0));
+    if (g >= kSeqSets) OF2D_HIP(hipStreamWaitEvent(ps, ev(ev_walk_, g - kSeqSets), 0));
+    launch_seqnorm_pass(B, L.dx, L.dy, L.P, ps);
+    OF2D_HIP(hipEventRecord(ev(ev_pass_, g), ps));
     OF2D_HIP(hipStreamWaitEvent(fx_st_, ev(ev_pass_, g), 0));
     launch_seqnorm_refine(B, L.dx, L.dy, L.P, fx_st_);
     OF2D_HIP(hipEventRecord(ev(ev_fix_, g), fx_st_));
@@ -537,6 +541,26 @@ void Registration::print_sn_debug(const Level &L, const int *dbg, int k0, int lo
 // not read the stop word) is enqueued after every earlier block is decided.
 int Registration::run_exact_pipelined(Level &L, int niter, const StepFn &step, int &final_buf,
                                       const StepFn3M &step3m) {
+    if (hs_st_) {
+        // the loop on the masked stream: it runs after st_'s work so far, and
+        // st_ runs after the loop (every launch below goes to st_)
+        OF2D_HIP(hipEventRecord(ev_fork_, st_));
+        OF2D_HIP(hipStreamWaitEvent(hs_st_, ev_fork_, 0));
+        std::swap(st_, hs_st_);
+        struct Back {
+            Registration *r;
+            ~Back() {
+                std::swap(r->st_, r->hs_st_);
+                (void)hipEventRecord(r->ev_join_, r->hs_st_);
+                (void)hipStreamWaitEvent(r->st_, r->ev_join_, 0);
+            }
+        } back{this};
+        return run_exact_pipelined_on(L, niter, step, final_buf, step3m);
+    }
+    return run_exact_pipelined_on(L, niter, step, final_buf, step3m);
+}
+int Registration::run_exact_pipelined_on(Level &L, int niter, const StepFn &step, int &final_buf,
+                                         const StepFn3M &step3m) {
     const double npx = (double)L.dx * L.dy;
     last_err_.clear();
     constexpr int R = kRing;

@@ -223,12 +223,14 @@ void local_exchange(of2d_slab *s, float2 *u, int lines, size_t cnt, hipStream_t 
         const of2d_slab *o = g->slabs[q];
         const float2 *src = static_cast<const float2 *>(g->xptr[(size_t)q * kXr + k]);
         OF2D_HIP(hipStreamWaitEvent(st, o->ev_xr[k], 0));
-        if (q < s->rank)  // its last lines into the ghost lines above row 0
-            OF2D_HIP(hipMemcpyAsync(u - lines * P, src + (long)(o->nrows - lines) * P, bytes,
-                                    hipMemcpyDeviceToDevice, st));
-        else  // its first lines below the last row
-            OF2D_HIP(hipMemcpyAsync(u + (long)s->nrows * P, src, bytes, hipMemcpyDeviceToDevice,
-                                    st));
+        // its last lines into the ghost lines above row 0, or its first lines
+        // below the last row
+        float2 *dst = q < s->rank ? u - lines * P : u + (long)s->nrows * P;
+        const float2 *from = q < s->rank ? src + (long)(o->nrows - lines) * P : src;
+        if (o->device == s->device)  // a few blocks, beside the other ranks' triples
+            of2d::launch_copy_lines(dst, from, bytes, st);
+        else
+            OF2D_HIP(hipMemcpyAsync(dst, from, bytes, hipMemcpyDeviceToDevice, st));
     }
     OF2D_HIP(hipEventRecord(s->ev_xd[k], st));
     g->xr_done[s->rank].store(x + 1, std::memory_order_release);
@@ -316,6 +318,7 @@ void allreduce_sums(of2d_slab *s, double *buf, size_t count, hipStream_t st) {
 // stream took 149 us).
 struct SlabGeometry {
     bool split = false;
+    int slots = 1024;  // block slots of an unsplit triple (triple_slots)
     int E = 16, re = 4;  // edge j-lines, j-lines per wave in an edge launch
     int ri = 0, bi = 0;  // interior j-lines per wave and block rows
     int n3 = 0;          // block partials a triple writes
@@ -359,10 +362,25 @@ bool remote_neighbour(const of2d_slab *s) {
 bool can_split(const of2d_slab *s) {
     return s->nranks > 1 && s->nrows >= 3 * SlabGeometry().E && s->dimx >= 2;
 }
-SlabGeometry slab_geometry_as(const of2d_slab *s, bool split) {
+// Block slots a whole-slab triple may take: the device's 1024 (4 per CU), or,
+// with k > 1 slabs of an in-process group on this device, 1024 / min(k, 4) —
+// their triples run side by side (up to four at once, one per hardware
+// queue), so each takes longer bands in fewer blocks instead of a whole
+// device's worth of short ones (512-row slabs of 4096: 245 blocks of 19-line
+// bands rather than 910 of 5-line bands, whose halo rows and prologue
+// double the work per pixel; profiles/r05f_ranks_attribution.txt)
+int triple_slots(const of2d_slab *s) {
+    if (!s->grp) return 1024;
+    int k = 0;
+    for (const of2d_slab *o : s->grp->slabs)
+        if (o && o->device == s->device) k++;
+    return k > 1 ? 1024 / std::min(k, 4) : 1024;
+}
+SlabGeometry slab_geometry_as(const of2d_slab *s, bool split, int slots = 1024) {
     SlabGeometry g;
     const int gx = (s->dimx + of2d::kHs3Out - 1) / of2d::kHs3Out;
     g.split = split && can_split(s);
+    g.slots = slots;
     if (g.split) {
         const int ni = s->nrows - 2 * g.E;
         constexpr int kCommBlocks = 8;
@@ -370,18 +388,23 @@ SlabGeometry slab_geometry_as(const of2d_slab *s, bool split) {
         g.bi = (ni + of2d::kHs3Waves * g.ri - 1) / (of2d::kHs3Waves * g.ri);
         g.n3 = gx * (g.bi + 2);
     } else {
-        g.n3 = of2d::hs3_nblocks(s->dimx, s->nrows);
+        const int r = of2d::hs3_rows(s->dimx, s->nrows, slots);
+        g.n3 = gx * ((s->nrows + of2d::kHs3Waves * r - 1) / (of2d::kHs3Waves * r));
     }
     g.nb = std::max(of2d::hs_partial_blocks(s->P, s->dimx, s->nrows), g.n3);
     return g;
 }
 SlabGeometry slab_geometry(const of2d_slab *s) {
-    return slab_geometry_as(s, s->split > 0 || (s->split < 0 && remote_neighbour(s)));
+    return slab_geometry_as(s, s->split > 0 || (s->split < 0 && remote_neighbour(s)),
+                            triple_slots(s));
 }
-// partial-row length for either geometry: the allocation at create, before the
-// group's other slabs (whose devices decide the split) or the option are known
+// partial-row length for every geometry: the allocation at create, before the
+// group's other slabs (whose devices decide the split and the slots) or the
+// option are known
 int partial_blocks_cap(const of2d_slab *s) {
-    return std::max(slab_geometry_as(s, false).nb, slab_geometry_as(s, true).nb);
+    int nb = slab_geometry_as(s, true).nb;
+    for (int slots : {1024, 512, 341, 256}) nb = std::max(nb, slab_geometry_as(s, false, slots).nb);
+    return nb;
 }
 // convergence-on runs take the reference's float running sums (run_exact)
 bool exact_logger(const of2d_slab *s) {
@@ -526,7 +549,8 @@ int run_exact(of2d_slab *s, int niter) {
                                         s->dimx, s->nrows, s->rb, s->dimy, alphasq, -3,
                                         s->nrows + 3, part(t), part(t + 1), part(t + 2),
                                         s->d_status, range_flag, s->st, -1, -1, ia,
-                                        exbuf(s, ring(a, t)).p, exbuf(s, ring(a, t + 1)).p);
+                                        exbuf(s, ring(a, t)).p, exbuf(s, ring(a, t + 1)).p,
+                                        nullptr, 0, slab_geometry(s).slots);
             } else {
                 for (int m = t; m < t + k; m++) single(src_of(a, m), ring(a, m), part(m));
             }
@@ -916,7 +940,8 @@ int of2d_slab_run(of2d_slab *s, int niter, int fixed_iters, int *iters_done) {
             if (K == 3)
                 of2d::launch_hs_jacobi3(uin, s->u[out].p, s->dI.p, s->It.p, s->P, s->dimx,
                                         s->nrows, s->rb, s->dimy, alphasq, -3, s->nrows + 3, p1,
-                                        p2, p3, s->d_status, range_flag, s->st, -1, -1, ia);
+                                        p2, p3, s->d_status, range_flag, s->st, -1, -1, ia,
+                                        nullptr, nullptr, nullptr, 0, G.slots);
             else
                 of2d::launch_hs_jacobi2(uin, s->u[out].p, s->dI.p, s->It.p, s->P, s->dimx,
                                         s->nrows, s->rb, s->dimy, alphasq, -3, s->nrows + 3, p1,
@@ -1118,7 +1143,8 @@ int of2d_slab_time_kernel(of2d_slab *s, int nlaunch, double *avg_us) {
             of2d::launch_hs_jacobi3(s->u[in].p, s->u[out].p, s->dI.p, s->It.p, s->P, s->dimx,
                                     s->nrows, s->rb, s->dimy, alphasq, -3, s->nrows + 3, p1, p2,
                                     p3, s->d_status, s->d_status + of2d::kRangeFlagWord, s->st,
-                                    -1, -1, use_gi(s) ? s->Imov.p : nullptr);
+                                    -1, -1, use_gi(s) ? s->Imov.p : nullptr, nullptr, nullptr,
+                                    nullptr, 0, slab_geometry(s).slots);
         };
         go();
         OF2D_HIP(hipEventRecord(s->ev0, s->st));

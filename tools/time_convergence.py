@@ -14,10 +14,16 @@ from opticalflow2d_amd import synthetic as S  # noqa: E402
 set_print_sink(lambda s: None)
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
 reps = int(sys.argv[2]) if len(sys.argv) > 2 else 3
-cases = {"texture": S.texture_pair(n), "procedural": S.procedural_pair(n, 0, n)}
+only = os.environ.get("OF2D_CONV_CASE")  # one of the pairs (traces)
+cases = {k: g() for k, g in (("texture", lambda: S.texture_pair(n)),
+                             ("procedural", lambda: S.procedural_pair(n, 0, n)))
+         if not only or k == only}
 for name, (ref, mov) in cases.items():
     for fp64 in ((0,) if os.environ.get("OF2D_CONV_ONLY") else (0, 1)):
-        with ImageRegistration((n, n), [1000], 0, 0, [0.1], logger_fp64=fp64) as r:
+        extra = {}
+        if os.environ.get("OF2D_CONV_CHUNK"):  # iterations per host decision block
+            extra["chunk"] = int(os.environ["OF2D_CONV_CHUNK"])
+        with ImageRegistration((n, n), [1000], 0, 0, [0.1], logger_fp64=fp64, **extra) as r:
             r.set_images(ref, mov)
             r.estimate()  # warm-up
             ts = []
