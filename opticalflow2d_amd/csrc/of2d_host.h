@@ -134,8 +134,23 @@ constexpr int kMaxEst = OF2D_SN_RING + 1 > 16 ? OF2D_SN_RING + 1 : 16;
 #ifndef OF2D_SN_CUMASK
 #define OF2D_SN_CUMASK 16
 #endif
+// iterations per host decision block of HS's exact loop (the "chunk" option
+// overrides it): the host enqueues one block ahead of its decision, so a
+// break leaves at most two blocks of no-op launches behind it (each group's
+// seven kernels chained by events: ~90 us a group at 4096^2).  12 instead of
+// 33: texture pair 162-165 -> 149 us per iteration, procedural 126-127 ->
+// 123-125 (profiles/r05h_chunk_ab.log); 9: 140-142 / 120-121 against 12's
+// 143-146 / 122-124, 6: 143-145 / 123 (profiles/r05i_blk_ab.log)
+#ifndef OF2D_SN_BLOCK
+#define OF2D_SN_BLOCK 9
+#endif
 #ifndef OF2D_SN_PASS_SERIAL
 #define OF2D_SN_PASS_SERIAL 0
+#endif
+// CUs of the exact loop's mask given to the passes alone (the triples get the
+// rest): 0 = passes and triples share the masked CUs (A/B knob)
+#ifndef OF2D_SN_PASS_CUS
+#define OF2D_SN_PASS_CUS 0
 #endif
 #ifndef OF2D_SN_CUMASK_CHAIN
 #define OF2D_SN_CUMASK_CHAIN 0
@@ -266,6 +281,7 @@ class Registration {
     DevArray<float> d_seq_;                    // per-iteration exact sums of a chunk
     int seq_dx_[kSeqWs] = {}, seq_dy_[kSeqWs] = {};  // grid of each workspace's last call
     int chunk_ = 33;  // eleven fused triples per chunk
+    bool chunk_set_ = false;  // the option was given (HS's exact loop then uses it too)
     int gi_ = -1;     // triple kernel: dI from Iaux (1), from dI (0), by size (-1)
     int split_ = -1;  // ranks' triples: interior / edge split (slab option "split")
     int device_ = -1;  // option "device" (-1: the current device at first use)

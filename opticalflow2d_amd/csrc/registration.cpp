@@ -193,6 +193,7 @@ void Registration::set_option(const std::string &key, double v) {
     else if (key == "chunk") {
         if (ready_) throw std::invalid_argument("option 'chunk' must be set before first use");
         chunk_ = std::max(1, (int)v);
+        chunk_set_ = true;
     }
     else if (key == "hs_gradients_from_image")
         gi_ = v < 0 ? -1 : (v != 0 ? 1 : 0);
@@ -218,11 +219,18 @@ void Registration::ensure_device() {
     OF2D_HIP(hipDeviceGetStreamPriorityRange(&prio_lo, &pr));
     OF2D_HIP(hipStreamCreateWithFlags(&st_, hipStreamNonBlocking));
     if (OF2D_SN_CUMASK > 0 && OF2D_SN_CUMASK < ncu_) {
-        std::vector<uint32_t> big((ncu_ + 31) / 32, 0u), small(big.size(), 0u);
-        for (int c = 0; c < ncu_; c++) (c < OF2D_SN_CUMASK ? small : big)[c / 32] |= 1u << (c % 32);
+        std::vector<uint32_t> big((ncu_ + 31) / 32, 0u), small(big.size(), 0u), pass(big.size(), 0u);
+        const int pc = OF2D_SN_PASS_CUS > 0 && OF2D_SN_CUMASK + OF2D_SN_PASS_CUS < ncu_
+                           ? OF2D_SN_PASS_CUS : 0;
+        for (int c = 0; c < ncu_; c++) {
+            if (c < OF2D_SN_CUMASK) small[c / 32] |= 1u << (c % 32);
+            else if (c < OF2D_SN_CUMASK + pc) pass[c / 32] |= 1u << (c % 32);
+            else big[c / 32] |= 1u << (c % 32);
+        }
         OF2D_HIP(hipExtStreamCreateWithCUMask(&hs_st_, (uint32_t)big.size(), big.data()));
-        OF2D_HIP(hipExtStreamCreateWithCUMask(&sn_st_, (uint32_t)big.size(), big.data()));
-        tri_slots_ = 4 * (ncu_ - OF2D_SN_CUMASK);
+        OF2D_HIP(hipExtStreamCreateWithCUMask(&sn_st_, (uint32_t)big.size(),
+                                              pc ? pass.data() : big.data()));
+        tri_slots_ = 4 * (ncu_ - OF2D_SN_CUMASK - pc);
         if (OF2D_SN_CUMASK_CHAIN) {
             OF2D_HIP(hipExtStreamCreateWithCUMask(&fx_st_, (uint32_t)small.size(), small.data()));
             for (hipStream_t &w : wk_st_)
@@ -574,7 +582,8 @@ int Registration::run_exact_pipelined_on(Level &L, int niter, const StepFn &step
     constexpr int kNoStop = 0x7f7f7f7f;
     // a block: whole triples, few enough groups that no event of a block being
     // read is recorded again before it is (two blocks in flight)
-    const int blk = std::min(3 * ((chunk_ + 2) / 3), 3 * (kExactEv / 2 - 4));
+    const int cb = chunk_set_ ? chunk_ : OF2D_SN_BLOCK;
+    const int blk = std::min(3 * ((cb + 2) / 3), 3 * (kExactEv / 2 - 4));
     const int ring2 = 2 * blk;  // the sums' ring: two blocks of iterations
     hs_.ensure(std::max(chunk_, 64));
     constexpr bool sn_debug = OF2D_SN_DEBUG != 0;
