@@ -288,6 +288,9 @@ struct SeqnormBatch {
     // iteration)
     const int *stop = nullptr;
     int t0 = 0;
+    // the pass (launch_seqnorm_pass) over tiles [tile_lo, tile_hi) only
+    // (tile_hi 0: every tile); the launch with tile_lo 0 resets the check's list
+    unsigned tile_lo = 0, tile_hi = 0;
 };
 // the Logger errors of a walked batch (pair i's sums at seq[2i], seq[2i + 1]),
 // as logger_error does on the host: the first iteration t0 + i > 1 whose

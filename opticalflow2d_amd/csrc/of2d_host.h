@@ -144,6 +144,13 @@ constexpr int kMaxEst = OF2D_SN_RING + 1 > 16 ? OF2D_SN_RING + 1 : 16;
 #ifndef OF2D_SN_BLOCK
 #define OF2D_SN_BLOCK 9
 #endif
+// HS's exact loop: each triple and its batch's pass in OF2D_SN_PARTS row parts
+// (the triple's bands split evenly), part q's pass on sn_st_ right behind part
+// q's triple on st_, so that it reads iterates just written (A/B knob; 1 =
+// whole-grid launches)
+#ifndef OF2D_SN_PARTS
+#define OF2D_SN_PARTS 1
+#endif
 #ifndef OF2D_SN_PASS_SERIAL
 #define OF2D_SN_PASS_SERIAL 0
 #endif
@@ -200,8 +207,9 @@ class Registration {
                                        double *partial2, double *partial3)>;
     // three iterations in one pass, every iterate stored (d1, d2, d3)
     // (t0: the triple's first iteration, for the stop word of run_exact_pipelined)
-    using StepFn3M =
-        std::function<void(const float2 *src, float2 *d1, float2 *d2, float2 *d3, int t0)>;
+    // (band_lo / band_hi: the triple's row bands this launch covers, -1 all)
+    using StepFn3M = std::function<void(const float2 *src, float2 *d1, float2 *d2, float2 *d3,
+                                        int t0, int band_lo, int band_hi)>;
 
    private:
     // nblk[k]: block partials written by step (k = 0), step2 (1), step3 (2)
@@ -256,8 +264,9 @@ class Registration {
                                const StepFn3M &step3m);
     // a group's norms behind its steps: pass on sn_st_, check and fix on
     // fx_st_, walk (and with B.stop seqnorm_decide) on wk_st_[g mod 3]
+    // (passed: the batch's pass is already enqueued and ev_pass_[g] recorded)
     void enqueue_norms(const SeqnormBatch &B, const Level &L, int g, double npx = 0.0,
-                       float *seqh_out = nullptr);
+                       float *seqh_out = nullptr, bool passed = false);
     void print_sn_debug(const Level &L, const int *dbg, int k0, int lo, int hi);
     hipStream_t sn_st_ = nullptr, fx_st_ = nullptr, wk_st_[OF2D_SN_WALKERS] = {};
     int ncu_ = 256;        // compute units of the device
@@ -265,6 +274,7 @@ class Registration {
     // loop) and its passes on sn_st_, both masked (OF2D_SN_CUMASK; null: no
     // mask), with tri_slots_ resident triple blocks
     hipStream_t hs_st_ = nullptr;
+    hipEvent_t ev_part_ = nullptr;  // a part's triple done (OF2D_SN_PARTS)
     int tri_slots_ = 1024;
     static constexpr int kExactEv = 64;  // event ring per group (two blocks in flight)
     // workspace sets: group g's walk is read (its profile) by group g + kSeqSets

@@ -160,6 +160,7 @@ Registration::~Registration() {
     if (d_scalar_) (void)hipFree(d_scalar_);
     lv_.clear();
     if (ev_fork_) (void)hipEventDestroy(ev_fork_);
+    if (ev_part_) (void)hipEventDestroy(ev_part_);
     if (ev_join_) (void)hipEventDestroy(ev_join_);
     if (sn_st_) (void)hipStreamDestroy(sn_st_);
     if (fx_st_) (void)hipStreamDestroy(fx_st_);
@@ -257,6 +258,7 @@ void Registration::ensure_device() {
         OF2D_HIP(hipEventCreateWithFlags(&ev_walk_[k], hipEventDisableTiming));
     }
     OF2D_HIP(hipEventCreateWithFlags(&ev_fork_, hipEventDisableTiming));
+    OF2D_HIP(hipEventCreateWithFlags(&ev_part_, hipEventDisableTiming));
     OF2D_HIP(hipEventCreateWithFlags(&ev_join_, hipEventDisableTiming));
     lv_.resize(nscales_ + 1);
     size_t maxnb = 1;
@@ -499,15 +501,17 @@ int Registration::run_chunked_exact(Level &L, int niter, int nb, const StepFn &s
 // and fix on fx_st_, the walk on wk_st_[g mod 3]; with B.stop, seqnorm_decide
 // after the walk (the sums' copy to seqh_out).  Records ev_walk_[g].
 void Registration::enqueue_norms(const SeqnormBatch &B, const Level &L, int g, double npx,
-                                 float *seqh_out) {
+                                 float *seqh_out, bool passed) {
     auto ev = [](hipEvent_t *e, int q) { return e[q % kExactEv]; };
-    // OF2D_SN_PASS_SERIAL (A/B knob): the pass right behind the triple on
-    // its stream instead of beside the next triples on sn_st_
-    hipStream_t ps = OF2D_SN_PASS_SERIAL ? st_ : sn_st_;
-    OF2D_HIP(hipStreamWaitEvent(ps, ev(ev_step_, g), 0));
-    if (g >= kSeqSets) OF2D_HIP(hipStreamWaitEvent(ps, ev(ev_walk_, g - kSeqSets), 0));
-    launch_seqnorm_pass(B, L.dx, L.dy, L.P, ps);
-    OF2D_HIP(hipEventRecord(ev(ev_pass_, g), ps));
+    if (!passed) {
+        // OF2D_SN_PASS_SERIAL (A/B knob): the pass right behind the triple on
+        // its stream instead of beside the next triples on sn_st_
+        hipStream_t ps = OF2D_SN_PASS_SERIAL ? st_ : sn_st_;
+        OF2D_HIP(hipStreamWaitEvent(ps, ev(ev_step_, g), 0));
+        if (g >= kSeqSets) OF2D_HIP(hipStreamWaitEvent(ps, ev(ev_walk_, g - kSeqSets), 0));
+        launch_seqnorm_pass(B, L.dx, L.dy, L.P, ps);
+        OF2D_HIP(hipEventRecord(ev(ev_pass_, g), ps));
+    }
     OF2D_HIP(hipStreamWaitEvent(fx_st_, ev(ev_pass_, g), 0));
     launch_seqnorm_refine(B, L.dx, L.dy, L.P, fx_st_);
     OF2D_HIP(hipEventRecord(ev(ev_fix_, g), fx_st_));
@@ -593,6 +597,9 @@ int Registration::run_exact_pipelined_on(Level &L, int niter, const StepFn &step
     bool walked[kSeqWs] = {};  // a new loop: each workspace starts from a fresh state
     std::vector<int> grp_of((size_t)std::max(niter, 1));
     int g = 0;
+    // the triple's row bands (launch_hs_jacobi3's geometry at tri_slots_)
+    const int band_rows = kHs3Waves * hs3_rows(L.dx, L.dy, tri_slots_);
+    const int nbands = (L.dy + band_rows - 1) / band_rows;
     // iterations [t, t + k) as group g (t a multiple of three)
     auto enqueue_group = [&](int t, int k) {
         for (int m = t; m < t + k; m++) grp_of[m] = g;
@@ -603,12 +610,12 @@ int Registration::run_exact_pipelined_on(Level &L, int niter, const StepFn &step
                 last = grp_of[q];
                 OF2D_HIP(hipStreamWaitEvent(st_, ev(ev_walk_, last), 0));
             }
-        if (k == 3)
+        const bool parts = k == 3 && OF2D_SN_PARTS > 1 && nbands >= OF2D_SN_PARTS;
+        if (k == 3 && !parts)
             step3m(L.est[slot(t)].p, L.est[slot(t + 1)].p, L.est[slot(t + 2)].p,
-                   L.est[slot(t + 3)].p, t);
-        else
+                   L.est[slot(t + 3)].p, t, -1, -1);
+        else if (k < 3)
             for (int m = t; m < t + k; m++) step(L.est[slot(m)].p, L.est[slot(m + 1)].p, d_partial_);
-        OF2D_HIP(hipEventRecord(ev(ev_step_, g), st_));
         SeqnormBatch B;
         B.K = k;
         B.stop = stop;
@@ -625,7 +632,35 @@ int Registration::run_exact_pipelined_on(Level &L, int niter, const StepFn &step
             B.out[i] = d_seq_.p + 2 * (size_t)((t + i) % ring2);
             B.dbg[i] = sn_debug ? dbg.p + kDbg * (size_t)((t + i) % ring2) : nullptr;
         }
-        enqueue_norms(B, L, g, npx, hs_.seqh + 2 * (size_t)(t % ring2));
+        if (parts) {
+            // part q: its bands' triple on st_, then on sn_st_ the pass over the
+            // tiles whose terms all lie in rows written so far
+            if (g >= kSeqSets) OF2D_HIP(hipStreamWaitEvent(sn_st_, ev(ev_walk_, g - kSeqSets), 0));
+            const int P = OF2D_SN_PARTS;
+            for (int q = 0; q < P; q++) {
+                const int blo = q * nbands / P, bhi = (q + 1) * nbands / P;
+                step3m(L.est[slot(t)].p, L.est[slot(t + 1)].p, L.est[slot(t + 2)].p,
+                       L.est[slot(t + 3)].p, t, blo, bhi);
+                OF2D_HIP(hipEventRecord(ev_part_, st_));
+                OF2D_HIP(hipStreamWaitEvent(sn_st_, ev_part_, 0));
+                const long rhi = q == P - 1 ? L.dy : std::min<long>(L.dy, (long)bhi * band_rows);
+                B.tile_lo = B.tile_hi;
+                B.tile_hi = q == P - 1 ? 0u : (unsigned)(rhi * L.dx / kSnTile);
+                if (q == P - 1 || B.tile_hi > B.tile_lo) {
+                    SeqnormBatch Bq = B;
+                    if (q == P - 1) Bq.tile_hi = 0;  // the rest
+                    launch_seqnorm_pass(Bq, L.dx, L.dy, L.P, sn_st_);
+                } else {
+                    B.tile_hi = B.tile_lo;
+                }
+            }
+            OF2D_HIP(hipEventRecord(ev(ev_step_, g), st_));
+            OF2D_HIP(hipEventRecord(ev(ev_pass_, g), sn_st_));
+            enqueue_norms(B, L, g, npx, hs_.seqh + 2 * (size_t)(t % ring2), true);
+        } else {
+            OF2D_HIP(hipEventRecord(ev(ev_step_, g), st_));
+            enqueue_norms(B, L, g, npx, hs_.seqh + 2 * (size_t)(t % ring2));
+        }
         g++;
     };
     const int ntrip = niter / 3 * 3;
@@ -832,11 +867,13 @@ int Registration::loop_hs(Level &L, int niter, float alpha, int &final_buf) {
         })
               : StepFn3(),
         nblk,
-        pairs ? StepFn3M([&](const float2 *src, float2 *d1, float2 *d2, float2 *d3, int t0) {
+        pairs ? StepFn3M([&](const float2 *src, float2 *d1, float2 *d2, float2 *d3, int t0,
+                             int band_lo, int band_hi) {
             // the exact Logger's triples: every iterate stored (partials unused)
             launch_hs_jacobi3(src, d3, L.dI.p, L.It.p, L.P, L.dx, L.dy, 0, L.dy, alphasq, -1,
                               L.dy + 1, d_partial_, d_partial_ + (size_t)nb * 2,
-                              d_partial_ + (size_t)nb * 4, d_status_, range_flag, st_, -1, -1,
+                              d_partial_ + (size_t)nb * 4, d_status_, range_flag, st_, band_lo,
+                              band_hi,
                               (gi_ < 0 ? hs3_gradients_from_image(L.dx, L.dy) : gi_ != 0)
                                   ? L.Iaux.p
                                   : nullptr,

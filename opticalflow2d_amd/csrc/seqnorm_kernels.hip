@@ -342,6 +342,7 @@ struct SnJobs {
     // past it returns at once (its norms are never read)
     const int *stop;
     int t0;
+    unsigned tlo, thi;  // the pass: tiles [tlo, thi) (thi 0: all)
 };
 __device__ __forceinline__ bool sn_stopped(const SnJobs &J) {
     return J.stop &&
@@ -646,12 +647,12 @@ template <int K>
 __global__ __launch_bounds__(kSnThreads) __attribute__((amdgpu_waves_per_eu(OF2D_SN_WPE)))
 void seqnorm_tables(unsigned N, int dimx, int P, unsigned nt, SnJobs J) {
     if (sn_block_stopped(J)) return;
-    if (blockIdx.x == 0 && threadIdx.x < 4)
+    if (blockIdx.x == 0 && threadIdx.x < 4 && J.tlo == 0)
 #pragma unroll
         for (int i = 0; i < K; i++) J.ws[i].cnt[threadIdx.x] = 0;  // seqnorm_check's list
-    const unsigned b = (unsigned)__builtin_amdgcn_readfirstlane(
-        (int)(blockIdx.x * (kSnThreads / 64) + threadIdx.x / 64));
-    if (b >= nt) return;
+    const unsigned b = J.tlo + (unsigned)__builtin_amdgcn_readfirstlane(
+                                   (int)(blockIdx.x * (kSnThreads / 64) + threadIdx.x / 64));
+    if (b >= (J.thi ? J.thi : nt)) return;
     unsigned hd[K][2];
     int ncmax = 0;
 #pragma unroll
@@ -1435,6 +1436,8 @@ SnJobs jobs_of(const SeqnormBatch &B, unsigned nt) {
     }
     J.stop = B.stop;
     J.t0 = B.t0;
+    J.tlo = B.tile_lo;
+    J.thi = B.tile_hi;
     return J;
 }
 }  // namespace
@@ -1443,7 +1446,9 @@ void launch_seqnorm_pass(const SeqnormBatch &B, int dimx, int dimy, int P, hipSt
     const unsigned nt = check_geometry(dimx, dimy, P);
     const unsigned N = (unsigned)((size_t)dimx * dimy);
     const SnJobs J = jobs_of(B, nt);
-    const dim3 grid((nt + kSnThreads / 64 - 1) / (kSnThreads / 64));
+    const unsigned hi = B.tile_hi ? std::min(B.tile_hi, nt) : nt;
+    if (B.tile_lo >= hi) return;
+    const dim3 grid((hi - B.tile_lo + kSnThreads / 64 - 1) / (kSnThreads / 64));
     switch (B.K) {
         case 1: hipLaunchKernelGGL(seqnorm_tables<1>, grid, dim3(kSnThreads), 0, st, N, dimx, P, nt, J); break;
         case 2: hipLaunchKernelGGL(seqnorm_tables<2>, grid, dim3(kSnThreads), 0, st, N, dimx, P, nt, J); break;
