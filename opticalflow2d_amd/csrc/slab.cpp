@@ -369,12 +369,15 @@ bool can_split(const of2d_slab *s) {
 // device's worth of short ones (512-row slabs of 4096: 245 blocks of 19-line
 // bands rather than 910 of 5-line bands, whose halo rows and prologue
 // double the work per pixel; profiles/r05f_ranks_attribution.txt)
+#ifndef OF2D_SLAB_SHARE_Q
+#define OF2D_SLAB_SHARE_Q 4  // slabs assumed to run side by side (A/B knob; 1: none)
+#endif
 int triple_slots(const of2d_slab *s) {
     if (!s->grp) return 1024;
     int k = 0;
     for (const of2d_slab *o : s->grp->slabs)
         if (o && o->device == s->device) k++;
-    return k > 1 ? 1024 / std::min(k, 4) : 1024;
+    return k > 1 ? 1024 / std::min(k, OF2D_SLAB_SHARE_Q) : 1024;
 }
 SlabGeometry slab_geometry_as(const of2d_slab *s, bool split, int slots = 1024) {
     SlabGeometry g;

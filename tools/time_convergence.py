@@ -23,15 +23,29 @@ for name, (ref, mov) in cases.items():
         extra = {}
         if os.environ.get("OF2D_CONV_CHUNK"):  # iterations per host decision block
             extra["chunk"] = int(os.environ["OF2D_CONV_CHUNK"])
-        with ImageRegistration((n, n), [1000], 0, 0, [0.1], logger_fp64=fp64, **extra) as r:
-            r.set_images(ref, mov)
-            r.estimate()  # warm-up
+        if os.environ.get("OF2D_CONV_FRESH"):
+            # a fresh registration per estimate (as a MEX register call after
+            # init: bench.py default_semantics), the first one a warm-up
             ts = []
-            for _ in range(reps):
-                t0 = time.perf_counter()
-                r.estimate()
-                ts.append(time.perf_counter() - t0)
-            it = r.iterations()[0]
+            for rep in range(reps + 1):
+                with ImageRegistration((n, n), [1000], 0, 0, [0.1], logger_fp64=fp64,
+                                       **extra) as r:
+                    r.set_images(ref, mov)
+                    t0 = time.perf_counter()
+                    r.estimate()
+                    if rep:
+                        ts.append(time.perf_counter() - t0)
+                    it = r.iterations()[0]
+        else:
+            with ImageRegistration((n, n), [1000], 0, 0, [0.1], logger_fp64=fp64, **extra) as r:
+                r.set_images(ref, mov)
+                r.estimate()  # warm-up
+                ts = []
+                for _ in range(reps):
+                    t0 = time.perf_counter()
+                    r.estimate()
+                    ts.append(time.perf_counter() - t0)
+                it = r.iterations()[0]
         # the second estimate warm-starts from the first's motion (reference
         # semantics): iterations of the timed calls, not of the first
         t = min(ts)
