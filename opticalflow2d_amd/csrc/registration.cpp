@@ -219,30 +219,39 @@ void Registration::ensure_device() {
     int prio_lo = 0, pr = 0;
     OF2D_HIP(hipDeviceGetStreamPriorityRange(&prio_lo, &pr));
     OF2D_HIP(hipStreamCreateWithFlags(&st_, hipStreamNonBlocking));
+    // HS's exact loop on CU-masked streams (OF2D_SN_CUMASK; a device or
+    // runtime without CU masks gets unmasked streams)
+    std::vector<uint32_t> big((ncu_ + 31) / 32, 0u), small(big.size(), 0u), pass(big.size(), 0u);
+    const int pc = OF2D_SN_PASS_CUS > 0 && OF2D_SN_CUMASK + OF2D_SN_PASS_CUS < ncu_
+                       ? OF2D_SN_PASS_CUS : 0;
+    bool masked = false;
     if (OF2D_SN_CUMASK > 0 && OF2D_SN_CUMASK < ncu_) {
-        std::vector<uint32_t> big((ncu_ + 31) / 32, 0u), small(big.size(), 0u), pass(big.size(), 0u);
-        const int pc = OF2D_SN_PASS_CUS > 0 && OF2D_SN_CUMASK + OF2D_SN_PASS_CUS < ncu_
-                           ? OF2D_SN_PASS_CUS : 0;
         for (int c = 0; c < ncu_; c++) {
             if (c < OF2D_SN_CUMASK) small[c / 32] |= 1u << (c % 32);
             else if (c < OF2D_SN_CUMASK + pc) pass[c / 32] |= 1u << (c % 32);
             else big[c / 32] |= 1u << (c % 32);
         }
-        OF2D_HIP(hipExtStreamCreateWithCUMask(&hs_st_, (uint32_t)big.size(), big.data()));
-        OF2D_HIP(hipExtStreamCreateWithCUMask(&sn_st_, (uint32_t)big.size(),
-                                              pc ? pass.data() : big.data()));
-        tri_slots_ = 4 * (ncu_ - OF2D_SN_CUMASK - pc);
-        if (OF2D_SN_CUMASK_CHAIN) {
-            OF2D_HIP(hipExtStreamCreateWithCUMask(&fx_st_, (uint32_t)small.size(), small.data()));
-            for (hipStream_t &w : wk_st_)
-                OF2D_HIP(hipExtStreamCreateWithCUMask(&w, (uint32_t)small.size(), small.data()));
-        } else {
-            OF2D_HIP(hipStreamCreateWithPriority(&fx_st_, hipStreamNonBlocking, pr));
-            for (hipStream_t &w : wk_st_)
-                OF2D_HIP(hipStreamCreateWithPriority(&w, hipStreamNonBlocking, pr));
+        masked = hipExtStreamCreateWithCUMask(&hs_st_, (uint32_t)big.size(), big.data()) ==
+                     hipSuccess &&
+                 hipExtStreamCreateWithCUMask(&sn_st_, (uint32_t)big.size(),
+                                              pc ? pass.data() : big.data()) == hipSuccess;
+        if (!masked) {
+            (void)hipGetLastError();
+            for (hipStream_t *q : {&hs_st_, &sn_st_})
+                if (*q) (void)hipStreamDestroy(*q);
+            hs_st_ = sn_st_ = nullptr;
         }
+    }
+    if (masked) {
+        tri_slots_ = 4 * (ncu_ - OF2D_SN_CUMASK - pc);
     } else {
         OF2D_HIP(hipStreamCreateWithFlags(&sn_st_, hipStreamNonBlocking));
+    }
+    if (masked && OF2D_SN_CUMASK_CHAIN) {
+        OF2D_HIP(hipExtStreamCreateWithCUMask(&fx_st_, (uint32_t)small.size(), small.data()));
+        for (hipStream_t &w : wk_st_)
+            OF2D_HIP(hipExtStreamCreateWithCUMask(&w, (uint32_t)small.size(), small.data()));
+    } else {
         // the fix and the walks at high priority: they are the latency chain that
         // gates the steps (ring) and passes (workspaces) a few groups later, and
         // wait for CUs behind the bandwidth kernels otherwise (4096^2 procedural
