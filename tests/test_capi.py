@@ -135,3 +135,27 @@ def test_field_size_guard(of2d_lib, dims, ok):
                 ImageRegistration(dims, [1], 0, 0, [0.1])
     finally:
         set_print_sink(None)
+
+
+def test_registration_options_host_validation(of2d_lib):
+    """of2d_set_option's host-side checks (include/of2d.h): every documented
+    key is accepted before first use, unknown keys and out-of-range ngpus are
+    refused with invalid_argument, and nothing here touches a device."""
+    from opticalflow2d_amd import ImageRegistration, InvalidArgument, set_print_sink
+    set_print_sink(lambda s: None)
+    try:
+        r = ImageRegistration((32, 24), [3], 0, 0, [0.1])
+        try:
+            for k, v in [("fixed_iters", 1), ("fixed_iters", 0), ("logger_fp64", 1),
+                         ("logger_fp64", 0), ("hs_gradients_from_image", -1),
+                         ("hs_gradients_from_image", 1), ("slab_split", -1), ("slab_split", 0),
+                         ("slab_split", 1), ("ngpus", 1), ("ngpus", 16), ("ngpus", 1),
+                         ("ngpus_share", 1), ("ngpus_share", 0), ("chunk", 9), ("device", 0)]:
+                r.set_option(k, v)
+            for k, v in [("ngpus", 0), ("ngpus", 17), ("no_such_option", 1)]:
+                with pytest.raises(InvalidArgument):
+                    r.set_option(k, v)
+        finally:
+            r.close()
+    finally:
+        set_print_sink(None)
