@@ -202,7 +202,12 @@ int of2d_slab_last_run_kernel_us(const of2d_slab *s, double *avg_us, int *nlaunc
  *   the halo exchange and two edge launches (auto: when a neighbour is on
  *   another device or behind RCCL), never, or whenever the slab has >= 48
  *   j-lines (tests of the multi-device launch order on one device);
- *   bit-identical either way */
+ *   bit-identical either way
+ *   "rccl_self_halo" (0 = default, 1; a one-rank RCCL communicator only):
+ *   every halo exchange also sends the slab's boundary j-lines to rank 0
+ *   itself (ncclSend / ncclRecv in a group, into a scratch buffer that is never
+ *   read), and "split" 1 then splits the one-rank slab: the RCCL halo calls
+ *   of an N-rank run, rehearsed on one GPU; bit-identical */
 int of2d_slab_set_option(of2d_slab *s, const char *key, double value);
 int of2d_slab_destroy(of2d_slab *s);
 const char *of2d_slab_last_error(const of2d_slab *s);

@@ -66,6 +66,14 @@ struct of2d_slab {
     // slab is tall enough (option "split": tests run the multi-device launch
     // order on co-located slabs)
     int split = -1;
+    // a rehearsal of the RCCL halo on one GPU (option "rccl_self_halo", tests
+    // only): a one-rank communicator sends its boundary j-lines to itself into
+    // a scratch buffer at every exchange, and its triples take the split
+    // launches, so ncclGroupStart / ncclSend / ncclRecv run on comm_st between
+    // the interior and edge launches as on an N-rank communicator; the motion
+    // is untouched (the scratch is never read)
+    int self_halo = 0;
+    float *d_selfx = nullptr;
     of2d::SlabExact *ex = nullptr;
     int device = 0;
     float alpha = 0.0f;
@@ -243,10 +251,22 @@ void local_exchange(of2d_slab *s, float2 *u, int lines, size_t cnt, hipStream_t 
 
 // `lines` (1..3) boundary j-lines to each neighbour, on stream `st`
 void halo_exchange(of2d_slab *s, float2 *u, int lines, hipStream_t st) {
-    if (s->nranks == 1) return;
     const long P = s->P;
     // lines are contiguous at pitch P: 2 floats per px, the padding travels too
     const size_t cnt = 2 * ((size_t)(lines - 1) * P + (size_t)s->dimx);
+    if (s->nranks == 1) {
+        if (!(s->self_halo && s->comm)) return;
+        const size_t cap = 2 * ((size_t)2 * P + (size_t)s->dimx);  // three lines
+        if (!s->d_selfx) OF2D_HIP(hipMalloc(&s->d_selfx, 2 * cap * sizeof(float)));
+        for (int side = 0; side < 2; side++) {  // one peer op pair per group, as below
+            OF2D_NCCL(ncclGroupStart());
+            OF2D_NCCL(ncclSend(side ? u + (long)(s->nrows - lines) * P : u, cnt, ncclFloat, 0,
+                               s->comm, st));
+            OF2D_NCCL(ncclRecv(s->d_selfx + side * cap, cnt, ncclFloat, 0, s->comm, st));
+            OF2D_NCCL(ncclGroupEnd());
+        }
+        return;
+    }
     if (s->grp) return local_exchange(s, u, lines, cnt, st);
     OF2D_NCCL(ncclGroupStart());
     if (s->rank > 0) {
@@ -359,8 +379,11 @@ bool remote_neighbour(const of2d_slab *s) {
 
 // the slab is tall enough for the interior / edge split (two E-line edges and
 // an interior of at least E lines)
+bool can_split_shape(const of2d_slab *s) {
+    return s->nrows >= 3 * SlabGeometry().E && s->dimx >= 2;
+}
 bool can_split(const of2d_slab *s) {
-    return s->nranks > 1 && s->nrows >= 3 * SlabGeometry().E && s->dimx >= 2;
+    return (s->nranks > 1 || (s->self_halo && s->comm)) && can_split_shape(s);
 }
 // Block slots a whole-slab triple may take: the device's 1024 (4 per CU), or,
 // with k > 1 slabs of an in-process group on this device, 1024 / min(k, 4) —
@@ -379,10 +402,11 @@ int triple_slots(const of2d_slab *s) {
         if (o && o->device == s->device) k++;
     return k > 1 ? 1024 / std::min(k, OF2D_SLAB_SHARE_Q) : 1024;
 }
-SlabGeometry slab_geometry_as(const of2d_slab *s, bool split, int slots = 1024) {
+SlabGeometry slab_geometry_as(const of2d_slab *s, bool split, int slots = 1024,
+                              bool any_ranks = false) {
     SlabGeometry g;
     const int gx = (s->dimx + of2d::kHs3Out - 1) / of2d::kHs3Out;
-    g.split = split && can_split(s);
+    g.split = split && (any_ranks ? can_split_shape(s) : can_split(s));
     g.slots = slots;
     if (g.split) {
         const int ni = s->nrows - 2 * g.E;
@@ -403,9 +427,10 @@ SlabGeometry slab_geometry(const of2d_slab *s) {
 }
 // partial-row length for every geometry: the allocation at create, before the
 // group's other slabs (whose devices decide the split and the slots) or the
-// option are known
+// options are known (the split shape whatever the rank count: rccl_self_halo
+// splits a one-rank slab)
 int partial_blocks_cap(const of2d_slab *s) {
-    int nb = slab_geometry_as(s, true).nb;
+    int nb = slab_geometry_as(s, true, 1024, true).nb;
     for (int slots : {1024, 512, 341, 256}) nb = std::max(nb, slab_geometry_as(s, false, slots).nb);
     return nb;
 }
@@ -1182,6 +1207,14 @@ int of2d_slab_set_option(of2d_slab *s, const char *key, double value) {
         s->split = value < 0.0 ? -1 : (value != 0.0 ? 1 : 0);
         return OF2D_OK;
     }
+    if (std::strcmp(key, "rccl_self_halo") == 0) {
+        if (value != 0.0 && !(s->comm && s->nranks == 1)) {
+            s->err = "slab: rccl_self_halo needs a one-rank RCCL communicator";
+            return OF2D_ERR_INVALID_ARGUMENT;
+        }
+        s->self_halo = value != 0.0;
+        return OF2D_OK;
+    }
     if (std::strcmp(key, "hs_gradients_from_image") == 0) {
         s->gi = value < 0.0 ? -1 : (value != 0.0 ? 1 : 0);
         return OF2D_OK;
@@ -1234,6 +1267,7 @@ int of2d_slab_destroy(of2d_slab *s) {
     if (s->d_partial) (void)hipFree(s->d_partial);
     if (s->d_sums) (void)hipFree(s->d_sums);
     if (s->d_all) (void)hipFree(s->d_all);
+    if (s->d_selfx) (void)hipFree(s->d_selfx);
     if (s->d_status) (void)hipFree(s->d_status);
     if (s->d_stage) (void)hipFree(s->d_stage);
     if (s->ev0) (void)hipEventDestroy(s->ev0);

@@ -10,7 +10,10 @@ the process layout the multi-GPU bench uses:
   line) with a one-rank RCCL communicator (``--rccl``);
 * a one-rank communicator (``ncclCommInitRank`` + the Logger ``ncclAllReduce``
   per chunk + the divide-by-zero vote) against the communicator-free slab:
-  bit-identical motion and the same iteration count, with convergence on.
+  bit-identical motion and the same iteration count, with convergence on;
+* the halo's send / recv calls themselves, rehearsed by a one-rank
+  communicator sending its boundary lines to itself between the interior and
+  edge launches of split triples (option ``rccl_self_halo``).
 
 Each case runs in a fresh process so the library load order is the bench's.
 """
@@ -49,6 +52,55 @@ assert d0 == d1, (d0, d1)
 assert np.array_equal(m0.view(np.uint64), m1.view(np.uint64))
 print("ONE-RANK-OK", d0)
 """
+
+
+SELF_HALO = r"""
+import sys, numpy as np
+sys.path.insert(0, sys.argv[1])
+from opticalflow2d_amd import SlabSolver, lib
+from opticalflow2d_amd import synthetic as S
+from opticalflow2d_amd.slab import rccl_unique_id
+lib()
+import torch.distributed  # noqa: F401
+n = 640
+ref, mov = S.procedural_pair(n, 0, n)
+for fixed, niter in ((True, 31), (False, 1000)):
+    out = []
+    for uid in (None, rccl_unique_id()):
+        s = SlabSolver(n, n, 0.1, 0, 1, device=0, unique_id=uid)
+        if uid is not None:
+            s.set_option("rccl_self_halo", 1)
+            s.set_option("split", 1)
+            assert s.info()["split"] == 1, s.info()
+        else:
+            assert s.info()["split"] == 0, s.info()
+        s.set_images(ref, mov)
+        done = s.run(niter, fixed_iters=fixed)
+        out.append((done, s.motion()))
+        s.close()
+    (d0, m0), (d1, m1) = out
+    assert d0 == d1 and (fixed or 1 < d0 <= niter), (d0, d1)
+    assert np.array_equal(m0.view(np.uint64), m1.view(np.uint64))
+    print("SELF-HALO-OK", fixed, d0)
+try:
+    s = SlabSolver(64, 64, 0.1, 0, 1, device=0)
+    s.set_option("rccl_self_halo", 1)
+    raise SystemExit("rccl_self_halo accepted without a communicator")
+except Exception as e:
+    assert "one-rank RCCL communicator" in str(e), e
+print("SELF-HALO-REFUSED")
+"""
+
+
+def test_rccl_halo_rehearsal_on_one_rank():
+    """The halo's ncclGroupStart / ncclSend / ncclRecv between the interior and
+    edge launches of split triples (the N-rank launch order, slab.cpp fused),
+    sent by a one-rank communicator to itself: the fixed-iteration and
+    convergence-on runs stay bit-identical to the communicator-free slab."""
+    r = subprocess.run([sys.executable, "-c", SELF_HALO, ROOT], capture_output=True, text=True,
+                       timeout=240)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    assert r.stdout.count("SELF-HALO-OK") == 2 and "SELF-HALO-REFUSED" in r.stdout
 
 
 def _free_port():
