@@ -8,7 +8,8 @@
 #        prof (rocprofv3 kernel stats of bench.py), conv (convergence-on
 #        timings at 4096^2), convprof (their kernel trace + stats),
 #        configs (bench_configs.py), ranks (ngpus timings), ranksprof (their
-#        kernel trace, 8 ranks), snbench /
+#        kernel trace, 8 ranks), texprof / freshprof (kernel trace of the
+#        texture pair's warm / fresh loops), snbench /
 #        snprof (the Logger-norm harness: stage timings / kernel stats)
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
@@ -40,6 +41,7 @@ for s in "$@"; do
         ranks) run ranks 600 python -u tools/time_ranks.py ;;
         ranksprof) run ranksprof 600 rocprofv3 --kernel-trace --output-format csv -d "$R/$O/${tag}_ranksprof" -o k -- python3 -u "$R/tools/time_ranks.py" 4096 1 fixed,conv 8 ;;
         texprof) OF2D_CONV_CASE=texture OF2D_CONV_ONLY=1 run texprof 300 rocprofv3 --kernel-trace --output-format csv -d "$R/$O/${tag}_texprof" -o k -- python3 -u "$R/tools/time_convergence.py" 4096 1 ;;
+        freshprof) OF2D_CONV_FRESH=1 OF2D_CONV_CASE=texture OF2D_CONV_ONLY=1 run freshprof 300 rocprofv3 --kernel-trace --output-format csv -d "$R/$O/${tag}_freshprof" -o k -- python3 -u "$R/tools/time_convergence.py" 4096 1 ;;
         snbench) run snbench 300 bash -c "tools/seqnorm_bench 4096 12 3 0.95 && tools/seqnorm_bench 4096 12 1 0.95 && tools/seqnorm_bench 4096 12 3 0.8" ;;
         snws) run snws 300 env SNB_WS=1 tools/seqnorm_bench 4096 12 3 0.95 ;;
         sndebug) run sndebug 300 env OF2D_LIB_PATH=tools/ab/sndebug/libof2d.so python -u tools/time_convergence.py 4096 1 ;;  # tools/build_variant.sh sndebug registration.cpp -DOF2D_SN_DEBUG=1
