@@ -162,6 +162,10 @@ constexpr int kMaxEst = OF2D_SN_RING + 1 > 16 ? OF2D_SN_RING + 1 : 16;
 #ifndef OF2D_SN_CUMASK_CHAIN
 #define OF2D_SN_CUMASK_CHAIN 0
 #endif
+// 1: only the walks on the reserved CUs (check and entries on every CU)
+#ifndef OF2D_SN_CUMASK_WALK
+#define OF2D_SN_CUMASK_WALK 0
+#endif
 
 struct Level {
     int dx = 0, dy = 0, P = 0;

@@ -251,6 +251,10 @@ void Registration::ensure_device() {
         OF2D_HIP(hipExtStreamCreateWithCUMask(&fx_st_, (uint32_t)small.size(), small.data()));
         for (hipStream_t &w : wk_st_)
             OF2D_HIP(hipExtStreamCreateWithCUMask(&w, (uint32_t)small.size(), small.data()));
+    } else if (masked && OF2D_SN_CUMASK_WALK) {
+        OF2D_HIP(hipStreamCreateWithPriority(&fx_st_, hipStreamNonBlocking, pr));
+        for (hipStream_t &w : wk_st_)
+            OF2D_HIP(hipExtStreamCreateWithCUMask(&w, (uint32_t)small.size(), small.data()));
     } else {
         // the fix and the walks at high priority: they are the latency chain that
         // gates the steps (ring) and passes (workspaces) a few groups later, and

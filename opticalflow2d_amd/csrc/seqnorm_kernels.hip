@@ -76,6 +76,15 @@ namespace of2d {
 namespace {
 
 constexpr int kSnThreads = 256;                 // table kernels: 4 waves
+// issue priority of the Logger chain's waves (check, entries, walk): the
+// triple kernel's waves run at raised priority (progress_prio) and would
+// otherwise win every issue slot of a SIMD they share with a walker
+#ifndef OF2D_SN_CHAIN_PRIO
+#define OF2D_SN_CHAIN_PRIO 0
+#endif
+__device__ __forceinline__ void sn_chain_prio() {
+    if constexpr (OF2D_SN_CHAIN_PRIO > 0) __builtin_amdgcn_s_setprio(OF2D_SN_CHAIN_PRIO);
+}
 constexpr int kSnSegs = kSnTile / 64;           // 64-term segments per tile
 constexpr int kSnCand = 4;                      // candidate binades per tile and norm
 // relative width of the profile's prediction window (tables): a tile takes the
@@ -745,6 +754,7 @@ __device__ __forceinline__ double sn_drift(const SnWs &ws, unsigned nt, int src,
 }
 __global__ __launch_bounds__(kSnChk) void seqnorm_check_sums(unsigned nt, SnJobs J) {
     if (sn_block_stopped(J)) return;
+    sn_chain_prio();
     const SnWs &ws = J.ws[blockIdx.y];
     const int use_prof = J.use_prof[blockIdx.y];
     const unsigned b = blockIdx.x * kSnChk + threadIdx.x;
@@ -769,6 +779,7 @@ __global__ __launch_bounds__(kSnChk) void seqnorm_check_sums(unsigned nt, SnJobs
 // total
 __global__ __launch_bounds__(kSnScan) void seqnorm_check_scan(unsigned nt, unsigned nb, SnJobs J) {
     if (sn_block_stopped(J)) return;
+    sn_chain_prio();
     const SnWs &ws = J.ws[blockIdx.y];
     const double *p_off = J.p_off[blockIdx.y];
     const unsigned chunk = (nb + kSnScan - 1) / kSnScan;
@@ -826,6 +837,7 @@ __global__ __launch_bounds__(kSnScan) void seqnorm_check_scan(unsigned nt, unsig
 }
 __global__ __launch_bounds__(kSnChk) void seqnorm_check(unsigned nt, SnJobs J) {
     if (sn_block_stopped(J)) return;
+    sn_chain_prio();
     const SnWs &ws = J.ws[blockIdx.y];
     const int use_prof = J.use_prof[blockIdx.y];
     const unsigned b = blockIdx.x * kSnChk + threadIdx.x;
@@ -925,6 +937,7 @@ template <int K>
 __global__ __launch_bounds__(kSnThreads) void seqnorm_entries(unsigned N, int dimx, int P,
                                                               unsigned nt, SnJobs J) {
     if (sn_block_stopped(J)) return;
+    sn_chain_prio();
     bool many = false;
 #pragma unroll
     for (int i = 0; i < K; i++) many |= J.ws[i].cnt[0] > kSnRefillMin;
@@ -1236,6 +1249,7 @@ constexpr int kSnAhead = 8;  // windows loaded per step: the next step's loads h
 __global__ __launch_bounds__(64 * kSnWalkWaves) void seqnorm_walk(unsigned N, int dimx, int P,
                                                                    unsigned nt, SnJobs J) {
     if (sn_block_stopped(J)) return;  // one decision for the whole block
+    sn_chain_prio();
     const int job = blockIdx.x >> 1;
     const int n = blockIdx.x & 1;  // 0: |cur - prev|, 1: |prev|
     const int lane = threadIdx.x & 63;

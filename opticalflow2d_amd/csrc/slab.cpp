@@ -393,7 +393,7 @@ bool can_split(const of2d_slab *s) {
 // bands rather than 910 of 5-line bands, whose halo rows and prologue
 // double the work per pixel; profiles/r05f_ranks_attribution.txt)
 #ifndef OF2D_SLAB_SHARE_Q
-#define OF2D_SLAB_SHARE_Q 4  // slabs assumed to run side by side (A/B knob; 1: none)
+#define OF2D_SLAB_SHARE_Q 2  // slabs assumed to run side by side (A/B knob; 1: none)
 #endif
 int triple_slots(const of2d_slab *s) {
     if (!s->grp) return 1024;
