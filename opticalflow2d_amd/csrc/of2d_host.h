@@ -162,9 +162,13 @@ constexpr int kMaxEst = OF2D_SN_RING + 1 > 16 ? OF2D_SN_RING + 1 : 16;
 #ifndef OF2D_SN_CUMASK_CHAIN
 #define OF2D_SN_CUMASK_CHAIN 0
 #endif
-// 1: only the walks on the reserved CUs (check and entries on every CU)
+// 1: the walks on the reserved CUs, the check and entries on every CU (a walk
+// block beside the triple's and pass's blocks slows them more than the walk
+// gains there: 4096^2 convergence on, texture 142-144 -> 132-136, procedural
+// 118-120 -> 114-116 us per iteration; 8, 24 or 32 reserved CUs the same,
+// profiles/r05m_cuwalk_ab.log)
 #ifndef OF2D_SN_CUMASK_WALK
-#define OF2D_SN_CUMASK_WALK 0
+#define OF2D_SN_CUMASK_WALK 1
 #endif
 
 struct Level {
