@@ -167,6 +167,15 @@ constexpr double kMallBytes = 256.0 * 1024 * 1024;
 inline bool hs3_gradients_from_image(int dimx, int nrows) {
     return 12.0 * dimx * nrows > kMallBytes;
 }
+// HS's exact-Logger loop streams more than the triple: per three iterations
+// the MID triple (u0 in, three iterates out) and the Logger pass (four
+// iterates in, non-temporal) move 64 B/px beside the gradients' 12, so dI + It
+// stay in the MALL only where all of it fits (4096^2: GI and the pass's
+// non-temporal loads 140 -> 131 us per iteration texture, 118 -> 107
+// procedural, profiles/r05o_gi_nt_ab.log)
+inline bool hs3_exact_gradients_from_image(int dimx, int nrows) {
+    return 76.0 * dimx * nrows > kMallBytes;
+}
 // Ia (Iaux, the image dI was taken of) non-null: the kernel derives the
 // gradients from it (24 instead of 28 B/px per launch, same bits); null: it
 // reads dI

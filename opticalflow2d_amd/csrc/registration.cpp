@@ -887,7 +887,7 @@ int Registration::loop_hs(Level &L, int niter, float alpha, int &final_buf) {
                               L.dy + 1, d_partial_, d_partial_ + (size_t)nb * 2,
                               d_partial_ + (size_t)nb * 4, d_status_, range_flag, st_, band_lo,
                               band_hi,
-                              (gi_ < 0 ? hs3_gradients_from_image(L.dx, L.dy) : gi_ != 0)
+                              (gi_ < 0 ? hs3_exact_gradients_from_image(L.dx, L.dy) : gi_ != 0)
                                   ? L.Iaux.p
                                   : nullptr,
                               d1, d2, reinterpret_cast<const int *>(d_status_ + kStopWord), t0,

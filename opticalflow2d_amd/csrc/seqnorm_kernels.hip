@@ -379,6 +379,14 @@ __device__ __forceinline__ bool sn_block_stopped(const SnJobs &J) {
 // (K = 3: a ring of 2 measured 119 us per three-update pass against 144 for 4,
 // whose 155 VGPRs leave 3 waves per SIMD, and 93 for the loads alone;
 // profiles/r04g_sn_ring_ab.log)
+// the pass's (and refill's) iterate loads non-temporal: its 537 MB per batch
+// at 4096^2 would otherwise push the triple's gradient fields out of the MALL
+// they stay in between launches (with the exact loop's GI triples, of2d_device.h
+// hs3_exact_gradients_from_image: -7 to -10 % per iteration,
+// profiles/r05o_gi_nt_ab.log)
+#ifndef OF2D_SN_NT
+#define OF2D_SN_NT 1
+#endif
 #ifndef OF2D_SN_RING3
 #define OF2D_SN_RING3 2
 #endif
@@ -402,7 +410,15 @@ struct SnLoader {
         if (L < N) {
             const size_t off = (size_t)jj * (size_t)P + ii;
 #pragma unroll
-            for (int k = 0; k <= K; k++) v[k] = J.u[j0 + k][off];
+            for (int k = 0; k <= K; k++) {
+#if OF2D_SN_NT
+                typedef float v2f __attribute__((ext_vector_type(2)));
+                const v2f w = __builtin_nontemporal_load(reinterpret_cast<const v2f *>(J.u[j0 + k] + off));
+                v[k] = make_float2(w.x, w.y);
+#else
+                v[k] = J.u[j0 + k][off];
+#endif
+            }
         }
         L += 64u;
         ii += 64u;

@@ -347,6 +347,11 @@ struct SlabGeometry {
 bool use_gi(const of2d_slab *s) {
     return s->gi < 0 ? of2d::hs3_gradients_from_image(s->dimx, s->nrows) : s->gi != 0;
 }
+// the exact-Logger loop's triples (run_exact): its passes stream the iterates
+// beside them (of2d::hs3_exact_gradients_from_image)
+bool use_gi_exact(const of2d_slab *s) {
+    return s->gi < 0 ? of2d::hs3_exact_gradients_from_image(s->dimx, s->nrows) : s->gi != 0;
+}
 // the motion buffer holding neither the result nor the next run's zeroed start
 int scratch_buffer(const of2d_slab *s) {
     for (int b = 0; b < 3; b++)
@@ -541,7 +546,7 @@ int run_exact(of2d_slab *s, int niter) {
     const double npx = (double)s->dimx * s->dimy;
     const int nb = slab_geometry(s).nb;
     unsigned *range_flag = s->d_status + of2d::kRangeFlagWord;
-    const float *ia = use_gi(s) ? s->Imov.p : nullptr;
+    const float *ia = use_gi_exact(s) ? s->Imov.p : nullptr;
     for (bool &w : E.walked) w = false;  // a new loop: no profile yet
     auto ring = [](int a, int t) {  // the (t mod kExR)-th buffer other than a
         const int i = t % kExR;
