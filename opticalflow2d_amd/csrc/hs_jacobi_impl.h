@@ -24,10 +24,13 @@
 #include <type_traits>
 
 
-// the intermediate iterates of the MID triple (read again by the Logger's pass
-// right behind it): default cache policy (0) or non-temporal (1), an A/B knob
+// the intermediate iterates of the MID triple (read again by the Logger's
+// pass): default cache policy (0) or non-temporal (1).  Non-temporal, like the
+// pass's loads, so the MALL keeps the triple's gradient fields: 4096^2 texture
+// convergence 132 -> 124-126 us per iteration, procedural unchanged
+// (profiles/r05q_ahead_ab.log)
 #ifndef OF2D_HS_MID_NT
-#define OF2D_HS_MID_NT 0
+#define OF2D_HS_MID_NT 1
 #endif
 
 namespace of2d {

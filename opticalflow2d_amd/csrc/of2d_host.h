@@ -124,6 +124,12 @@ float logger_error(double sum_diff, double sum_prev, double npx);
 #ifndef OF2D_SN_WALKERS
 #define OF2D_SN_WALKERS 3
 #endif
+// decision blocks the host enqueues ahead of the one it reads while the
+// errors are far from the break (1 near it: a break leaves the enqueued blocks
+// behind it as no-op launches)
+#ifndef OF2D_SN_AHEAD
+#define OF2D_SN_AHEAD 1
+#endif
 constexpr int kMaxEst = OF2D_SN_RING + 1 > 16 ? OF2D_SN_RING + 1 : 16;
 // CUs kept from the bandwidth kernels of HS's exact loop (its triples and
 // passes run on streams with a CU mask without them), so that the loop's

@@ -598,11 +598,13 @@ int Registration::run_exact_pipelined_on(Level &L, int niter, const StepFn &step
     OF2D_HIP(hipMemsetAsync(stop, 0x7f, sizeof(int), st_));  // no break yet
     constexpr int kNoStop = 0x7f7f7f7f;
     // a block: whole triples, few enough groups that no event of a block being
-    // read is recorded again before it is (two blocks in flight)
+    // read is recorded again before it is (OF2D_SN_AHEAD + 1 blocks in flight)
+    constexpr int kInFlight = OF2D_SN_AHEAD + 1;
     const int cb = chunk_set_ ? chunk_ : OF2D_SN_BLOCK;
-    const int blk = std::min(3 * ((cb + 2) / 3), 3 * (kExactEv / 2 - 4));
-    const int ring2 = 2 * blk;  // the sums' ring: two blocks of iterations
-    hs_.ensure(std::max(chunk_, 64));
+    const int blk = std::min(3 * ((cb + 2) / 3), 3 * (kExactEv / kInFlight - 4));
+    const int ring2 = kInFlight * blk;  // the sums' ring: the blocks in flight
+    hs_.ensure(std::max(std::max(chunk_, 64), ring2));
+    if (d_seq_.n < 2 * (size_t)ring2) d_seq_.alloc(2 * (size_t)ring2);
     constexpr bool sn_debug = OF2D_SN_DEBUG != 0;
     constexpr int kDbg = 10;
     DevArray<int> dbg;
@@ -707,9 +709,15 @@ int Registration::run_exact_pipelined_on(Level &L, int niter, const StepFn &step
             throw DeviceError("internal error: the device's Logger break (" + std::to_string(dev) +
                               ") is not the host's (" + std::to_string(tbreak) + ")");
     };
-    if (nblocks > 0) enqueue_block(0);
+    // blocks enqueued so far (of the nbt blocks of triples); the host keeps
+    // `ahead` blocks queued beyond the one it reads: OF2D_SN_AHEAD while the
+    // errors' decay says the break is further away than that, one near it
+    int enq = 0;
+    int ahead = OF2D_SN_AHEAD;
+    float err_prev = -1.0f;  // the last error of the block before
+    if (nblocks > 0) enqueue_block(enq++);
     for (int b = 0; b < nblocks; b++) {
-        if (b + 1 < nbt) enqueue_block(b + 1);  // one block ahead
+        while (enq < nbt && enq <= b + ahead) enqueue_block(enq++);
         // block b's sums: the last walk of each walk stream, then its decide
         for (int q = std::max(gbeg[b + 1] - kWalkers, gbeg[b]); q < gbeg[b + 1]; q++)
             OF2D_HIP(hipEventSynchronize(ev(ev_walk_, q)));
@@ -725,9 +733,10 @@ int Registration::run_exact_pipelined_on(Level &L, int niter, const StepFn &step
                              h[9]);
             }
         }
+        float err = 0.0f;
         for (int t = lo_of(b); t < hi_of(b); t++) {
             const float *sm = hs_.seqh + 2 * (size_t)(t % ring2);
-            const float err = logger_error(sm[0], sm[1], npx);
+            err = logger_error(sm[0], sm[1], npx);
             last_err_.push_back(err);
             if (verbose_) print("Iteration: %d\tError:%.4f\n", t, (double)err);
             if (err < 0.001f && t > 1) {  // ImageRegistrationOpticalFlow.cpp:131-134
@@ -735,6 +744,20 @@ int Registration::run_exact_pipelined_on(Level &L, int niter, const StepFn &step
                 final_buf = slot(t + 1);
                 return t + 1;
             }
+        }
+        if (OF2D_SN_AHEAD > 1) {
+            // blocks to the break at this block's decay of the error (its
+            // ratio to the last block's), or none known: keep the deep queue
+            // only while more than `OF2D_SN_AHEAD + 1` blocks remain
+            ahead = 1;
+            if (err_prev > 0.0f && err > 0.001f && err < err_prev) {
+                const double q = std::log((double)err / err_prev);  // per block, < 0
+                const double left = std::log(0.001 / (double)err) / q;
+                if (left > OF2D_SN_AHEAD + 2) ahead = OF2D_SN_AHEAD;
+            } else if (err_prev > 0.0f && err >= err_prev && err > 0.004f) {
+                ahead = OF2D_SN_AHEAD;  // not decaying and far above the threshold
+            }
+            err_prev = err;
         }
         if (b + 1 == nbt && nblocks > nbt) enqueue_block(nbt);  // the tail, after the rest
     }
