@@ -300,6 +300,11 @@ struct SeqnormBatch {
     // the pass (launch_seqnorm_pass) over tiles [tile_lo, tile_hi) only
     // (tile_hi 0: every tile); the launch with tile_lo 0 resets the check's list
     unsigned tile_lo = 0, tile_hi = 0;
+    // the pass's scale prediction (OF2D_SN_NEAR): workspaces of pair i in the
+    // three groups before this one (their checks' fp64 totals, taken when the
+    // check has stamped them with `epoch` + its iteration + 1), null: none
+    void *near[3][3] = {};
+    unsigned epoch = 0;  // the loop's tag in the stamps' high 12 bits
 };
 // the Logger errors of a walked batch (pair i's sums at seq[2i], seq[2i + 1]),
 // as logger_error does on the host: the first iteration t0 + i > 1 whose

@@ -306,6 +306,7 @@ class Registration {
     int seq_dx_[kSeqWs] = {}, seq_dy_[kSeqWs] = {};  // grid of each workspace's last call
     int chunk_ = 33;  // eleven fused triples per chunk
     bool chunk_set_ = false;  // the option was given (HS's exact loop then uses it too)
+    unsigned exact_epoch_ = 0;  // run_exact_pipelined loops so far (the checks' stamps)
     int gi_ = -1;     // triple kernel: dI from Iaux (1), from dI (0), by size (-1)
     int split_ = -1;  // ranks' triples: interior / edge split (slab option "split")
     int device_ = -1;  // option "device" (-1: the current device at first use)

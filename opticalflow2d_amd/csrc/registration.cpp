@@ -610,6 +610,9 @@ int Registration::run_exact_pipelined_on(Level &L, int niter, const StepFn &step
     DevArray<int> dbg;
     if (sn_debug) dbg.alloc(kDbg * (size_t)ring2);
     bool walked[kSeqWs] = {};  // a new loop: each workspace starts from a fresh state
+    // this loop's tag in the checks' stamps (a stamp of an earlier loop never
+    // matches one of this loop's iterations)
+    const unsigned epoch = (++exact_epoch_ & 0xfffu) << 20;
     std::vector<int> grp_of((size_t)std::max(niter, 1));
     int g = 0;
     // the triple's row bands (launch_hs_jacobi3's geometry at tri_slots_)
@@ -646,7 +649,10 @@ int Registration::run_exact_pipelined_on(Level &L, int niter, const StepFn &step
             walked[w] = true;
             B.out[i] = d_seq_.p + 2 * (size_t)((t + i) % ring2);
             B.dbg[i] = sn_debug ? dbg.p + kDbg * (size_t)((t + i) % ring2) : nullptr;
+            for (int q = 1; q <= 3; q++)  // the pair's workspaces in groups g - 1 .. g - 3
+                if (g - q >= 0) B.near[i][q - 1] = d_seqws_[3 * ((g - q) % kSeqSets) + i].p;
         }
+        B.epoch = epoch;
         if (parts) {
             // part q: its bands' triple on st_, then on sn_st_ the pass over the
             // tiles whose terms all lie in rows written so far

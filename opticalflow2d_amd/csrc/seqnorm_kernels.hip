@@ -294,6 +294,7 @@ struct SnWs {
     double *bs;             // [2][nb] block sums, then block offsets (check)
     float *dr;              // [2][nt + 1] the last call's drift at each tile (check, pass 1)
     unsigned *miss;         // [2] raw segments the last walk stepped (its profile's quality)
+    unsigned *stamp;        // [1] epoch + iteration + 1 of the call whose check wrote Pp[.][nt]
 };
 // The profile of the last call that predicts norm n: its own, except for
 // |prev| after a call whose prev was zero (the Logger's first update), whose
@@ -352,6 +353,10 @@ struct SnJobs {
     const int *stop;
     int t0;
     unsigned tlo, thi;  // the pass: tiles [tlo, thi) (thi 0: all)
+    // the pass: pair i's fp64 totals (Pp) and stamps in the 3 groups before
+    const double *nq[kSnMaxJobs][3];
+    const unsigned *ns[kSnMaxJobs][3];
+    unsigned epoch;
 };
 __device__ __forceinline__ bool sn_stopped(const SnJobs &J) {
     return J.stop &&
@@ -386,6 +391,17 @@ __device__ __forceinline__ bool sn_block_stopped(const SnJobs &J) {
 // profiles/r05o_gi_nt_ab.log)
 #ifndef OF2D_SN_NT
 #define OF2D_SN_NT 1
+#endif
+// the pass scales its profile (the walk of the same pair 12 updates back) by
+// the freshest fp64 total of the pair's norms that a later group's check has
+// written (3, 6 or 9 updates back; read with relaxed loads, each check stamps
+// its totals), extrapolated geometrically, instead of by the trend of the
+// profile's own two last totals: 4096^2 texture convergence 128 -> 122 us per
+// iteration warm, 148 -> 136 fresh, procedural unchanged
+// (profiles/r05t_near_ab.log; an acquire load there cost 30-50 %: each wave
+// waits for its L1 invalidate)
+#ifndef OF2D_SN_NEAR
+#define OF2D_SN_NEAR 1
 #endif
 #ifndef OF2D_SN_RING3
 #define OF2D_SN_RING3 2
@@ -694,6 +710,35 @@ void seqnorm_tables(unsigned N, int dimx, int P, unsigned nt, SnJobs J) {
                 const float t0 = ws.tot[2 * src], t1 = ws.tot[2 * src + 1];
                 double r = (src == n && t1 > 0.0f && t0 > 0.0f) ? (double)t0 / t1 : 1.0;
                 r = r < 0.25 ? 0.25 : (r > 4.0 ? 4.0 : r);
+#if OF2D_SN_NEAR
+                if (src == n) {
+                    const double q12 = ws.Pp[(size_t)n * (nt + 1) + nt];
+#pragma unroll
+                    for (int k = 0; k < 3; k++) {
+                        const double *qp = J.nq[i][k];
+                        if (!qp || !(q12 > 0.0) || J.t0 + i < 3 * (k + 1)) break;
+                        const unsigned want = J.epoch + (unsigned)(J.t0 + i - 3 * (k + 1)) + 1u;
+                        // relaxed device-scope loads (no acquire: its cache
+                        // invalidation would cost every wave beside this one);
+                        // a total older than its stamp only predicts worse
+                        if (__hip_atomic_load(J.ns[i][k], __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT) != want)
+                            continue;
+                        const double qk = __longlong_as_double(__hip_atomic_load(
+                            reinterpret_cast<const long long *>(qp + (size_t)n * (nt + 1) + nt),
+                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+                        if (qk > 0.0 && qk < INFINITY) {
+                            // Q(t) = Qk (Qk / Q12)^(d / (12 - d)), d = 3 (k + 1)
+                            const float e = 12.0f / (float)(12 - 3 * (k + 1));
+                            const float lr = __builtin_amdgcn_logf((float)(qk / q12));
+                            float rf = __builtin_amdgcn_exp2f(e * lr);
+                            rf = rf < 0.0625f ? 0.0625f : (rf > 16.0f ? 16.0f : rf);
+                            r = rf;
+                        }
+                        break;
+                    }
+                }
+#endif
                 h = cand_window((double)pr[b] * r * (1.0 - kSnWin),
                                 (double)pr[b + 1] * r / (1.0 - kSnWin));
             }
@@ -849,6 +894,9 @@ __global__ __launch_bounds__(kSnScan) void seqnorm_check_scan(unsigned nt, unsig
             ws.cnt[1 + n] = !ok ? 0u : (q < 1.25 && q > 0.8) ? 2u : (q < 2.5 && q > 0.4) ? 1u : 3u;
         }
         for (int n = 0; n < 2; n++) ws.Pp[(size_t)n * (nt + 1) + nt] = total[n];
+        // the totals' iteration for a later group's pass (OF2D_SN_NEAR)
+        __hip_atomic_store(ws.stamp, J.epoch + (unsigned)(J.t0 + (int)blockIdx.y) + 1u,
+                           __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 __global__ __launch_bounds__(kSnChk) void seqnorm_check(unsigned nt, SnJobs J) {
@@ -1441,6 +1489,7 @@ SnWs carve(void *ws, unsigned nt) {
     w.bs = w.tot64 + 2;
     w.dr = reinterpret_cast<float *>(w.bs + 2 * (size_t)((nt + 1 + kSnChk - 1) / kSnChk));
     w.miss = reinterpret_cast<unsigned *>(w.dr + 2 * (size_t)(nt + 1));
+    w.stamp = w.miss + 2;  // inside the allocation's slack
     return w;
 }
 unsigned check_geometry(int dimx, int dimy, int P) {
@@ -1468,6 +1517,17 @@ SnJobs jobs_of(const SeqnormBatch &B, unsigned nt) {
     J.t0 = B.t0;
     J.tlo = B.tile_lo;
     J.thi = B.tile_hi;
+    J.epoch = B.epoch;
+    for (int i = 0; i < B.K; i++)
+        for (int k = 0; k < 3; k++) {
+            J.nq[i][k] = nullptr;
+            J.ns[i][k] = nullptr;
+            if (B.near[i][k]) {
+                const SnWs w = carve(B.near[i][k], nt);
+                J.nq[i][k] = w.Pp;
+                J.ns[i][k] = w.stamp;
+            }
+        }
     return J;
 }
 }  // namespace
