@@ -808,6 +808,16 @@ constexpr int kSnChk = 256;  // tiles per block of the check
 // resolved few tiles was tried in round 4: one overshooting trend scaling of
 // a profile then cost a walk thousands of resolves; the check's drift-
 // corrected fp64 prefix predicts well, so it runs for every call.)
+// without a usable profile (a loop's first four groups) the float sum is taken
+// to lie in [P lo, P' 17/16] of the fp64 prefix P: lo = 1/2 (two candidates,
+// mostly) instead of 1/16 (four) leaves the refill half the increments; the
+// 4096^2 loops' float sums stay within 5 % of P (a grid whose sum drifts
+// further only costs the walk term-level steps in those groups): fresh texture
+// 136-137 -> 131-132 us per iteration (profiles/r05aa_wide_lo_ab.log)
+#ifndef OF2D_SN_WIDE_LO
+#define OF2D_SN_WIDE_LO 0.5
+#endif
+constexpr double kSnWideLo = OF2D_SN_WIDE_LO;
 constexpr unsigned kSnMissMax = 256;  // raw segments of a walk whose profile still predicts
 __device__ __forceinline__ double sn_drift(const SnWs &ws, unsigned nt, int src, unsigned b) {
     const double f = ws.prof[(size_t)src * (nt + 1) + b], q = ws.Pp[(size_t)src * (nt + 1) + b];
@@ -945,7 +955,7 @@ __global__ __launch_bounds__(kSnChk) void seqnorm_check(unsigned nt, SnJobs J) {
             const double wd = pq == 2 ? 1.0 / 64 : (pq == 1 ? 1.0 / 32 : 1.0 / 16);
             const unsigned want =
                 pq ? cand_window(Pb[n] * d0[n] * (1.0 - wd), (Pb[n] + a[n]) * d1[n] * (1.0 + wd))
-                   : cand_window(Pb[n] * (1.0 / 16), (Pb[n] + a[n]) * (1.0 + 1.0 / 16));
+                   : cand_window(Pb[n] * kSnWideLo, (Pb[n] + a[n]) * (1.0 + 1.0 / 16));
             const int wl = hdr_elo(want), wn = hdr_nc(want), hl = hdr_elo(h[n]), hn = hdr_nc(h[n]);
             unsigned hh = h[n];
             // (a header the pass left pending, its window wider than two
