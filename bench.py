@@ -34,10 +34,13 @@ run.  The timed region is exactly K loops of 1000 iterations, each followed
 by the read-back of its Logger sums (one host synchronisation per loop, as the
 reference returns to its caller after every loop).
 
-After the timed region (N = 1, rank 0) the JSON line's `default_semantics`
-object records the default convergence-on loop at 4096^2 — the reference's
-Logger and break, not part of `value`: iterations executed against the
-reference fixtures' 102 / 397, the motion's match, us per iteration.
+After the timed region (N = 1 on config 2's grid, rank 0) the JSON line's
+`default_semantics` object records the default convergence-on loop at 4096^2 —
+the reference's Logger and break, not part of `value`: iterations executed
+against the reference fixtures' 102 / 397, the motion's match, us per
+iteration (or the error it raised).  With row slabs whose triples split
+(N > 1, or --rccl --self-halo), `config.halo_timing` holds the halo's cost per
+launch for rank 0, a middle rank and every rank, sampled with HIP events.
 
 Inputs are a synthetic procedural texture pair generated per slab.  For N > 1
 launch with torch.distributed.run (one process per GPU); torch.distributed
@@ -102,6 +105,11 @@ def parse_args(argv=None):
                          "timed region")
     ap.add_argument("--rccl", action="store_true",
                     help="N = 1: run the Logger all-reduces through a one-rank RCCL communicator")
+    ap.add_argument("--self-halo", action="store_true",
+                    help="with --rccl at N = 1: the one-rank communicator also sends its "
+                         "boundary j-lines to itself between split interior / edge launches "
+                         "(slab options rccl_self_halo, split): the N > 1 halo path and its "
+                         "timing fields on one GPU")
     return ap.parse_args(argv)
 
 
@@ -220,6 +228,20 @@ def default_semantics(reps: int = 2) -> dict:
     return out
 
 
+def halo_summary(per_rank: list) -> dict | None:
+    """The halo's cost per split triple launch (slab.last_run_halo_us averaged
+    over the timed runs), for rank 0, a middle rank and every rank: how long
+    the solver stream waited for the previous launch's edge launches (stall),
+    the exchange on the halo stream, the two edge launches."""
+    if not per_rank or not any(r and r.get("sampled") for r in per_rank):
+        return None
+    mid = len(per_rank) // 2
+    return {"sampled_launches_per_run": max(r.get("sampled", 0) for r in per_rank),
+            "unit": "us per sampled split triple",
+            "rank0": per_rank[0], "rank_mid": dict(per_rank[mid], rank=mid),
+            "per_rank": per_rank}
+
+
 def load_traffic(dimx: int, rows: int, gradients: str = "field"):
     """PMC traffic per launch from the committed profile, only for the grid it
     was measured on (it is not measured inside this run)."""
@@ -236,7 +258,7 @@ def load_traffic(dimx: int, rows: int, gradients: str = "field"):
 def make_record(*, world, wl, steps, warmup, elapsed, gpu_ms, avg_us, iso_us, px_rank, info,
                 loop_us=None, avg_n=0,
                 traffic, cpu, rows_per_rank, iters_per_step=1, gradients="image",
-                semantics=None):
+                semantics=None, halo=None):
     """The JSON line (bench.py contract + roofline + cpu_baseline)."""
     dimx, dimy = wl["dimx"], wl["dimy"]
     total_px = dimx * dimy
@@ -272,6 +294,7 @@ def make_record(*, world, wl, steps, warmup, elapsed, gpu_ms, avg_us, iso_us, px
             "halo_bytes_per_exchange": (2 * info.get("halo_lines", 0) * dimx * 8
                                         if world > 1 else 0),
             "interior_edge_split": bool(info.get("split", 0)),
+            "halo_timing": halo,
             "gpu_ms_rank0": round(gpu_ms, 3),
             "wall_over_gpu_rank0": round(elapsed * 1000.0 / gpu_ms, 4) if gpu_ms > 0 else None,
             # the path's own algorithmic traffic (28 B/px per fused launch) per GPU
@@ -354,6 +377,12 @@ def main():
     del ref, mov
     solver.set_option("hs_gradients_from_image",
                       {"auto": -1, "image": 1, "field": 0}[args.gradients])
+    if args.self_halo:
+        if not (world == 1 and uid is not None):
+            print("bench.py: --self-halo needs --rccl at N = 1", file=sys.stderr)
+            sys.exit(2)
+        solver.set_option("rccl_self_halo", 1)
+        solver.set_option("split", 1)
     ips = args.iters_per_step
     solver.reserve(ips)
     info = solver.info()
@@ -375,6 +404,7 @@ def main():
     gpu_ms = 0.0
     done = 0
     tri_us, tri_n = 0.0, 0
+    halo = {"stall_us": 0.0, "exchange_us": 0.0, "edges_us": 0.0, "sampled": 0}
     t0 = time.perf_counter()
     for _ in range(args.steps):
         done += solver.run(ips, fixed_iters=True)  # returns after the stream is drained
@@ -382,6 +412,10 @@ def main():
         us, n = solver.last_run_kernel_us()
         tri_us += us * n
         tri_n += n
+        h = solver.last_run_halo_us()
+        for k in ("stall_us", "exchange_us", "edges_us"):
+            halo[k] += h[k] / args.steps
+        halo["sampled"] = max(halo["sampled"], h["sampled"])
     t1 = time.perf_counter()
     barrier()
     elapsed = t1 - t0
@@ -391,6 +425,12 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     assert done == args.steps * ips
+    halo = {"rank": rank, **{k: round(v, 3) if isinstance(v, float) else v
+                             for k, v in halo.items()}}
+    halos = [halo]
+    if dist is not None:
+        halos = [None] * world
+        dist.all_gather_object(halos, halo)
 
     # dominant kernel: its own average duration per launch inside the timed
     # loops, from the HIP events the solver records on its stream around each
@@ -407,8 +447,14 @@ def main():
     if rank == 0:
         cpu = None
         semantics = None
-        if world == 1 and not args.no_default_semantics:
-            semantics = default_semantics()
+        # the convergence-on loop at config 2's grid, only when that is the
+        # timed grid; a failure there is recorded and never costs the line
+        if (world == 1 and not args.no_default_semantics
+                and (dimx, dimy) == (4096, 4096)):
+            try:
+                semantics = default_semantics()
+            except Exception as e:  # noqa: BLE001
+                semantics = {"error": f"{type(e).__name__}: {e}"}
         if world == 1 and not args.no_cpu_baseline:
             # the same grid; iterations scaled to keep the sample at ~15-30 s
             cpu_it = max(1, int(args.cpu_iters * (4096.0 / dimx) ** 2))
@@ -418,7 +464,8 @@ def main():
                           loop_us=loop_us, avg_n=tri_n,
                           px_rank=px_rank, info=info, traffic=load_traffic(dimx, rows, gradients),
                           cpu=cpu, rows_per_rank=rows, iters_per_step=ips,
-                          gradients=gradients, semantics=semantics)
+                          gradients=gradients, semantics=semantics,
+                          halo=halo_summary(halos))
         print(json.dumps(rec), flush=True)
     solver.close()
     if dist is not None:

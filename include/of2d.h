@@ -169,11 +169,13 @@ int of2d_slab_get_motion(of2d_slab *s, double *out);
  * launched on.  The launches read the zeroed start buffer and write scratch:
  * the last run's motion (of2d_slab_get_motion) is left intact. */
 int of2d_slab_time_kernel(of2d_slab *s, int nlaunch, double *avg_us);
-/* slab facts for reports: info[0..9] = {nranks, ranks of the RCCL
+/* slab facts for reports: info[0..10] = {nranks, ranks of the RCCL
  * communicator (ncclCommCount; 0 without one), in-process group (0/1),
  * row_begin, row_end, dimx, pitch (elements), halo j-lines exchanged per fused
- * launch, interior/edge split (0/1), triple kernel derives dI from Iaux (0/1)};
- * returns the number of entries written */
+ * launch, interior/edge split (0/1), triple kernel derives dI from Iaux (0/1),
+ * Logger of a convergence-on run (1: the reference's float running sums,
+ * 0: fp64 sums — "logger_fp64" resolved)}; returns the number of entries
+ * written */
 int of2d_slab_info(const of2d_slab *s, int *info, int n);
 /* the Logger errors of the last of2d_slab_run's iterations (the global ones:
  * the same on every rank), up to n into out; returns how many there are */
@@ -185,6 +187,15 @@ int of2d_slab_last_run_ms(const of2d_slab *s, double *ms);
  * first 64 chunks on the solver's stream (halo exchange included for N > 1),
  * and the number of launches that average covers */
 int of2d_slab_last_run_kernel_us(const of2d_slab *s, double *avg_us, int *nlaunch);
+/* the halo's cost inside the last run, sampled with HIP events on the first 8
+ * split triples (interior launch beside the exchange and two edge launches):
+ * us3[0] the solver stream's wait for the previous launch's edges before the
+ * interior may start (the stall the halo puts on the critical stream),
+ * us3[1] the exchange on the halo stream (ncclGroupStart .. ncclGroupEnd of
+ * the sends / receives, or the in-process copies, including the wait for the
+ * neighbours), us3[2] the two edge launches; averages per sampled launch, and
+ * *nsampled the launches sampled (0 when the run had no split triples) */
+int of2d_slab_last_run_halo_us(const of2d_slab *s, double *us3, int *nsampled);
 /* options (no reference counterpart):
  *   "hs_gradients_from_image" (-1 auto = default, 0, 1): the triple kernel
  *   derives dI from Iaux in the kernel (24 B/px per launch) instead of reading
@@ -201,8 +212,10 @@ int of2d_slab_last_run_kernel_us(const of2d_slab *s, double *avg_us, int *nlaunc
  *   "split" (-1 auto = default, 0, 1): triples as an interior launch beside
  *   the halo exchange and two edge launches (auto: when a neighbour is on
  *   another device or behind RCCL), never, or whenever the slab has >= 48
- *   j-lines (tests of the multi-device launch order on one device);
- *   bit-identical either way
+ *   j-lines AND a halo to exchange — two or more ranks, or a one-rank
+ *   communicator with "rccl_self_halo" (tests of the multi-device launch
+ *   order on one device; a one-rank slab without either stays unsplit
+ *   whatever is set); bit-identical either way
  *   "rccl_self_halo" (0 = default, 1; a one-rank RCCL communicator only):
  *   every halo exchange also sends the slab's boundary j-lines to rank 0
  *   itself (ncclSend / ncclRecv in a group, into a scratch buffer that is never

@@ -64,6 +64,8 @@ SIGNATURES = {
     "of2d_slab_set_option": (C.c_int, [C.c_void_p, C.c_char_p, C.c_double]),
     "of2d_slab_last_run_kernel_us": (C.c_int, [C.c_void_p, C.POINTER(C.c_double),
                                                 C.POINTER(C.c_int)]),
+    "of2d_slab_last_run_halo_us": (C.c_int, [C.c_void_p, C.POINTER(C.c_double),
+                                              C.POINTER(C.c_int)]),
     "of2d_slab_last_errors": (C.c_int, [C.c_void_p, _f32p, C.c_int]),
     "of2d_slab_destroy": (C.c_int, [C.c_void_p]),
     "of2d_slab_last_error": (C.c_char_p, [C.c_void_p]),

@@ -65,6 +65,14 @@ constexpr int kCr = OF2D_DEMONS_CR;
 #ifndef OF2D_DEMONS_BW
 #define OF2D_DEMONS_BW 6
 #endif
+// fused kernel's output tile: OF2D_DEMONS_TX columns (threads across) x
+// OF2D_DEMONS_TY thread rows of kCr j-lines (A/B builds: 128 x 4, 64 x 8)
+#ifndef OF2D_DEMONS_TX
+#define OF2D_DEMONS_TX 64
+#endif
+#ifndef OF2D_DEMONS_TY
+#define OF2D_DEMONS_TY 4
+#endif
 typedef float v2f __attribute__((ext_vector_type(2)));
 
 // warp2d values of Imov at B pixels (a[q], b[q]) with motion u
@@ -341,12 +349,12 @@ __device__ __forceinline__ void conv_load_tile(float2 *tile, const float2 *__res
 // false when the weight sum is 0 (then the reference leaves the pixel as is)
 // KW > 0: kernel width known at compile time (taps unrolled, weights in
 // scalar registers); KW == 0: runtime width.
-template <int KW>
+template <int KW, int TX = kCx>
 __device__ __forceinline__ bool conv_px(const float2 *tile, const ConvArgs &a, int i, int j,
                                         int tx, int ty, int dimx, long N, float2 &out) {
     const int kw = KW > 0 ? KW : a.kw;
     const int cx = KW > 0 ? (KW - 1) / 2 : a.cx, cy = KW > 0 ? (KW - 1) / 2 : a.cy;
-    const int TW = kCx + 2 * cx;
+    const int TW = TX + 2 * cx;
     const long lin = (long)j * dimx + i;
     const bool interior = (lin - cx - (long)cy * dimx >= 0) && (lin + cx + (long)cy * dimx < N);
     float vx = 0.0f, vy = 0.0f;
@@ -397,12 +405,12 @@ __device__ __forceinline__ bool conv_rows_interior(int i, int j0, int dimx, int 
 // packed pair (PK) or as two scalars; otherwise per pixel.
 // W1: the interior weight sum (float)wfull is exactly 1 (a normalised kernel,
 // the reference's set_gaussian / set_average), so acc / wf is acc itself
-template <int KW, int R, bool PK, bool W1 = false>
+template <int KW, int R, bool PK, bool W1 = false, int TX = kCx>
 __device__ __forceinline__ void convR(const float2 *tile, const ConvArgs &a, int i, int j0,
                                       int tx, int ty0, int dimx, int dimy, long N, float2 res[R],
                                       bool has[R]) {
     if constexpr (KW > 0) {
-        constexpr int c = (KW - 1) / 2, TW = kCx + 2 * c;
+        constexpr int c = (KW - 1) / 2, TW = TX + 2 * c;
         if (conv_rows_interior<KW, R>(i, j0, dimx, dimy, N)) {
             v2f acc[R];
 #pragma unroll
@@ -441,7 +449,8 @@ __device__ __forceinline__ void convR(const float2 *tile, const ConvArgs &a, int
 #pragma unroll
     for (int k = 0; k < R; k++) {
         has[k] = false;
-        if (j0 + k < dimy) has[k] = conv_px<KW>(tile, a, i, j0 + k, tx, ty0 + k, dimx, N, res[k]);
+        if (j0 + k < dimy)
+            has[k] = conv_px<KW, TX>(tile, a, i, j0 + k, tx, ty0 + k, dimx, N, res[k]);
     }
 }
 
@@ -589,22 +598,25 @@ __global__ __launch_bounds__(256) void smooth_compose_kernel(
 // most: dimx >= 2 * 64 (launch_demons_update).
 // FAST: (float)ca.wfull == 1 and sigma_xsq a power of two whose reciprocal
 // `sxq` carries (convR W1, demons_corr SXP); otherwise `sxq` is sigma_xsq
-template <int KW, int R, bool FAST>
-__global__ __launch_bounds__(256) OF2D_DEMONS_FUSED_ATTR void demons_fused_kernel(
+// TX x (TY R) output tile: TX (64 or 128) threads across (one or two waves
+// per tile row of threads), TY thread rows of R j-lines each
+template <int KW, int R, bool FAST, int TX = kCx, int TY = kCThreadsY>
+__global__ __launch_bounds__(TX * TY) OF2D_DEMONS_FUSED_ATTR void demons_fused_kernel(
     const float *__restrict__ Iref, const float *__restrict__ Imov, const float2 *__restrict__ u,
     float2 *__restrict__ out, int dimx, int dimy, int P, float sigma_isq, float sxq,
     ConvArgs ca, int mode, unsigned *__restrict__ status, int bx0) {
     constexpr int c = (KW - 1) / 2;
-    constexpr int CY = kCThreadsY * R;
-    constexpr int CW = kCx + 2 * c, CH = CY + 2 * c;  // correction tile
-    constexpr int WW = CW + 2, WH = CH + 2;           // warped-image tile
+    constexpr int NT = TX * TY;  // threads
+    constexpr int CY = TY * R;
+    constexpr int CW = TX + 2 * c, CH = CY + 2 * c;  // correction tile
+    constexpr int WW = CW + 2, WH = CH + 2;          // warped-image tile
     __shared__ float wt[WH * WW];
     __shared__ __attribute__((aligned(16))) float2 ct[CH * CW];
-    const int x0 = ((int)blockIdx.x + bx0) * kCx, y0 = blockIdx.y * CY;
-    const int tid = threadIdx.y * 64 + threadIdx.x;
+    const int x0 = ((int)blockIdx.x + bx0) * TX, y0 = blockIdx.y * CY;
+    const int tid = threadIdx.y * TX + threadIdx.x;
     // block-uniform: the warped tile crosses an x edge (its slots past it
     // hold the wrapped pixels)
-    const bool xedge = x0 - c - 1 < 0 || x0 + kCx + c + 1 > dimx;
+    const bool xedge = x0 - c - 1 < 0 || x0 + TX + c + 1 > dimx;
     auto wrap = [&](int &x, int &y) __attribute__((always_inline)) {
         const int lo = x < 0, hi = x >= dimx;
         x += lo ? dimx : (hi ? -dimx : 0);
@@ -613,7 +625,7 @@ __global__ __launch_bounds__(256) OF2D_DEMONS_FUSED_ATTR void demons_fused_kerne
     {
         // 1. slot s <-> pixel (x0 - c - 1 + s % WW, y0 - c - 1 + s / WW)
         // (wrapped), in batches of BW slots per thread
-        constexpr int NW = (WW * WH + 255) / 256, BW = OF2D_DEMONS_BW;
+        constexpr int NW = (WW * WH + NT - 1) / NT, BW = OF2D_DEMONS_BW;
 #pragma unroll
         for (int q0 = 0; q0 < NW; q0 += BW) {
             int a[BW], b[BW];
@@ -621,7 +633,7 @@ __global__ __launch_bounds__(256) OF2D_DEMONS_FUSED_ATTR void demons_fused_kerne
             float res[BW];
 #pragma unroll
             for (int q = 0; q < BW; q++) {
-                const int s = tid + 256 * (q0 + q), r = s / WW;
+                const int s = tid + NT * (q0 + q), r = s / WW;
                 a[q] = x0 - c - 1 + (s - r * WW);
                 b[q] = y0 - c - 1 + r;
                 if (xedge) wrap(a[q], b[q]);
@@ -639,7 +651,7 @@ __global__ __launch_bounds__(256) OF2D_DEMONS_FUSED_ATTR void demons_fused_kerne
             }
 #pragma unroll
             for (int q = 0; q < BW; q++)
-                if (valid[q]) wt[tid + 256 * (q0 + q)] = in[q] ? res[q] : 0.0f;
+                if (valid[q]) wt[tid + NT * (q0 + q)] = in[q] ? res[q] : 0.0f;
         }
     }
     // 2. correction slot (r, cc) <-> pixel (x0 - c + cc, y0 - c + r), cc < CW,
@@ -650,11 +662,11 @@ __global__ __launch_bounds__(256) OF2D_DEMONS_FUSED_ATTR void demons_fused_kerne
     // the warp tile completes.
     // (unconditional loads: a slot outside the image reads element 0 and keeps
     // 0, so the loads issue back to back instead of one branch each)
-    constexpr int NC = (WW * CH + 255) / 256;
+    constexpr int NC = (WW * CH + NT - 1) / NT;
     float iref[NC];
 #pragma unroll
     for (int q = 0; q < NC; q++) {
-        const int s = tid + 256 * q, r = s / WW, cc = s - r * WW;
+        const int s = tid + NT * q, r = s / WW, cc = s - r * WW;
         int i = x0 - c + cc, j = y0 - c + r;
         if (xedge) wrap(i, j);
         const bool ok = (s < WW * CH) & (cc < CW) & ((unsigned)j < (unsigned)dimy);
@@ -672,7 +684,7 @@ __global__ __launch_bounds__(256) OF2D_DEMONS_FUSED_ATTR void demons_fused_kerne
         if (tin) {
 #pragma unroll
             for (int q = 0; q < NC; q++) {
-                const int s = tid + 256 * q, r = s / WW, cc = s - r * WW;
+                const int s = tid + NT * q, r = s / WW, cc = s - r * WW;
                 if (s < WW * CH && cc < CW) {
                     const float *w = wt + (r + 1) * WW + (cc + 1);
                     const float gx = (w[1] - w[-1]) / 2.0f, gy = (w[WW] - w[-WW]) / 2.0f;
@@ -688,7 +700,7 @@ __global__ __launch_bounds__(256) OF2D_DEMONS_FUSED_ATTR void demons_fused_kerne
         } else {
 #pragma unroll
         for (int q = 0; q < NC; q++) {
-            const int s = tid + 256 * q, r = s / WW, cc = s - r * WW;
+            const int s = tid + NT * q, r = s / WW, cc = s - r * WW;
             if (s < WW * CH && cc < CW) {
                 int i = x0 - c + cc, j = y0 - c + r;
                 if (xedge) wrap(i, j);
@@ -730,7 +742,7 @@ __global__ __launch_bounds__(256) OF2D_DEMONS_FUSED_ATTR void demons_fused_kerne
 #pragma unroll
         for (int k = 0; k < R; k++) has[k] = false;
     } else {
-        convR<KW, R, true, FAST>(ct, ca, i, y0 + r0, threadIdx.x, r0, dimx, dimy, N, sm, has);
+        convR<KW, R, true, FAST, TX>(ct, ca, i, y0 + r0, threadIdx.x, r0, dimx, dimy, N, sm, has);
     }
     float2 cv[R];
 #pragma unroll
@@ -868,7 +880,6 @@ void launch_demons_update(const float *Iref, const float *Imov, const float2 *u,
         smooth_compose_tiles(corr, u, out, dimx, dimy, P, a, mode, gx, gx, gx, st);
         return;
     }
-    const dim3 g(gx, conv_grid(dimx, dimy).y);
     if (OF2D_DEMONS_WARP1) {  // corr is free on this path: the warped plane
         float *iw = reinterpret_cast<float *>(corr);
         launch_warp(Imov, u, iw, dimx, dimy, P, st);
@@ -876,17 +887,25 @@ void launch_demons_update(const float *Iref, const float *Imov, const float2 *u,
     }
     float rsx = 0.0f;
     const bool fast = (float)wfull == 1.0f && pow2_reciprocal(sigma_xsq, &rsx);
+    constexpr int TX = OF2D_DEMONS_TX, TY = OF2D_DEMONS_TY;
+    // one wrap at most per tile: the tile narrower than half the image
+    if (dimx < 2 * TX) {
+        launch_demons_force(Iref, Imov, u, corr, dimx, dimy, P, sigma_isq, sigma_xsq, status, st);
+        smooth_compose_tiles(corr, u, out, dimx, dimy, P, a, mode, gx, gx, gx, st);
+        return;
+    }
+    const dim3 g((dimx + TX - 1) / TX, (dimy + TY * kCr - 1) / (TY * kCr));
     auto go = [&](auto kern) {
-        hipLaunchKernelGGL(kern, g, dim3(64, kCThreadsY), 0, st, Iref, Imov, u, out, dimx, dimy, P,
+        hipLaunchKernelGGL(kern, g, dim3(TX, TY), 0, st, Iref, Imov, u, out, dimx, dimy, P,
                            sigma_isq, fast ? rsx : sigma_xsq, a, mode, status, 0);
     };
     switch (kw * 2 + fast) {
-        case 6: go(demons_fused_kernel<3, kCr, false>); break;
-        case 7: go(demons_fused_kernel<3, kCr, true>); break;
-        case 10: go(demons_fused_kernel<5, kCr, false>); break;
-        case 11: go(demons_fused_kernel<5, kCr, true>); break;
-        case 15: go(demons_fused_kernel<7, kCr, true>); break;
-        default: go(demons_fused_kernel<7, kCr, false>); break;
+        case 6: go(demons_fused_kernel<3, kCr, false, TX, TY>); break;
+        case 7: go(demons_fused_kernel<3, kCr, true, TX, TY>); break;
+        case 10: go(demons_fused_kernel<5, kCr, false, TX, TY>); break;
+        case 11: go(demons_fused_kernel<5, kCr, true, TX, TY>); break;
+        case 15: go(demons_fused_kernel<7, kCr, true, TX, TY>); break;
+        default: go(demons_fused_kernel<7, kCr, false, TX, TY>); break;
     }
     OF2D_HIP(hipGetLastError());
 }

@@ -129,6 +129,16 @@ struct of2d_slab {
     int tri_pairs = 0, tri_launches = 0;
     double tri_us = 0.0;  // average per triple launch of the last run
     int tri_n = 0;        // triple launches that average covers
+    // the halo's cost, sampled on the first kHaloTimed split triples of a run
+    // (five events each, so that the other launches keep no extra packets):
+    // st before / after its wait on the previous edge launches (the stall the
+    // halo puts on the interior), comm_st before / after the exchange and after
+    // the two edge launches
+    static constexpr int kHaloTimed = 8;
+    hipEvent_t ev_halo[5 * kHaloTimed] = {};
+    int halo_n = 0;  // sampled in this run so far
+    double halo_us[3] = {};  // last run: stall, exchange, edges (us per sampled launch)
+    int halo_samples = 0;
 };
 
 // The ranks of one grid inside ONE process, one host thread per rank: halos
@@ -727,6 +737,7 @@ static int slab_create(of2d_slab **out, int dimx, int dimy, float alpha, int ran
         OF2D_HIP(hipEventCreate(&s->ev0));
         OF2D_HIP(hipEventCreate(&s->ev1));
         for (auto &e : s->ev_tri) OF2D_HIP(hipEventCreate(&e));
+        for (auto &e : s->ev_halo) OF2D_HIP(hipEventCreate(&e));
         OF2D_HIP(hipStreamCreateWithFlags(&s->comm_st, hipStreamNonBlocking));
         OF2D_HIP(hipEventCreateWithFlags(&s->ev_int, hipEventDisableTiming));
         OF2D_HIP(hipEventCreateWithFlags(&s->ev_edge, hipEventDisableTiming));
@@ -958,13 +969,20 @@ int of2d_slab_run(of2d_slab *s, int niter, int fixed_iters, int *iters_done) {
         auto fused = [&](int K, int in, int out, double *p1, double *p2, double *p3) {
             float2 *uin = s->u[in].p;
             if (K == 3 && G.split) {
+                hipEvent_t *eh = s->halo_n < of2d_slab::kHaloTimed
+                                     ? s->ev_halo + 5 * s->halo_n++ : nullptr;
                 OF2D_HIP(hipStreamWaitEvent(s->comm_st, s->ev_int, 0));
+                if (eh) OF2D_HIP(hipEventRecord(eh[0], s->st));
                 join_st();
+                if (eh) OF2D_HIP(hipEventRecord(eh[1], s->st));
                 win3(s->st, in, out, G.E, s->nrows - G.E, G.ri, 0, p1, p2, p3);
                 mark_st();
+                if (eh) OF2D_HIP(hipEventRecord(eh[2], s->comm_st));
                 halo_exchange(s, uin, 3, s->comm_st);
+                if (eh) OF2D_HIP(hipEventRecord(eh[3], s->comm_st));
                 win3(s->comm_st, in, out, 0, G.E, G.re, G.bi, p1, p2, p3);
                 win3(s->comm_st, in, out, s->nrows - G.E, s->nrows, G.re, G.bi + 1, p1, p2, p3);
+                if (eh) OF2D_HIP(hipEventRecord(eh[4], s->comm_st));
                 OF2D_HIP(hipEventRecord(s->ev_edge, s->comm_st));
                 return;
             }
@@ -1004,6 +1022,7 @@ int of2d_slab_run(of2d_slab *s, int niter, int fixed_iters, int *iters_done) {
         s->errs.clear();
         s->tri_pairs = 0;
         s->tri_launches = 0;
+        s->halo_n = 0;
         OF2D_HIP(hipEventRecord(s->ev0, s->st));
         mark_st();  // comm_st starts after everything enqueued so far
         OF2D_HIP(hipStreamWaitEvent(s->comm_st, s->ev_int, 0));
@@ -1138,6 +1157,17 @@ int of2d_slab_run(of2d_slab *s, int niter, int fixed_iters, int *iters_done) {
         }
         s->tri_n = s->tri_launches;
         s->tri_us = s->tri_launches ? 1000.0 * tri_ms / s->tri_launches : 0.0;
+        for (double &h : s->halo_us) h = 0.0;
+        for (int p = 0; p < s->halo_n; p++) {
+            const hipEvent_t *eh = s->ev_halo + 5 * p;
+            const int from[3] = {0, 2, 3}, to[3] = {1, 3, 4};
+            for (int q = 0; q < 3; q++) {
+                float m = 0.0f;
+                OF2D_HIP(hipEventElapsedTime(&m, eh[from[q]], eh[to[q]]));
+                s->halo_us[q] += 1000.0 * m / s->halo_n;
+            }
+        }
+        s->halo_samples = s->halo_n;
         if (iters_done) *iters_done = done;
     });
 }
@@ -1196,7 +1226,8 @@ int of2d_slab_info(const of2d_slab *s, int *info, int n) {
     if (s->comm && ncclCommCount(s->comm, &rccl) != ncclSuccess) return -OF2D_ERR_DEVICE;
     const int halo_lines = s->nranks > 1 ? 3 : 0;
     const int v[] = {s->nranks, rccl, s->grp ? 1 : 0, s->rb, s->re, s->dimx, s->P,
-                     halo_lines, slab_geometry(s).split ? 1 : 0, use_gi(s) ? 1 : 0};
+                     halo_lines, slab_geometry(s).split ? 1 : 0, use_gi(s) ? 1 : 0,
+                     exact_logger(s) ? 1 : 0};
     const int k = std::min(n, (int)(sizeof v / sizeof v[0]));
     for (int i = 0; i < k; i++) info[i] = v[i];
     return k;
@@ -1232,6 +1263,13 @@ int of2d_slab_last_run_kernel_us(const of2d_slab *s, double *avg_us, int *nlaunc
     if (!s || !avg_us || !nlaunch) return OF2D_ERR_INVALID_ARGUMENT;
     *avg_us = s->tri_us;
     *nlaunch = s->tri_n;
+    return OF2D_OK;
+}
+
+int of2d_slab_last_run_halo_us(const of2d_slab *s, double *us3, int *nsampled) {
+    if (!s || !us3 || !nsampled) return OF2D_ERR_INVALID_ARGUMENT;
+    for (int q = 0; q < 3; q++) us3[q] = s->halo_us[q];
+    *nsampled = s->halo_samples;
     return OF2D_OK;
 }
 
@@ -1278,6 +1316,8 @@ int of2d_slab_destroy(of2d_slab *s) {
     if (s->ev0) (void)hipEventDestroy(s->ev0);
     if (s->ev1) (void)hipEventDestroy(s->ev1);
     for (auto &e : s->ev_tri)
+        if (e) (void)hipEventDestroy(e);
+    for (auto &e : s->ev_halo)
         if (e) (void)hipEventDestroy(e);
     if (s->ev_int) (void)hipEventDestroy(s->ev_int);
     if (s->ev_edge) (void)hipEventDestroy(s->ev_edge);

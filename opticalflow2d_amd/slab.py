@@ -115,13 +115,15 @@ class SlabSolver:
     def info(self) -> dict:
         """nranks, the RCCL communicator's rank count (ncclCommCount; 0 without
         one), rows, pitch, halo lines per fused launch, interior/edge split,
-        whether the triple kernel derives dI from Iaux."""
-        buf = (C.c_int * 10)()
-        n = _lib.lib().of2d_slab_info(self._h, buf, 10)
+        whether the triple kernel derives dI from Iaux, and the Logger a
+        convergence-on run takes (1: the reference's float running sums, 0:
+        fp64 sums)."""
+        buf = (C.c_int * 11)()
+        n = _lib.lib().of2d_slab_info(self._h, buf, 11)
         if n < 0:
             self._chk(-n)
         keys = ["nranks", "rccl_ranks", "in_process_group", "row_begin", "row_end", "dimx",
-                "pitch", "halo_lines", "split", "gradients_from_image"]
+                "pitch", "halo_lines", "split", "gradients_from_image", "logger_reference"]
         return {k: int(buf[i]) for i, k in enumerate(keys[:n])}
 
     def set_option(self, key: str, value: float) -> None:
@@ -152,6 +154,17 @@ class SlabSolver:
         n = C.c_int(0)
         self._chk(_lib.lib().of2d_slab_last_run_kernel_us(self._h, C.byref(us), C.byref(n)))
         return us.value, n.value
+
+    def last_run_halo_us(self) -> dict:
+        """The halo's cost inside the last run, sampled on its first split
+        triples (include/of2d.h of2d_slab_last_run_halo_us): the solver stream's
+        stall on the previous edge launches, the exchange, the edge launches
+        (us per sampled launch), and the launches sampled."""
+        us = (C.c_double * 3)()
+        n = C.c_int(0)
+        self._chk(_lib.lib().of2d_slab_last_run_halo_us(self._h, us, C.byref(n)))
+        return {"stall_us": us[0], "exchange_us": us[1], "edges_us": us[2],
+                "sampled": n.value}
 
     def errors(self) -> np.ndarray:
         """The Logger errors of the last run's iterations (float32; global)."""

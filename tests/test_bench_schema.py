@@ -71,6 +71,34 @@ def test_record_schema(world):
     assert rf["traffic"] is None and rf["traffic_source"] is None
     assert rf["kernel"].startswith("of2d::hs::jacobi3_kernel")
     assert r["default_semantics"] is None  # measured on a GPU only, outside `value`
+    assert c["halo_timing"] is None  # given by make_record's caller (GPU runs)
+
+
+def test_halo_summary():
+    """config.halo_timing for N > 1: rank 0, a middle rank, every rank."""
+    per = [{"rank": r, "stall_us": 1.0 + r, "exchange_us": 10.0, "edges_us": 5.0, "sampled": 8}
+           for r in range(8)]
+    h = bench.halo_summary(per)
+    assert h["sampled_launches_per_run"] == 8 and h["per_rank"] == per
+    assert h["rank0"]["rank"] == 0 and h["rank_mid"]["rank"] == 4
+    assert h["rank_mid"]["stall_us"] == 5.0
+    # unsplit runs (N = 1 without --self-halo) sample nothing
+    assert bench.halo_summary([{"rank": 0, "stall_us": 0.0, "exchange_us": 0.0,
+                                "edges_us": 0.0, "sampled": 0}]) is None
+    r = _record(2, 16384, 16384, 8192)
+    rec = bench.make_record(**{**dict(world=2, wl=bench.workload(bench.parse_args([]), 2),
+                                      steps=20, warmup=5, elapsed=0.6, gpu_ms=580.0,
+                                      avg_us=87.0, iso_us=85.0, px_rank=16384 * 8192,
+                                      info={"halo_lines": 3, "split": 1}, traffic=None,
+                                      cpu=None, rows_per_rank=8192, iters_per_step=1000)},
+                            halo=bench.halo_summary(per[:2]))
+    assert rec["config"]["halo_timing"]["rank_mid"]["rank"] == 1
+    assert r["config"]["interior_edge_split"] is True
+    json.loads(json.dumps(rec))
+
+
+def test_self_halo_flag():
+    assert bench.parse_args(["--rccl", "--self-halo"]).self_halo
 
 
 def test_default_semantics_flag():

@@ -42,6 +42,8 @@ ref, mov = S.procedural_pair(n, 0, n)
 out = []
 for uid in (None, rccl_unique_id()):
     s = SlabSolver(n, n, 0.1, 0, 1, device=0, unique_id=uid)
+    # a one-rank communicator keeps the reference's Logger (logger_fp64 auto)
+    assert s.info()["logger_reference"] == 1, s.info()
     s.set_images(ref, mov)
     done = s.run(1000, fixed_iters=False)
     out.append((done, s.motion()))
@@ -120,7 +122,8 @@ def test_bench_under_torch_distributed_run():
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
            os.path.join(ROOT, "bench.py"), "--gpus", "1", "--steps", "99", "--warmup", "3",
-           "--size", "1024", "--no-cpu-baseline", "--rccl", "--timing-launches", "5"]
+           "--size", "1024", "--no-cpu-baseline", "--rccl", "--self-halo",
+           "--timing-launches", "5"]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=ROOT)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
@@ -128,3 +131,11 @@ def test_bench_under_torch_distributed_run():
     res = json.loads(lines[0])
     assert res["n_gpus"] == 1 and res["steps"] == 99 and res["value"] > 0
     assert res["roofline"]["avg_launch_us"] > 0
+    # the self-halo's split triples: the halo timing of the N > 1 line
+    assert res["config"]["interior_edge_split"] is True
+    h = res["config"]["halo_timing"]
+    assert h["sampled_launches_per_run"] == 8 and h["rank0"]["rank"] == 0
+    assert h["rank0"]["exchange_us"] > 0 and h["rank0"]["edges_us"] > 0
+    assert h["rank0"]["stall_us"] >= 0
+    # the grid is not config 2's: no convergence-on measurement
+    assert res["default_semantics"] is None

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Build libof2d.so with extra compile flags for one source into tools/ab/<name>/
+# Build libof2d.so with extra compile flags for one source into tools/abx/<name>/ (travels to the GPU box; tools/ab/ does not)
 # (an A/B variant; the in-tree objects for everything else):
 #   [REV=<git rev>] tools/build_variant.sh <name> <source under csrc> <flags...>
 # (REV: that revision's text of the source, compiled beside today's headers)
@@ -8,7 +8,7 @@ cd "$(dirname "$0")/.."
 C=opticalflow2d_amd/csrc
 name=$1 src=$2; shift 2
 make -C $C -j8 > /dev/null
-D=tools/ab/$name
+D=tools/abx/$name
 mkdir -p $D
 b=$(basename "$src" .hip); b=$(basename "$b" .cpp)
 SRC=$C/$src

@@ -10,7 +10,11 @@
 #        configs (bench_configs.py), ranks (ngpus timings), ranksprof (their
 #        kernel trace, 8 ranks), texprof / freshprof (kernel trace of the
 #        texture pair's warm / fresh loops), snbench /
-#        snprof (the Logger-norm harness: stage timings / kernel stats)
+#        snprof (the Logger-norm harness: stage timings / kernel stats),
+#        mtprobe / mtprobeprof (tools/mt_launch_probe: the slab group's
+#        multi-thread launch pattern without the library, plain / under the
+#        kernel trace; q16: 16 hardware queues, one per stream; serial: the eight
+#        streams fed from one host thread)
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 R=$PWD
@@ -39,13 +43,17 @@ for s in "$@"; do
         convprof) run convprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/$O/${tag}_convprof" -o k -- python3 -u "$R/tools/time_convergence.py" 4096 1 ;;
         configs) run configs 900 python -u bench_configs.py ;;
         ranks) run ranks 600 python -u tools/time_ranks.py ;;
-        ranksprof) run ranksprof 600 rocprofv3 --kernel-trace --output-format csv -d "$R/$O/${tag}_ranksprof" -o k -- python3 -u "$R/tools/time_ranks.py" 4096 1 fixed,conv 8 ;;
+        ranksprof) OF2D_MAPS_DUMP="$R/$O/${tag}_ranksprof_maps.txt" run ranksprof 600 rocprofv3 --kernel-trace --output-format csv -d "$R/$O/${tag}_ranksprof" -o k -- python3 -u "$R/tools/time_ranks.py" 4096 1 fixed,conv 8 ;;
         texprof) OF2D_CONV_CASE=texture OF2D_CONV_ONLY=1 run texprof 300 rocprofv3 --kernel-trace --output-format csv -d "$R/$O/${tag}_texprof" -o k -- python3 -u "$R/tools/time_convergence.py" 4096 1 ;;
         freshprof) OF2D_CONV_FRESH=1 OF2D_CONV_CASE=texture OF2D_CONV_ONLY=1 run freshprof 300 rocprofv3 --kernel-trace --output-format csv -d "$R/$O/${tag}_freshprof" -o k -- python3 -u "$R/tools/time_convergence.py" 4096 1 ;;
         snbench) run snbench 300 bash -c "tools/seqnorm_bench 4096 12 3 0.95 && tools/seqnorm_bench 4096 12 1 0.95 && tools/seqnorm_bench 4096 12 3 0.8" ;;
         snws) run snws 300 env SNB_WS=1 tools/seqnorm_bench 4096 12 3 0.95 ;;
         sndebug) run sndebug 300 env OF2D_LIB_PATH=tools/ab/sndebug/libof2d.so python -u tools/time_convergence.py 4096 1 ;;  # tools/build_variant.sh sndebug registration.cpp -DOF2D_SN_DEBUG=1
         snprof) run snprof 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/$O/${tag}_snprof" -o k -- "$R/tools/seqnorm_bench" 4096 24 3 ;;
+        mtprobe) run mtprobe 120 tools/mt_launch_probe 8 3000 ;;
+        mtprobeprofserial) run mtprobeprofserial 180 rocprofv3 --kernel-trace --output-format csv -d "$R/$O/${tag}_mtprobeprofserial" -o k -- "$R/tools/mt_launch_probe" 8 3000 64 serial ;;
+        mtprobeprofq16) GPU_MAX_HW_QUEUES=16 run mtprobeprofq16 180 rocprofv3 --kernel-trace --output-format csv -d "$R/$O/${tag}_mtprobeprofq16" -o k -- "$R/tools/mt_launch_probe" 8 3000 ;;
+        mtprobeprof) MT_PROBE_MAPS="$R/$O/${tag}_mtprobeprof_maps.txt" run mtprobeprof 180 rocprofv3 --kernel-trace --output-format csv -d "$R/$O/${tag}_mtprobeprof" -o k -- "$R/tools/mt_launch_probe" 8 3000 ;;
         *) echo "unknown step $s"; exit 2 ;;
     esac || exit $?
 done

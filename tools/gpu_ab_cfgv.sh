@@ -1,11 +1,11 @@
 #!/bin/bash
 # bench_configs.py configuration A/B: the in-tree library ("base") and
-# tools/ab/<variant> builds (tools/build_variant.sh), interleaved, each
+# tools/abx/<variant> builds (tools/build_variant.sh), interleaved, each
 # variant's parity tests (a pytest file, or -) first:
 #   tools/gpu_ab_cfgv.sh <rounds> <config> <pytest file|-> <variant>...
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 rounds=$1 cfg=$2 tf=$3; shift 3
-lib() { [ "$1" = base ] && echo "" || echo "$PWD/tools/ab/$1/libof2d.so"; }
+lib() { [ "$1" = base ] && echo "" || echo "$PWD/tools/abx/$1/libof2d.so"; }
 if [ "$tf" != "-" ]; then
     for v in "$@"; do
         echo "== tests $v"

@@ -28,6 +28,9 @@ for mode, opts, niter in (("fixed 999", {"fixed_iters": 1}, 999), ("convergence"
         continue
     base = None
     for ng, share in [(g, sh) for g in ngs for sh in ((0,) if g == 1 else (0, 1))]:
+        if os.environ.get("OF2D_MAPS_DUMP"):  # to symbolise a crash's frames afterwards
+            with open("/proc/self/maps") as f, open(os.environ["OF2D_MAPS_DUMP"], "w") as g:
+                g.write(f.read())
         with ImageRegistration((n, n), [niter], 0, 0, [0.1], ngpus=ng, ngpus_share=share,
                                **opts) as r:
             r.set_images(ref, mov)
