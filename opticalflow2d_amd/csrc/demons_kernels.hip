@@ -49,19 +49,7 @@ constexpr int kCThreadsY = 4;
 constexpr int kCr = OF2D_DEMONS_CR;
 // warped slots per thread per gather batch of the fused kernel (tools/ A/B
 // builds override it)
-// stage ablation of the fused kernel (tools/demons_abl.sh; TIMING ONLY, the
-// results are wrong): 1 no bilinear warp (the tile reads Imov at the pixel),
-// 2 no force (the correction is the gradient), 3 no sigma_fluid convolution,
-// 4 no composition (the update is an addition)
-// A/B knob (round 4): 1 warps the moving image once per iteration into a
-// scratch plane (warp_kernel, 16 B/px) and the fused kernel loads the warped
-// slots instead of warping 1.3 slots per output pixel itself
-#ifndef OF2D_DEMONS_WARP1
-#define OF2D_DEMONS_WARP1 0
-#endif
-#ifndef OF2D_DEMONS_ABL
-#define OF2D_DEMONS_ABL 0
-#endif
+// warped slots per thread per gather batch of the fused kernel
 #ifndef OF2D_DEMONS_BW
 #define OF2D_DEMONS_BW 6
 #endif
@@ -154,43 +142,6 @@ __device__ __forceinline__ float2 demons_corr(float gx, float gy, float it, floa
     const float den = (gx * gx + gy * gy) + (SXP ? t * sxq : t / sxq);
     zero |= den == 0.0f;
     return make_float2(((gx * it) / den) * -1.0f, ((gy * it) / den) * -1.0f);
-}
-
-// The same with the two components' divisions by the one denominator as the
-// unscaled exact sequence with a shared refined reciprocal (hs_jacobi_impl.h
-// div2_unscaled: bit-identical to the compiler's IEEE quotient while den is in
-// [2^-40, 2^40) and each numerator in [2^-80, 2^50)), taken when every lane
-// of the wave is in that range (one ballot), the IEEE divisions otherwise.
-// An A/B build knob (OF2D_DEMONS_DIVU, round 5).
-#ifndef OF2D_DEMONS_DIVU
-#define OF2D_DEMONS_DIVU 0
-#endif
-__device__ __forceinline__ float dm_rcp_refined(float b) {
-    const float r0 = __builtin_amdgcn_rcpf(b);
-    return __builtin_fmaf(__builtin_fmaf(-b, r0, 1.0f), r0, r0);
-}
-template <bool SXP = false>
-__device__ __forceinline__ float2 demons_corr_u(float gx, float gy, float it, float sigma_isq,
-                                                float sxq, bool &zero) {
-    const float t = (it * it) * sigma_isq;
-    const float den = (gx * gx + gy * gy) + (SXP ? t * sxq : t / sxq);
-    zero |= den == 0.0f;
-    const float ax = gx * it, ay = gy * it;
-    const float mn = fminf(fabsf(ax), fabsf(ay)), mx = fmaxf(fabsf(ax), fabsf(ay));
-    const bool ok = den >= 0x1p-40f && den < 0x1p40f && mn >= 0x1p-80f && mx < 0x1p50f;
-    if (__builtin_amdgcn_ballot_w64(!ok) == 0) {
-        typedef float v2f_ __attribute__((ext_vector_type(2)));
-        const float r = dm_rcp_refined(den);
-        const v2f_ a = {ax, ay}, nb = {-den, -den}, rr = {r, r};
-        v2f_ q = a * rr;
-        v2f_ e = __builtin_elementwise_fma(nb, q, a);
-        q = __builtin_elementwise_fma(e, rr, q);
-        e = __builtin_elementwise_fma(nb, q, a);
-        q = __builtin_elementwise_fma(e, rr, q);
-        return make_float2(__builtin_amdgcn_div_fixupf(q.x, den, ax) * -1.0f,
-                           __builtin_amdgcn_div_fixupf(q.y, den, ay) * -1.0f);
-    }
-    return make_float2((ax / den) * -1.0f, (ay / den) * -1.0f);
 }
 
 // x tile of a launch over a subset of the tile columns: block columns
@@ -639,16 +590,7 @@ __global__ __launch_bounds__(TX * TY) OF2D_DEMONS_FUSED_ATTR void demons_fused_k
                 if (xedge) wrap(a[q], b[q]);
                 valid[q] = q0 + q < NW && s < WW * WH;
             }
-            if (OF2D_DEMONS_ABL == 1 || OF2D_DEMONS_WARP1) {  // Imov: the warped image
-#pragma unroll
-                for (int q = 0; q < BW; q++) {
-                    in[q] = valid[q] && (unsigned)a[q] < (unsigned)dimx &&
-                            (unsigned)b[q] < (unsigned)dimy;
-                    res[q] = Imov[in[q] ? ((unsigned)b[q] * (unsigned)P + (unsigned)a[q]) : 0u];
-                }
-            } else {
-                warp_batch<BW>(Imov, u, a, b, valid, dimx, dimy, P, res, in);
-            }
+            warp_batch<BW>(Imov, u, a, b, valid, dimx, dimy, P, res, in);
 #pragma unroll
             for (int q = 0; q < BW; q++)
                 if (valid[q]) wt[tid + NT * (q0 + q)] = in[q] ? res[q] : 0.0f;
@@ -688,13 +630,8 @@ __global__ __launch_bounds__(TX * TY) OF2D_DEMONS_FUSED_ATTR void demons_fused_k
                 if (s < WW * CH && cc < CW) {
                     const float *w = wt + (r + 1) * WW + (cc + 1);
                     const float gx = (w[1] - w[-1]) / 2.0f, gy = (w[WW] - w[-WW]) / 2.0f;
-                    ct[r * CW + cc] = OF2D_DEMONS_ABL == 2
-                                          ? make_float2(gx, gy + (w[0] - iref[q]))
-                                      : OF2D_DEMONS_DIVU
-                                          ? demons_corr_u<FAST>(gx, gy, w[0] - iref[q], sigma_isq,
-                                                                sxq, zero)
-                                          : demons_corr<FAST>(gx, gy, w[0] - iref[q], sigma_isq,
-                                                              sxq, zero);
+                    ct[r * CW + cc] =
+                        demons_corr<FAST>(gx, gy, w[0] - iref[q], sigma_isq, sxq, zero);
                 }
             }
         } else {
@@ -738,19 +675,14 @@ __global__ __launch_bounds__(TX * TY) OF2D_DEMONS_FUSED_ATTR void demons_fused_k
     const int r0 = (int)__builtin_amdgcn_readfirstlane(threadIdx.y) * R;
     float2 sm[R];
     bool has[R];
-    if (OF2D_DEMONS_ABL == 3) {
-#pragma unroll
-        for (int k = 0; k < R; k++) has[k] = false;
-    } else {
-        convR<KW, R, true, FAST, TX>(ct, ca, i, y0 + r0, threadIdx.x, r0, dimx, dimy, N, sm, has);
-    }
+    convR<KW, R, true, FAST, TX>(ct, ca, i, y0 + r0, threadIdx.x, r0, dimx, dimy, N, sm, has);
     float2 cv[R];
 #pragma unroll
     for (int k = 0; k < R; k++) {
         cv[k] = make_float2(0.0f, 0.0f);
         if (y0 + r0 + k < dimy) cv[k] = has[k] ? sm[k] : ct[(r0 + k + c) * CW + threadIdx.x + c];
     }
-    store_update<R>(u, out, i, y0 + r0, dimx, dimy, P, cv, OF2D_DEMONS_ABL == 4 ? 1 : mode);
+    store_update<R>(u, out, i, y0 + r0, dimx, dimy, P, cv, mode);
 }
 
 // u_new = u_mid (*) G(sigma_diffusion); Logger partials sum ||u_new - prev||,
@@ -879,11 +811,6 @@ void launch_demons_update(const float *Iref, const float *Imov, const float2 *u,
         launch_demons_force(Iref, Imov, u, corr, dimx, dimy, P, sigma_isq, sigma_xsq, status, st);
         smooth_compose_tiles(corr, u, out, dimx, dimy, P, a, mode, gx, gx, gx, st);
         return;
-    }
-    if (OF2D_DEMONS_WARP1) {  // corr is free on this path: the warped plane
-        float *iw = reinterpret_cast<float *>(corr);
-        launch_warp(Imov, u, iw, dimx, dimy, P, st);
-        Imov = iw;
     }
     float rsx = 0.0f;
     const bool fast = (float)wfull == 1.0f && pow2_reciprocal(sigma_xsq, &rsx);

@@ -222,14 +222,6 @@ static_assert(kSorGLead >= 1 && kSorGLead <= kSorNB, "granule vectors rotate thr
 #ifndef OF2D_SOR_LD_AUX
 #define OF2D_SOR_LD_AUX 2
 #endif
-// timing ablations of the sweep's step (tools/sor_harness.hip builds only;
-// results WRONG when set): bit 0 no row loads of the next group, 1 no value
-// store, 2 no granule publish, 3 the DPP lane shifts as plain register
-// copies, 4 the update without its cross-diagonal term, 5 no granule tag
-// check (strip 0 never waits anyway)
-#ifndef OF2D_SOR_ABL
-#define OF2D_SOR_ABL 0
-#endif
 #ifndef OF2D_SOR_ST_AUX
 #define OF2D_SOR_ST_AUX 0
 #endif
@@ -536,13 +528,8 @@ __global__ __launch_bounds__(kInc ? 256 : 64) void sor_strip_kernel(float4 *__re
     v2f LU = v2f{0.0f, 0.0f}, L = LU, D = lo2(W0);
     v2f G = LU;  // lane k: ghost row (step + 2 + k) of the current batch
 
-#if OF2D_SOR_ABL & 8
-#define SOR_SHL(x) (x)
-#define SOR_SHR(o, x) (x)
-#else
 #define SOR_SHL(x) dpp_shl(x)
 #define SOR_SHR(o, x) dpp_shr_old(o, x)
-#endif
     auto step = [&](auto chk, int s, int j, __amdgpu_buffer_rsrc_t rs,
                     __amdgpu_buffer_rsrc_t ps, v4u xin) {
         const v2f C = lo2(W0), b = hi2(W0), U = lo2(W1);
@@ -555,29 +542,20 @@ __global__ __launch_bounds__(kInc ? 256 : 64) void sor_strip_kernel(float4 *__re
         // OpticalFlowFluid.cpp:27-35, same association, no contraction
         const v2f RL = R + L;
         const v2f s1v = (RL + U) + D;
-#if OF2D_SOR_ABL & 16
-        const v2f s2v = RL;
-        (void)LD;
-#else
         const v2f t = ((RU - LU) - RD) + LD;
         const v2f s2v = RL + 0.25f * t.yx;
-#endif
         const v2f n = A * C + B * ((b - M * s1v) - ML * s2v);
         v2f out = n;
         if constexpr (decltype(chk)::value) {
             const int r = s + 1 - 2 * lane;
             if ((unsigned)(r - 1) >= (unsigned)(dimy - 2)) out = C;  // boundary row: OLD value
         }
-#if !(OF2D_SOR_ABL & 2)
         __builtin_amdgcn_raw_buffer_store_b64(
             v2u{__float_as_uint(out.x), __float_as_uint(out.y)}, rs, voff_st, j * (int)P16,
             OF2D_SOR_ST_AUX);
-#endif
-#if !(OF2D_SOR_ABL & 4)
         __builtin_amdgcn_raw_buffer_store_b128(
             v4u{__float_as_uint(out.x), __float_as_uint(out.y), epoch, epoch}, ps,
             voff_pub + (unsigned)j * 16u, 0, 16 /* sc1 */);
-#endif
         D = out;
         W0 = W1;
         W1 = W2;
@@ -600,7 +578,7 @@ __global__ __launch_bounds__(kInc ? 256 : 64) void sor_strip_kernel(float4 *__re
 #ifdef OF2D_SOR_HTRACE  // tools/sor_harness.hip: per-batch hand-off timeline
             unsigned long long polled = 0;
 #endif
-            if (!(OF2D_SOR_ABL & 32) && !granules_ready(gv, sb + 2, dimy, epoch)) {
+            if (!granules_ready(gv, sb + 2, dimy, epoch)) {
                 gv = granule_poll(gr, voff_gin, kSorB * b * 16, sb + 2, dimy, epoch, status);
                 npoll++;
 #ifdef OF2D_SOR_HTRACE
@@ -625,10 +603,8 @@ __global__ __launch_bounds__(kInc ? 256 : 64) void sor_strip_kernel(float4 *__re
                 step(chk, sb + j, j, rs, ps, X[b][j]);
             }
             // batch b of the next group: rows 32 further down
-#if !(OF2D_SOR_ABL & 1)
 #pragma unroll
             for (int j = 0; j < kSorB; j++) X[b][j] = ldrow(rs, (4 + kSorG + j) * (int)P16, AuxLd{});
-#endif
             vrow += vstep;
             prow += kSorB * 16;
         }

@@ -124,19 +124,13 @@ float logger_error(double sum_diff, double sum_prev, double npx);
 #ifndef OF2D_SN_WALKERS
 #define OF2D_SN_WALKERS 3
 #endif
-// decision blocks the host enqueues ahead of the one it reads while the
-// errors are far from the break (1 near it: a break leaves the enqueued blocks
-// behind it as no-op launches)
-#ifndef OF2D_SN_AHEAD
-#define OF2D_SN_AHEAD 1
-#endif
 constexpr int kMaxEst = OF2D_SN_RING + 1 > 16 ? OF2D_SN_RING + 1 : 16;
 // CUs kept from the bandwidth kernels of HS's exact loop (its triples and
 // passes run on streams with a CU mask without them), so that the loop's
 // latency chain (check, entries, walks) finds free slots: 4096^2 procedural
 // 141-142 -> 128-131 us per iteration with 8-32 CUs kept, texture unchanged
-// (profiles/r05e_conv_cumask_ab.log); OF2D_SN_CUMASK_CHAIN 1 also keeps the
-// chain's streams on those CUs only (slower: r05d).  0 = no mask.
+// (profiles/r05e_conv_cumask_ab.log; the chain's streams on those CUs only
+// was slower: r05d).  0 = no mask.
 #ifndef OF2D_SN_CUMASK
 #define OF2D_SN_CUMASK 16
 #endif
@@ -149,24 +143,6 @@ constexpr int kMaxEst = OF2D_SN_RING + 1 > 16 ? OF2D_SN_RING + 1 : 16;
 // 143-146 / 122-124, 6: 143-145 / 123 (profiles/r05i_blk_ab.log)
 #ifndef OF2D_SN_BLOCK
 #define OF2D_SN_BLOCK 9
-#endif
-// HS's exact loop: each triple and its batch's pass in OF2D_SN_PARTS row parts
-// (the triple's bands split evenly), part q's pass on sn_st_ right behind part
-// q's triple on st_, so that it reads iterates just written (A/B knob; 1 =
-// whole-grid launches)
-#ifndef OF2D_SN_PARTS
-#define OF2D_SN_PARTS 1
-#endif
-#ifndef OF2D_SN_PASS_SERIAL
-#define OF2D_SN_PASS_SERIAL 0
-#endif
-// CUs of the exact loop's mask given to the passes alone (the triples get the
-// rest): 0 = passes and triples share the masked CUs (A/B knob)
-#ifndef OF2D_SN_PASS_CUS
-#define OF2D_SN_PASS_CUS 0
-#endif
-#ifndef OF2D_SN_CUMASK_CHAIN
-#define OF2D_SN_CUMASK_CHAIN 0
 #endif
 // 1: the walks on the reserved CUs, the check and entries on every CU (a walk
 // block beside the triple's and pass's blocks slows them more than the walk
@@ -288,7 +264,6 @@ class Registration {
     // loop) and its passes on sn_st_, both masked (OF2D_SN_CUMASK; null: no
     // mask), with tri_slots_ resident triple blocks
     hipStream_t hs_st_ = nullptr;
-    hipEvent_t ev_part_ = nullptr;  // a part's triple done (OF2D_SN_PARTS)
     int tri_slots_ = 1024;
     static constexpr int kExactEv = 64;  // event ring per group (two blocks in flight)
     // workspace sets: group g's walk is read (its profile) by group g + kSeqSets

@@ -160,7 +160,6 @@ Registration::~Registration() {
     if (d_scalar_) (void)hipFree(d_scalar_);
     lv_.clear();
     if (ev_fork_) (void)hipEventDestroy(ev_fork_);
-    if (ev_part_) (void)hipEventDestroy(ev_part_);
     if (ev_join_) (void)hipEventDestroy(ev_join_);
     if (sn_st_) (void)hipStreamDestroy(sn_st_);
     if (fx_st_) (void)hipStreamDestroy(fx_st_);
@@ -221,20 +220,20 @@ void Registration::ensure_device() {
     OF2D_HIP(hipStreamCreateWithFlags(&st_, hipStreamNonBlocking));
     // HS's exact loop on CU-masked streams (OF2D_SN_CUMASK; a device or
     // runtime without CU masks gets unmasked streams)
-    std::vector<uint32_t> big((ncu_ + 31) / 32, 0u), small(big.size(), 0u), pass(big.size(), 0u);
-    const int pc = OF2D_SN_PASS_CUS > 0 && OF2D_SN_CUMASK + OF2D_SN_PASS_CUS < ncu_
-                       ? OF2D_SN_PASS_CUS : 0;
+    // (hipExtStreamCreateWithCUMask makes BLOCKING streams: they order against
+    // the null stream, so the library keeps its own null-stream calls — the
+    // synchronous hipMemcpy / hipMemset of setup and read-back — off the loop)
+    std::vector<uint32_t> big((ncu_ + 31) / 32, 0u), small(big.size(), 0u);
     bool masked = false;
     if (OF2D_SN_CUMASK > 0 && OF2D_SN_CUMASK < ncu_) {
         for (int c = 0; c < ncu_; c++) {
             if (c < OF2D_SN_CUMASK) small[c / 32] |= 1u << (c % 32);
-            else if (c < OF2D_SN_CUMASK + pc) pass[c / 32] |= 1u << (c % 32);
             else big[c / 32] |= 1u << (c % 32);
         }
         masked = hipExtStreamCreateWithCUMask(&hs_st_, (uint32_t)big.size(), big.data()) ==
                      hipSuccess &&
-                 hipExtStreamCreateWithCUMask(&sn_st_, (uint32_t)big.size(),
-                                              pc ? pass.data() : big.data()) == hipSuccess;
+                 hipExtStreamCreateWithCUMask(&sn_st_, (uint32_t)big.size(), big.data()) ==
+                     hipSuccess;
         if (!masked) {
             (void)hipGetLastError();
             for (hipStream_t *q : {&hs_st_, &sn_st_})
@@ -243,15 +242,11 @@ void Registration::ensure_device() {
         }
     }
     if (masked) {
-        tri_slots_ = 4 * (ncu_ - OF2D_SN_CUMASK - pc);
+        tri_slots_ = 4 * (ncu_ - OF2D_SN_CUMASK);
     } else {
         OF2D_HIP(hipStreamCreateWithFlags(&sn_st_, hipStreamNonBlocking));
     }
-    if (masked && OF2D_SN_CUMASK_CHAIN) {
-        OF2D_HIP(hipExtStreamCreateWithCUMask(&fx_st_, (uint32_t)small.size(), small.data()));
-        for (hipStream_t &w : wk_st_)
-            OF2D_HIP(hipExtStreamCreateWithCUMask(&w, (uint32_t)small.size(), small.data()));
-    } else if (masked && OF2D_SN_CUMASK_WALK) {
+    if (masked && OF2D_SN_CUMASK_WALK) {
         OF2D_HIP(hipStreamCreateWithPriority(&fx_st_, hipStreamNonBlocking, pr));
         for (hipStream_t &w : wk_st_)
             OF2D_HIP(hipExtStreamCreateWithCUMask(&w, (uint32_t)small.size(), small.data()));
@@ -271,7 +266,6 @@ void Registration::ensure_device() {
         OF2D_HIP(hipEventCreateWithFlags(&ev_walk_[k], hipEventDisableTiming));
     }
     OF2D_HIP(hipEventCreateWithFlags(&ev_fork_, hipEventDisableTiming));
-    OF2D_HIP(hipEventCreateWithFlags(&ev_part_, hipEventDisableTiming));
     OF2D_HIP(hipEventCreateWithFlags(&ev_join_, hipEventDisableTiming));
     lv_.resize(nscales_ + 1);
     size_t maxnb = 1;
@@ -517,13 +511,10 @@ void Registration::enqueue_norms(const SeqnormBatch &B, const Level &L, int g, d
                                  float *seqh_out, bool passed) {
     auto ev = [](hipEvent_t *e, int q) { return e[q % kExactEv]; };
     if (!passed) {
-        // OF2D_SN_PASS_SERIAL (A/B knob): the pass right behind the triple on
-        // its stream instead of beside the next triples on sn_st_
-        hipStream_t ps = OF2D_SN_PASS_SERIAL ? st_ : sn_st_;
-        OF2D_HIP(hipStreamWaitEvent(ps, ev(ev_step_, g), 0));
-        if (g >= kSeqSets) OF2D_HIP(hipStreamWaitEvent(ps, ev(ev_walk_, g - kSeqSets), 0));
-        launch_seqnorm_pass(B, L.dx, L.dy, L.P, ps);
-        OF2D_HIP(hipEventRecord(ev(ev_pass_, g), ps));
+        OF2D_HIP(hipStreamWaitEvent(sn_st_, ev(ev_step_, g), 0));
+        if (g >= kSeqSets) OF2D_HIP(hipStreamWaitEvent(sn_st_, ev(ev_walk_, g - kSeqSets), 0));
+        launch_seqnorm_pass(B, L.dx, L.dy, L.P, sn_st_);
+        OF2D_HIP(hipEventRecord(ev(ev_pass_, g), sn_st_));
     }
     OF2D_HIP(hipStreamWaitEvent(fx_st_, ev(ev_pass_, g), 0));
     launch_seqnorm_refine(B, L.dx, L.dy, L.P, fx_st_);
@@ -598,8 +589,10 @@ int Registration::run_exact_pipelined_on(Level &L, int niter, const StepFn &step
     OF2D_HIP(hipMemsetAsync(stop, 0x7f, sizeof(int), st_));  // no break yet
     constexpr int kNoStop = 0x7f7f7f7f;
     // a block: whole triples, few enough groups that no event of a block being
-    // read is recorded again before it is (OF2D_SN_AHEAD + 1 blocks in flight)
-    constexpr int kInFlight = OF2D_SN_AHEAD + 1;
+    // read is recorded again before it is (two blocks in flight: the host
+    // enqueues one ahead of the one it reads; deeper queues measured no better,
+    // profiles/r05q_ahead_ab.log)
+    constexpr int kInFlight = 2;
     const int cb = chunk_set_ ? chunk_ : OF2D_SN_BLOCK;
     const int blk = std::min(3 * ((cb + 2) / 3), 3 * (kExactEv / kInFlight - 4));
     const int ring2 = kInFlight * blk;  // the sums' ring: the blocks in flight
@@ -615,9 +608,6 @@ int Registration::run_exact_pipelined_on(Level &L, int niter, const StepFn &step
     const unsigned epoch = (++exact_epoch_ & 0xfffu) << 20;
     std::vector<int> grp_of((size_t)std::max(niter, 1));
     int g = 0;
-    // the triple's row bands (launch_hs_jacobi3's geometry at tri_slots_)
-    const int band_rows = kHs3Waves * hs3_rows(L.dx, L.dy, tri_slots_);
-    const int nbands = (L.dy + band_rows - 1) / band_rows;
     // iterations [t, t + k) as group g (t a multiple of three)
     auto enqueue_group = [&](int t, int k) {
         for (int m = t; m < t + k; m++) grp_of[m] = g;
@@ -628,11 +618,10 @@ int Registration::run_exact_pipelined_on(Level &L, int niter, const StepFn &step
                 last = grp_of[q];
                 OF2D_HIP(hipStreamWaitEvent(st_, ev(ev_walk_, last), 0));
             }
-        const bool parts = k == 3 && OF2D_SN_PARTS > 1 && nbands >= OF2D_SN_PARTS;
-        if (k == 3 && !parts)
+        if (k == 3)
             step3m(L.est[slot(t)].p, L.est[slot(t + 1)].p, L.est[slot(t + 2)].p,
                    L.est[slot(t + 3)].p, t, -1, -1);
-        else if (k < 3)
+        else
             for (int m = t; m < t + k; m++) step(L.est[slot(m)].p, L.est[slot(m + 1)].p, d_partial_);
         SeqnormBatch B;
         B.K = k;
@@ -653,35 +642,8 @@ int Registration::run_exact_pipelined_on(Level &L, int niter, const StepFn &step
                 if (g - q >= 0) B.near[i][q - 1] = d_seqws_[3 * ((g - q) % kSeqSets) + i].p;
         }
         B.epoch = epoch;
-        if (parts) {
-            // part q: its bands' triple on st_, then on sn_st_ the pass over the
-            // tiles whose terms all lie in rows written so far
-            if (g >= kSeqSets) OF2D_HIP(hipStreamWaitEvent(sn_st_, ev(ev_walk_, g - kSeqSets), 0));
-            const int P = OF2D_SN_PARTS;
-            for (int q = 0; q < P; q++) {
-                const int blo = q * nbands / P, bhi = (q + 1) * nbands / P;
-                step3m(L.est[slot(t)].p, L.est[slot(t + 1)].p, L.est[slot(t + 2)].p,
-                       L.est[slot(t + 3)].p, t, blo, bhi);
-                OF2D_HIP(hipEventRecord(ev_part_, st_));
-                OF2D_HIP(hipStreamWaitEvent(sn_st_, ev_part_, 0));
-                const long rhi = q == P - 1 ? L.dy : std::min<long>(L.dy, (long)bhi * band_rows);
-                B.tile_lo = B.tile_hi;
-                B.tile_hi = q == P - 1 ? 0u : (unsigned)(rhi * L.dx / kSnTile);
-                if (q == P - 1 || B.tile_hi > B.tile_lo) {
-                    SeqnormBatch Bq = B;
-                    if (q == P - 1) Bq.tile_hi = 0;  // the rest
-                    launch_seqnorm_pass(Bq, L.dx, L.dy, L.P, sn_st_);
-                } else {
-                    B.tile_hi = B.tile_lo;
-                }
-            }
-            OF2D_HIP(hipEventRecord(ev(ev_step_, g), st_));
-            OF2D_HIP(hipEventRecord(ev(ev_pass_, g), sn_st_));
-            enqueue_norms(B, L, g, npx, hs_.seqh + 2 * (size_t)(t % ring2), true);
-        } else {
-            OF2D_HIP(hipEventRecord(ev(ev_step_, g), st_));
-            enqueue_norms(B, L, g, npx, hs_.seqh + 2 * (size_t)(t % ring2));
-        }
+        OF2D_HIP(hipEventRecord(ev(ev_step_, g), st_));
+        enqueue_norms(B, L, g, npx, hs_.seqh + 2 * (size_t)(t % ring2));
         g++;
     };
     const int ntrip = niter / 3 * 3;
@@ -716,14 +678,11 @@ int Registration::run_exact_pipelined_on(Level &L, int niter, const StepFn &step
                               ") is not the host's (" + std::to_string(tbreak) + ")");
     };
     // blocks enqueued so far (of the nbt blocks of triples); the host keeps
-    // `ahead` blocks queued beyond the one it reads: OF2D_SN_AHEAD while the
-    // errors' decay says the break is further away than that, one near it
+    // one block queued beyond the one it reads
     int enq = 0;
-    int ahead = OF2D_SN_AHEAD;
-    float err_prev = -1.0f;  // the last error of the block before
     if (nblocks > 0) enqueue_block(enq++);
     for (int b = 0; b < nblocks; b++) {
-        while (enq < nbt && enq <= b + ahead) enqueue_block(enq++);
+        while (enq < nbt && enq <= b + 1) enqueue_block(enq++);
         // block b's sums: the last walk of each walk stream, then its decide
         for (int q = std::max(gbeg[b + 1] - kWalkers, gbeg[b]); q < gbeg[b + 1]; q++)
             OF2D_HIP(hipEventSynchronize(ev(ev_walk_, q)));
@@ -739,10 +698,9 @@ int Registration::run_exact_pipelined_on(Level &L, int niter, const StepFn &step
                              h[9]);
             }
         }
-        float err = 0.0f;
         for (int t = lo_of(b); t < hi_of(b); t++) {
             const float *sm = hs_.seqh + 2 * (size_t)(t % ring2);
-            err = logger_error(sm[0], sm[1], npx);
+            const float err = logger_error(sm[0], sm[1], npx);
             last_err_.push_back(err);
             if (verbose_) print("Iteration: %d\tError:%.4f\n", t, (double)err);
             if (err < 0.001f && t > 1) {  // ImageRegistrationOpticalFlow.cpp:131-134
@@ -750,20 +708,6 @@ int Registration::run_exact_pipelined_on(Level &L, int niter, const StepFn &step
                 final_buf = slot(t + 1);
                 return t + 1;
             }
-        }
-        if (OF2D_SN_AHEAD > 1) {
-            // blocks to the break at this block's decay of the error (its
-            // ratio to the last block's), or none known: keep the deep queue
-            // only while more than `OF2D_SN_AHEAD + 1` blocks remain
-            ahead = 1;
-            if (err_prev > 0.0f && err > 0.001f && err < err_prev) {
-                const double q = std::log((double)err / err_prev);  // per block, < 0
-                const double left = std::log(0.001 / (double)err) / q;
-                if (left > OF2D_SN_AHEAD + 2) ahead = OF2D_SN_AHEAD;
-            } else if (err_prev > 0.0f && err >= err_prev && err > 0.004f) {
-                ahead = OF2D_SN_AHEAD;  // not decaying and far above the threshold
-            }
-            err_prev = err;
         }
         if (b + 1 == nbt && nblocks > nbt) enqueue_block(nbt);  // the tail, after the rest
     }

@@ -76,15 +76,6 @@ namespace of2d {
 namespace {
 
 constexpr int kSnThreads = 256;                 // table kernels: 4 waves
-// issue priority of the Logger chain's waves (check, entries, walk): the
-// triple kernel's waves run at raised priority (progress_prio) and would
-// otherwise win every issue slot of a SIMD they share with a walker
-#ifndef OF2D_SN_CHAIN_PRIO
-#define OF2D_SN_CHAIN_PRIO 0
-#endif
-__device__ __forceinline__ void sn_chain_prio() {
-    if constexpr (OF2D_SN_CHAIN_PRIO > 0) __builtin_amdgcn_s_setprio(OF2D_SN_CHAIN_PRIO);
-}
 constexpr int kSnSegs = kSnTile / 64;           // 64-term segments per tile
 constexpr int kSnCand = 4;                      // candidate binades per tile and norm
 // relative width of the profile's prediction window (tables): a tile takes the
@@ -378,9 +369,6 @@ __device__ __forceinline__ bool sn_block_stopped(const SnJobs &J) {
 // with the segment D ahead right after its own is consumed, so a load has
 // D - 1 segments' arithmetic to arrive (the pass: 2-4 x (K + 1) float2; the
 // fix, one pair: 8 x 2)
-#ifndef OF2D_SN_ABL
-#define OF2D_SN_ABL 0  // timing ablations of the pass (results wrong when set)
-#endif
 // (K = 3: a ring of 2 measured 119 us per three-update pass against 144 for 4,
 // whose 155 VGPRs leave 3 waves per SIMD, and 93 for the loads alone;
 // profiles/r04g_sn_ring_ab.log)
@@ -510,10 +498,6 @@ __device__ __forceinline__ void sn_wave_pass(const SnJobs &J, unsigned N, int di
                     // Field::operator- (Field.tpp:305-334) for |cur - prev|
                     const float x = n ? cv[d][i].x : cv[d][i + 1].x - cv[d][i].x;
                     const float y = n ? cv[d][i].y : cv[d][i + 1].y - cv[d][i].y;
-#if OF2D_SN_ABL == 2  // timing only: the loads and a sum, no arithmetic
-                    fs[i][n] += x + y;
-                    continue;
-#endif
                     const SnEst v = sn_est(x, y);
                     const bool nz = sn_ballot(v.nz) != 0ull;
                     zv[i][n] = lane == s ? nz : zv[i][n];
@@ -756,9 +740,6 @@ void seqnorm_tables(unsigned N, int dimx, int P, unsigned nt, SnJobs J) {
                 if (hdr_nc(hd[i][n])) hd[i][n] |= kHdrPending;
         ncmax = 0;
     }
-#if OF2D_SN_ABL  // timing only: no tile entries
-    ncmax = 0;
-#endif
     if (ncmax == 0) sn_wave_pass<K, 0>(J, N, dimx, P, nt, b, hd);
     else if (ncmax == 1) sn_wave_pass<K, 1>(J, N, dimx, P, nt, b, hd);
     else sn_wave_pass<K, 2>(J, N, dimx, P, nt, b, hd);
@@ -825,7 +806,6 @@ __device__ __forceinline__ double sn_drift(const SnWs &ws, unsigned nt, int src,
 }
 __global__ __launch_bounds__(kSnChk) void seqnorm_check_sums(unsigned nt, SnJobs J) {
     if (sn_block_stopped(J)) return;
-    sn_chain_prio();
     const SnWs &ws = J.ws[blockIdx.y];
     const int use_prof = J.use_prof[blockIdx.y];
     const unsigned b = blockIdx.x * kSnChk + threadIdx.x;
@@ -850,7 +830,6 @@ __global__ __launch_bounds__(kSnChk) void seqnorm_check_sums(unsigned nt, SnJobs
 // total
 __global__ __launch_bounds__(kSnScan) void seqnorm_check_scan(unsigned nt, unsigned nb, SnJobs J) {
     if (sn_block_stopped(J)) return;
-    sn_chain_prio();
     const SnWs &ws = J.ws[blockIdx.y];
     const double *p_off = J.p_off[blockIdx.y];
     const unsigned chunk = (nb + kSnScan - 1) / kSnScan;
@@ -911,7 +890,6 @@ __global__ __launch_bounds__(kSnScan) void seqnorm_check_scan(unsigned nt, unsig
 }
 __global__ __launch_bounds__(kSnChk) void seqnorm_check(unsigned nt, SnJobs J) {
     if (sn_block_stopped(J)) return;
-    sn_chain_prio();
     const SnWs &ws = J.ws[blockIdx.y];
     const int use_prof = J.use_prof[blockIdx.y];
     const unsigned b = blockIdx.x * kSnChk + threadIdx.x;
@@ -1011,7 +989,6 @@ template <int K>
 __global__ __launch_bounds__(kSnThreads) void seqnorm_entries(unsigned N, int dimx, int P,
                                                               unsigned nt, SnJobs J) {
     if (sn_block_stopped(J)) return;
-    sn_chain_prio();
     bool many = false;
 #pragma unroll
     for (int i = 0; i < K; i++) many |= J.ws[i].cnt[0] > kSnRefillMin;
@@ -1323,7 +1300,6 @@ constexpr int kSnAhead = 8;  // windows loaded per step: the next step's loads h
 __global__ __launch_bounds__(64 * kSnWalkWaves) void seqnorm_walk(unsigned N, int dimx, int P,
                                                                    unsigned nt, SnJobs J) {
     if (sn_block_stopped(J)) return;  // one decision for the whole block
-    sn_chain_prio();
     const int job = blockIdx.x >> 1;
     const int n = blockIdx.x & 1;  // 0: |cur - prev|, 1: |prev|
     const int lane = threadIdx.x & 63;

@@ -8,7 +8,9 @@
 #        prof (rocprofv3 kernel stats of bench.py), conv (convergence-on
 #        timings at 4096^2), convprof (their kernel trace + stats),
 #        configs (bench_configs.py), ranks (ngpus timings), ranksprof (their
-#        kernel trace, 8 ranks), texprof / freshprof (kernel trace of the
+#        kernel trace, 8 ranks; ranksprofq16 with 16 hardware queues, which
+#        the profiler's queue interception needs for multi-thread launches,
+#        DESIGN.md §5), texprof / freshprof (kernel trace of the
 #        texture pair's warm / fresh loops), snbench /
 #        snprof (the Logger-norm harness: stage timings / kernel stats),
 #        mtprobe / mtprobeprof (tools/mt_launch_probe: the slab group's
@@ -44,6 +46,7 @@ for s in "$@"; do
         configs) run configs 900 python -u bench_configs.py ;;
         ranks) run ranks 600 python -u tools/time_ranks.py ;;
         ranksprof) OF2D_MAPS_DUMP="$R/$O/${tag}_ranksprof_maps.txt" run ranksprof 600 rocprofv3 --kernel-trace --output-format csv -d "$R/$O/${tag}_ranksprof" -o k -- python3 -u "$R/tools/time_ranks.py" 4096 1 fixed,conv 8 ;;
+        ranksprofq16) GPU_MAX_HW_QUEUES=16 run ranksprofq16 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/$O/${tag}_ranksprofq16" -o k -- python3 -u "$R/tools/time_ranks.py" 4096 1 fixed,conv 8 ;;
         texprof) OF2D_CONV_CASE=texture OF2D_CONV_ONLY=1 run texprof 300 rocprofv3 --kernel-trace --output-format csv -d "$R/$O/${tag}_texprof" -o k -- python3 -u "$R/tools/time_convergence.py" 4096 1 ;;
         freshprof) OF2D_CONV_FRESH=1 OF2D_CONV_CASE=texture OF2D_CONV_ONLY=1 run freshprof 300 rocprofv3 --kernel-trace --output-format csv -d "$R/$O/${tag}_freshprof" -o k -- python3 -u "$R/tools/time_convergence.py" 4096 1 ;;
         snbench) run snbench 300 bash -c "tools/seqnorm_bench 4096 12 3 0.95 && tools/seqnorm_bench 4096 12 1 0.95 && tools/seqnorm_bench 4096 12 3 0.8" ;;

@@ -2,7 +2,7 @@
 # bench_configs.py configuration A/B: the in-tree library ("base") and
 # tools/abx/<variant> builds (tools/build_variant.sh), interleaved, each
 # variant's parity tests (a pytest file, or -) first:
-#   tools/gpu_ab_cfgv.sh <rounds> <config> <pytest file|-> <variant>...
+#   tools/gpu_ab_cfgv.sh <rounds> <config: 1, 2c, 3, 4 or 5> <pytest file|-> <variant>...
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 rounds=$1 cfg=$2 tf=$3; shift 3
 lib() { [ "$1" = base ] && echo "" || echo "$PWD/tools/abx/$1/libof2d.so"; }
