@@ -344,6 +344,41 @@ void launch_regrid(const float2 *m_old, const float2 *est, float2 *est0, float2 
     OF2D_HIP(hipGetLastError());
 }
 
+// The device-decided form (Registration::loop_fluid): the regrid runs only
+// after an iteration whose report decided one (kFluidRegridWord), the motion
+// fields are picked by the flipped index (the accumulated motion goes to
+// motion[mcur]), and the estimate is not touched: the next iteration reads it
+// as zero (fluid_zero_est) and as the Logger's prev.  Per pixel the operations
+// of regrid_kernel.
+__global__ void regrid_if_kernel(float2 *__restrict__ m0, float2 *__restrict__ m1,
+                                 const float2 *__restrict__ est, const float *__restrict__ Imov,
+                                 float *__restrict__ Iaux, int dimx, int dimy, int P,
+                                 FluidCtl ctl) {
+    if (fluid_stopped(ctl) || !fluid_zero_est(ctl)) return;
+    const bool c1 = ctl.w[kFluidMcurWord] != 0u;
+    const float2 *mo = c1 ? m0 : m1;
+    float2 *mn = c1 ? m1 : m0;
+    // kBx x kBy pixel blocks in a grid-stride loop (a capped grid: most
+    // launches are no-ops)
+    const int nbx = (dimx + kBx - 1) / kBx, nb = nbx * ((dimy + kBy - 1) / kBy);
+    for (int t = blockIdx.x; t < nb; t += gridDim.x) {
+        const int i = (t % nbx) * kBx + threadIdx.x, j = (t / nbx) * kBy + threadIdx.y;
+        if (i >= dimx || j >= dimy) continue;
+        const long idx = (long)j * P + i;
+        const float2 m = accumulate_px(mo, est[idx], mo[idx], i, j, dimx, dimy, P);
+        mn[idx] = m;
+        Iaux[idx] = warp_px(Imov, m, Imov[idx], i, j, dimx, dimy, P);
+    }
+}
+void launch_regrid_if(float2 *m0, float2 *m1, const float2 *est, const float *Imov, float *Iaux,
+                      int dimx, int dimy, int P, hipStream_t st, FluidCtl ctl) {
+    if (!ctl.w) throw std::invalid_argument("launch_regrid_if: control words");
+    const dim3 g = grid2d(dimx, dimy);
+    hipLaunchKernelGGL(regrid_if_kernel, dim3(std::min((int)(g.x * g.y), kCappedGrid)),
+                       dim3(kBx, kBy), 0, st, m0, m1, est, Imov, Iaux, dimx, dimy, P, ctl);
+    OF2D_HIP(hipGetLastError());
+}
+
 // Motion::accumulate of an estimate onto a ZERO motion field (the end of the
 // single-level refine loop, ImageRegistrationOpticalFlow.cpp:138): the
 // interpolated old motion is 0, so u = est + 0 where (x + est) is inside the

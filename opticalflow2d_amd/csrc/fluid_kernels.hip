@@ -313,7 +313,7 @@ __device__ __forceinline__ unsigned ld_sc1_u32(const unsigned *p) {
 // sweep's loop)
 __device__ __attribute__((noinline)) void sor_increment_worker(const float4 *__restrict__ vb, int dimx, int dimy, int P,
                                      int nstrips, unsigned epoch, const SorInc &w,
-                                     unsigned *__restrict__ status) {
+                                     unsigned *__restrict__ status, bool zu) {
     // the tile's velocities (kSkJ x kSkI, as increment_kernel), one per wave:
     // the waves of a worker workgroup run independent tile loops, so they
     // synchronise only within themselves (LDS ops of one wave run in order)
@@ -335,7 +335,15 @@ __device__ __attribute__((noinline)) void sor_increment_worker(const float4 *__r
         // into the image (a clamped value is never used, gradients.h's
         // one-sided border taps take the others)
         float2 uc[34], ul[32], ur[32];
-        {
+        if (zu) {
+            // the zero estimate after a regrid: its gradients are +0 exactly as
+            // from a zeroed buffer
+#pragma unroll
+            for (int r = 0; r < 34; r++) {
+                uc[r] = make_float2(0.0f, 0.0f);
+                if (r >= 1 && r <= 32) ul[r - 1] = ur[r - 1] = uc[r];
+            }
+        } else {
             const int ic = min(i0 + lane, dimx - 1);
             const int il = max(ic - 1, 0), ir = min(ic + 1, dimx - 1);
 #pragma unroll
@@ -445,7 +453,10 @@ __global__ __launch_bounds__(kInc ? 256 : 64) void sor_strip_kernel(float4 *__re
                                                        unsigned *__restrict__ ticket, int nstrips,
                                                        unsigned *__restrict__ status,
                                                        unsigned long long *__restrict__ trace,
-                                                       SorInc inc) {
+                                                       SorInc inc, FluidCtl ctl) {
+    // an iteration past the loop's break: nothing (no ticket taken, so the
+    // counters stay a whole number of launches)
+    if (fluid_stopped(ctl)) return;
     const int lane = threadIdx.x;
     __shared__ int s_strip;
     if (lane == 0) {
@@ -459,7 +470,8 @@ __global__ __launch_bounds__(kInc ? 256 : 64) void sor_strip_kernel(float4 *__re
     const int I = __builtin_amdgcn_readfirstlane(s_strip);
     if constexpr (kInc) {
         if (I >= nstrips) {
-            sor_increment_worker(vb, dimx, dimy, P, nstrips, epoch, inc, status);
+            sor_increment_worker(vb, dimx, dimy, P, nstrips, epoch, inc, status,
+                                 fluid_zero_est(ctl));
             return;
         }
         if (threadIdx.x >= 64) return;  // a strip is one wave; its CU stays to itself
@@ -650,7 +662,7 @@ size_t sor_granule_bytes(int dimx, int dimy) {
 
 void launch_sor_traced(float4 *vb, int dimx, int dimy, int P, float mu, float lambda, float omega,
                        void *H, unsigned epoch, unsigned *ticket, unsigned *status,
-                       unsigned long long *trace, hipStream_t st) {
+                       unsigned long long *trace, hipStream_t st, FluidCtl ctl = {}) {
     if (dimx < 3 || dimy < 3) return;  // no interior (OpticalFlowFluid.cpp:23-24)
     const int ns = sor_nstrips(dimx);
     // per-pixel constants of OpticalFlowFluid.cpp:27 evaluated once, same float ops
@@ -659,12 +671,14 @@ void launch_sor_traced(float4 *vb, int dimx, int dimy, int P, float mu, float la
     const float ML = mu + lambda;
     hipLaunchKernelGGL(sor_strip_kernel<false>, dim3(ns), dim3(64), 0, st, vb, dimx, dimy, P, A,
                        B, mu, ML, (v4u *)H, sor_granule_stride(dimy), epoch, ticket, ns, status,
-                       trace, SorInc{});
+                       trace, SorInc{}, ctl);
     OF2D_HIP(hipGetLastError());
 }
 void launch_sor(float4 *vb, int dimx, int dimy, int P, float mu, float lambda, float omega,
-                void *H, unsigned epoch, unsigned *ticket, unsigned *status, hipStream_t st) {
-    launch_sor_traced(vb, dimx, dimy, P, mu, lambda, omega, H, epoch, ticket, status, nullptr, st);
+                void *H, unsigned epoch, unsigned *ticket, unsigned *status, hipStream_t st,
+                FluidCtl ctl) {
+    launch_sor_traced(vb, dimx, dimy, P, mu, lambda, omega, H, epoch, ticket, status, nullptr, st,
+                      ctl);
 }
 
 // Row-major <-> skewed transfer of a 64 (i) x 32 (j) pixel tile through LDS.
@@ -765,9 +779,15 @@ void launch_sor_pack(float4 *vb, const float2 *u, const float2 *dI, const float 
 __global__ __launch_bounds__(256) void regrid_pack_kernel(
     const float *__restrict__ Iref, const float *__restrict__ Ia, float2 *__restrict__ dI,
     float *__restrict__ It, float4 *__restrict__ vb, int dimx, int dimy, int P,
-    v4u *__restrict__ H, unsigned epoch) {
+    v4u *__restrict__ H, unsigned epoch, FluidCtl ctl) {
+    // with control words: only after an iteration that regridded
+    if (ctl.w && (fluid_stopped(ctl) || !fluid_zero_est(ctl))) return;
     __shared__ float2 fo[kSkJ][kSkI];
-    const int i0 = blockIdx.x * kSkI, j0 = blockIdx.y * kSkJ;
+    // tiles in a grid-stride loop: a capped grid keeps the launch cheap when
+    // the control words make it a no-op (most iterations)
+    const int ntx = (dimx + kSkI - 1) / kSkI, ntiles = ntx * ((dimy + kSkJ - 1) / kSkJ);
+    for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int i0 = (tile % ntx) * kSkI, j0 = (tile / ntx) * kSkJ;
     const int i = i0 + threadIdx.x;
     constexpr int NK = kSkJ / 4;
     // taps of every row of the thread first (border rows and columns pick the
@@ -810,12 +830,16 @@ __global__ __launch_bounds__(256) void regrid_pack_kernel(
     }
     __syncthreads();
     skew_tile_set_b(vb, i0, j0, dimx, dimy, P, [&](int ii, int jj) { return fo[jj][ii]; });
+    __syncthreads();  // fo is rewritten by the block's next tile
+    }
 }
 void launch_regrid_pack(const float *Iref, const float *Iaux, float2 *dI, float *It, float4 *vb,
-                        int dimx, int dimy, int P, void *H, unsigned epoch, hipStream_t st) {
-    hipLaunchKernelGGL(regrid_pack_kernel,
-                       dim3((dimx + kSkI - 1) / kSkI, (dimy + kSkJ - 1) / kSkJ), dim3(64, 4), 0,
-                       st, Iref, Iaux, dI, It, vb, dimx, dimy, P, (v4u *)H, epoch);
+                        int dimx, int dimy, int P, void *H, unsigned epoch, hipStream_t st,
+                        FluidCtl ctl) {
+    const int ntiles = ((dimx + kSkI - 1) / kSkI) * ((dimy + kSkJ - 1) / kSkJ);
+    hipLaunchKernelGGL(regrid_pack_kernel, dim3(ctl.w ? std::min(ntiles, kCappedGrid) : ntiles),
+                       dim3(64, 4), 0, st, Iref, Iaux, dI, It, vb, dimx, dimy, P, (v4u *)H,
+                       epoch, ctl);
     OF2D_HIP(hipGetLastError());
 }
 
@@ -845,7 +869,10 @@ void launch_force(const float2 *u, const float2 *dI, const float *It, float2 *f,
 __global__ __launch_bounds__(256) void increment_kernel(const float2 *__restrict__ u,
                                                         const float4 *__restrict__ vel,
                                                         float2 *__restrict__ R, int dimx, int dimy,
-                                                        int P, float *__restrict__ part) {
+                                                        int P, float *__restrict__ part,
+                                                        FluidCtl ctl) {
+    if (fluid_stopped(ctl)) return;
+    const bool zu = fluid_zero_est(ctl);
     __shared__ float2 vt[kSkJ][kSkI];  // the tile's velocities, read along skewed rows
     const int i0 = blockIdx.x * kSkI, j0 = blockIdx.y * kFieldRows;
     skew_tile_for_each(i0, j0, dimx, dimy, [&](int ii, int jj) {
@@ -859,7 +886,9 @@ __global__ __launch_bounds__(256) void increment_kernel(const float2 *__restrict
         if (i >= dimx || j >= dimy) break;
         const long idx = (long)j * P + i;
         const float2 v = vt[4 * k + threadIdx.y][threadIdx.x];
-        const Grad2 d = motion_gradients(u, idx, i, j, dimx, dimy, P);
+        // the zero estimate of a regrid: gradients +0, as from a zeroed buffer
+        const Grad2 d = zu ? Grad2{make_float2(0.0f, 0.0f), make_float2(0.0f, 0.0f)}
+                           : motion_gradients(u, idx, i, j, dimx, dimy, P);
         // (v - dudx*v.x) - dudy*v.y
         const float2 r = make_float2((v.x - d.dx.x * v.x) - d.dy.x * v.y,
                                      (v.y - d.dx.y * v.x) - d.dy.y * v.y);
@@ -874,7 +903,8 @@ __global__ __launch_bounds__(256) void increment_kernel(const float2 *__restrict
 
 // maxabs = sqrt(max) (float), dt = 0.65f / maxabs; scal[0]=maxabs, scal[1]=dt
 __global__ __launch_bounds__(1024) void timestep_kernel(const float *__restrict__ part, int n,
-                                                        float *__restrict__ scal) {
+                                                        float *__restrict__ scal, FluidCtl ctl) {
+    if (fluid_stopped(ctl)) return;
     float m = 0.0f;
     for (int k = threadIdx.x; k < n; k += 1024) m = (m < part[k]) ? part[k] : m;
     m = wide_max(m);
@@ -895,10 +925,12 @@ int increment_nblocks(int dimx, int dimy) {
 }
 
 void launch_increment(const float2 *u, const float4 *vel, float2 *R, int dimx, int dimy, int P,
-                      float *part, float *scal, hipStream_t st) {
+                      float *part, float *scal, hipStream_t st, FluidCtl ctl) {
     const dim3 g = field_grid(dimx, dimy);
-    hipLaunchKernelGGL(increment_kernel, g, dim3(64, 4), 0, st, u, vel, R, dimx, dimy, P, part);
-    hipLaunchKernelGGL(timestep_kernel, dim3(1), dim3(1024), 0, st, part, (int)(g.x * g.y), scal);
+    hipLaunchKernelGGL(increment_kernel, g, dim3(64, 4), 0, st, u, vel, R, dimx, dimy, P, part,
+                       ctl);
+    hipLaunchKernelGGL(timestep_kernel, dim3(1), dim3(1024), 0, st, part, (int)(g.x * g.y), scal,
+                       ctl);
     OF2D_HIP(hipGetLastError());
 }
 
@@ -913,7 +945,7 @@ int sor_increment_workers() { return OF2D_SOR_NCONS; }
 void launch_sor_increment(float4 *vb, int dimx, int dimy, int P, float mu, float lambda,
                           float omega, void *H, unsigned epoch, unsigned *ticket,
                           unsigned long long *ctr, const float2 *u, float2 *R, float *part,
-                          float *scal, unsigned *status, hipStream_t st) {
+                          float *scal, unsigned *status, hipStream_t st, FluidCtl ctl) {
     const int ns = sor_nstrips(dimx);
     const dim3 g = field_grid(dimx, dimy);
     const int ntiles = (int)(g.x * g.y);
@@ -932,8 +964,8 @@ void launch_sor_increment(float4 *vb, int dimx, int dimy, int P, float mu, float
     if (nwg < 0) nwg = ncu - ns;
     nwg = std::min(nwg, (ntiles + 3) / 4);
     if (ns == 0 || dimx < 3 || dimy < 3 || nwg < 8) {  // no sweep (OpticalFlowFluid.cpp:23-24)
-        launch_sor(vb, dimx, dimy, P, mu, lambda, omega, H, epoch, ticket, status, st);
-        launch_increment(u, vb, R, dimx, dimy, P, part, scal, st);
+        launch_sor(vb, dimx, dimy, P, mu, lambda, omega, H, epoch, ticket, status, st, ctl);
+        launch_increment(u, vb, R, dimx, dimy, P, part, scal, st, ctl);
         return;
     }
     const float A = 1.0f - omega;
@@ -942,8 +974,8 @@ void launch_sor_increment(float4 *vb, int dimx, int dimy, int P, float mu, float
     const SorInc inc{u, R, part, ticket + 1, ctr, nwg, ntiles, (int)g.y};
     hipLaunchKernelGGL(sor_strip_kernel<true>, dim3(ns + nwg), dim3(256), 0, st, vb, dimx, dimy,
                        P, A, B, mu, ML, (v4u *)H, sor_granule_stride(dimy), epoch, nullptr, ns,
-                       status, nullptr, inc);
-    hipLaunchKernelGGL(timestep_kernel, dim3(1), dim3(1024), 0, st, part, ntiles, scal);
+                       status, nullptr, inc, ctl);
+    hipLaunchKernelGGL(timestep_kernel, dim3(1), dim3(1024), 0, st, part, ntiles, scal, ctl);
     OF2D_HIP(hipGetLastError());
 }
 
@@ -970,7 +1002,11 @@ __global__ __launch_bounds__(256) void fluid_step_kernel(
     const float2 *__restrict__ prev,
     const float *__restrict__ scal, const float2 *__restrict__ dI, const float *__restrict__ It,
     float4 *__restrict__ vb, int dimx, int dimy, int P, v4u *__restrict__ H, unsigned epoch,
-    double *__restrict__ lpart, float *__restrict__ jpart) {
+    double *__restrict__ lpart, float *__restrict__ jpart, FluidCtl ctl) {
+    if (fluid_stopped(ctl)) return;
+    // the zero estimate of a regrid: integrated from +0, while the buffer's
+    // content (the pre-regrid estimate) is the Logger's prev
+    const bool zu = fluid_zero_est(ctl);
     constexpr int TW = kSkI + 2, TH = kSkJ + 2;
     __shared__ float2 un[TH][TW];       // new u at (i0 - 1 + c, j0 - 1 + r)
     __shared__ float2 fo[kSkJ][kSkI];   // the next iteration's force
@@ -998,7 +1034,7 @@ __global__ __launch_bounds__(256) void fluid_step_kernel(
 #pragma unroll
     for (int q = 0; q < NS; q++) {
         const int s = tid + 256 * q, r = s / TW, c = s - r * TW;
-        float2 m = mu[q];
+        float2 m = zu ? make_float2(0.0f, 0.0f) : mu[q];
         if (integ) m = make_float2(m.x + mr[q].x * dt, m.y + mr[q].y * dt);
         if (okq[q]) un[r][c] = m;
     }
@@ -1077,14 +1113,15 @@ __global__ __launch_bounds__(256) void fluid_step_kernel(
 void launch_fluid_step(const float2 *u, const float2 *R, float2 *uo, const float2 *prev,
                        const float *scal,
                        const float2 *dI, const float *It, float4 *vb, int dimx, int dimy, int P,
-                       void *H, unsigned epoch, double *lpart, float *jpart, hipStream_t st) {
+                       void *H, unsigned epoch, double *lpart, float *jpart, hipStream_t st,
+                       FluidCtl ctl) {
     const dim3 g = field_grid(dimx, dimy);
     if (prev)
         hipLaunchKernelGGL(fluid_step_kernel<true>, g, dim3(64, 4), 0, st, u, R, uo, prev, scal,
-                           dI, It, vb, dimx, dimy, P, (v4u *)H, epoch, lpart, jpart);
+                           dI, It, vb, dimx, dimy, P, (v4u *)H, epoch, lpart, jpart, ctl);
     else
         hipLaunchKernelGGL(fluid_step_kernel<false>, g, dim3(64, 4), 0, st, u, R, uo, prev, scal,
-                           dI, It, vb, dimx, dimy, P, (v4u *)H, epoch, lpart, jpart);
+                           dI, It, vb, dimx, dimy, P, (v4u *)H, epoch, lpart, jpart, ctl);
     OF2D_HIP(hipGetLastError());
 }
 
@@ -1134,6 +1171,78 @@ void launch_fluid_report(const double *lpart, int nb, const float *jpart, float 
                          const unsigned *status, FluidReport *report, hipStream_t st) {
     hipLaunchKernelGGL(fluid_report_kernel, dim3(1), dim3(1024), 0, st, lpart, nb, jpart, scal,
                        status, report);
+    OF2D_HIP(hipGetLastError());
+}
+
+// fluid_report_kernel's reductions and report, then the iteration's decisions
+// as the host loop took them (ImageRegistrationFluid.cpp:99-124 with
+// Logger::update_error, Logger.cpp:32-51): err = diffnorm / prevnorm in float
+// (Registration's logger_error) from the exact float sums or the fp64 sums;
+// break when !fixed && err < 0.001f && it > 1 (the stop word: every later
+// iteration's kernels return at once); otherwise regrid when the minimum
+// Jacobian is below 0.5 (kFluidRegridWord, and the motion index flips to the
+// field the regrid writes).  The report's flags word is written last.
+__global__ __launch_bounds__(1024) void fluid_report_decide_kernel(
+    const double *__restrict__ p, int nb, const float *__restrict__ jpart,
+    float *__restrict__ scal, const float *__restrict__ seq, float npx, int fixed,
+    FluidReport *__restrict__ rep, FluidCtl ctl) {
+    if (fluid_stopped(ctl)) return;
+    double a = 0.0, b = 0.0;
+    float m = __builtin_inff();
+    for (int i = threadIdx.x; i < nb; i += 1024) {
+        a += p[2 * i];
+        b += p[2 * i + 1];
+        m = (jpart[i] < m) ? jpart[i] : m;
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        a += __shfl_down(a, off);
+        b += __shfl_down(b, off);
+    }
+    __shared__ double red[2][16];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (lane == 0) {
+        red[0][wave] = a;
+        red[1][wave] = b;
+    }
+    m = wide_min(m);  // (synchronises the block)
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < 16; w++) {
+            a += red[0][w];
+            b += red[1][w];
+        }
+        scal[2] = m;
+        // Logger::update_error's two norms as floats (logger_error: the fp64
+        // sums rounded to float, or the reference's float running sums)
+        const float sd = seq ? seq[0] : (float)a, sp = seq ? seq[1] : (float)b;
+        const float prevnorm = sp / npx, diffnorm = sd / npx;
+        const float err = prevnorm == 0.0f ? 0.0f : diffnorm / prevnorm;
+        const bool brk = !fixed && err < 0.001f && ctl.it > 1;
+        const bool regrid = !brk && m < 0.5f;
+        unsigned *w = ctl.w;
+        if (brk) atomicMin(reinterpret_cast<int *>(w + kStopWord), ctl.it);
+        w[kFluidRegridWord] = regrid ? 1u : 0u;
+        if (regrid) w[kFluidMcurWord] ^= 1u;
+        rep->sums[0] = a;
+        rep->sums[1] = b;
+        rep->maxabs = scal[0];
+        rep->dt = scal[1];
+        rep->jmin = m;
+        rep->status = w[0];
+        rep->seq[0] = sd;
+        rep->seq[1] = sp;
+        rep->err = err;
+        __atomic_store_n(&rep->flags,
+                         kFluidDone | (brk ? kFluidBreak : 0u) | (regrid ? kFluidRegrid : 0u),
+                         __ATOMIC_RELEASE);
+    }
+}
+void launch_fluid_report_decide(const double *lpart, int nb, const float *jpart, float *scal,
+                                const float *seq, double npx, bool fixed, FluidReport *report,
+                                hipStream_t st, FluidCtl ctl) {
+    if (!ctl.w) throw std::invalid_argument("launch_fluid_report_decide: control words");
+    hipLaunchKernelGGL(fluid_report_decide_kernel, dim3(1), dim3(1024), 0, st, lpart, nb, jpart,
+                       scal, seq, (float)npx, fixed ? 1 : 0, report, ctl);
     OF2D_HIP(hipGetLastError());
 }
 

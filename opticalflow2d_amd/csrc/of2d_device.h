@@ -212,6 +212,34 @@ void launch_hs_precheck(const float2 *base, size_t count, int P, int ghost, int 
                         float alphasq, unsigned *range_flag, unsigned *status, hipStream_t st);
 constexpr int kRangeFlagWord = 32;  // word of the 64-word status buffers holding range_flag
 constexpr int kStopWord = 33;  // the exact-Logger loop's break (seqnorm_decide)
+// the Fluid loop's device-side decisions (Registration::loop_fluid, FluidCtl):
+// the iteration just decided regridded (the next iteration's estimate reads as
+// zero, its Logger prev is the buffer's content), and which of the level's two
+// motion fields holds the accumulated motion
+constexpr int kFluidRegridWord = 34;
+constexpr int kFluidMcurWord = 35;
+// A Fluid iteration's kernels and its place in the loop: w = the 64-word
+// status buffer (kStopWord: the first breaking iteration, 0x7f7f7f7f none;
+// kFluidRegridWord, kFluidMcurWord), it = the iteration.  Every kernel of an
+// iteration past the break returns at once; w == nullptr: no control words
+// (the kernels' plain behaviour, other callers)
+struct FluidCtl {
+    unsigned *w = nullptr;
+    int it = 0;
+};
+// blocks of the launches that the control words usually make no-ops (the
+// regrid's): grid-stride loops over a capped grid, so an idle launch costs a
+// few microseconds instead of dispatching a block per tile
+constexpr int kCappedGrid = 2048;
+// (plain loads: the words are written by earlier kernels of the same stream)
+__device__ __forceinline__ bool fluid_stopped(const FluidCtl &c) {
+    return c.w && (int)c.w[kStopWord] < c.it;
+}
+// the iteration's input estimate is the zero field of a regrid (its buffer
+// still holds the pre-regrid estimate, the Logger's prev)
+__device__ __forceinline__ bool fluid_zero_est(const FluidCtl &c) {
+    return c.w && c.w[kFluidRegridWord] != 0u;
+}
 // partial-row length that fits every HS kernel (single, pair, triple)
 inline int hs_partial_blocks(int P, int dimx, int nrows) {
     int nb = hs_nblocks(P, nrows);
@@ -414,7 +442,8 @@ size_t sor_granule_bytes(int dimx, int dimy);
 // epoch: > every earlier epoch on H, the same epoch as the sor_pack before it;
 // ticket: per-H counter, a multiple of nstrips before the launch.
 void launch_sor(float4 *vb, int dimx, int dimy, int P, float mu, float lambda, float omega,
-                void *H, unsigned epoch, unsigned *ticket, unsigned *status, hipStream_t st);
+                void *H, unsigned epoch, unsigned *ticket, unsigned *status, hipStream_t st,
+                FluidCtl ctl = {});
 // vb's b <- force(u, dI, It); if v != nullptr also vb's v <- v; granule region
 // 0 <- column 0 of v tagged with epoch
 void launch_sor_pack(float4 *vb, const float2 *u, const float2 *dI, const float *It,
@@ -423,7 +452,8 @@ void launch_sor_pack(float4 *vb, const float2 *u, const float2 *dI, const float 
 // after a regrid: dI, It <- gradients of Iaux (set_derivatives) and vb's b <-
 // force of a zero estimate, granule region 0 <- column 0 of v tagged epoch
 void launch_regrid_pack(const float *Iref, const float *Iaux, float2 *dI, float *It, float4 *vb,
-                        int dimx, int dimy, int P, void *H, unsigned epoch, hipStream_t st);
+                        int dimx, int dimy, int P, void *H, unsigned epoch, hipStream_t st,
+                        FluidCtl ctl = {});
 void launch_force(const float2 *u, const float2 *dI, const float *It, float2 *f, int dimx,
                   int dimy, int P, hipStream_t st);
 int increment_nblocks(int dimx, int dimy);
@@ -438,10 +468,10 @@ int sor_increment_workers();
 void launch_sor_increment(float4 *vb, int dimx, int dimy, int P, float mu, float lambda,
                           float omega, void *H, unsigned epoch, unsigned *ticket,
                           unsigned long long *ctr, const float2 *u, float2 *R, float *part,
-                          float *scal, unsigned *status, hipStream_t st);
+                          float *scal, unsigned *status, hipStream_t st, FluidCtl ctl = {});
 // R and scal[0] = maxabs(R), scal[1] = 0.65f / maxabs
 void launch_increment(const float2 *u, const float4 *vel, float2 *R, int dimx, int dimy, int P,
-                      float *part, float *scal, hipStream_t st);
+                      float *part, float *scal, hipStream_t st, FluidCtl ctl = {});
 // uo <- u + R dt (dt < 65) or u; Logger partials of uo against prev (against u
 // when prev is null); per-block Jacobian minima of uo into jpart (their min:
 // launch_fluid_report); vb's b <- force(uo) and granule region 0 tagged with
@@ -449,7 +479,7 @@ void launch_increment(const float2 *u, const float4 *vel, float2 *R, int dimx, i
 void launch_fluid_step(const float2 *u, const float2 *R, float2 *uo, const float2 *prev,
                        const float *scal, const float2 *dI, const float *It, float4 *vb, int dimx,
                        int dimy, int P, void *H, unsigned epoch, double *lpart, float *jpart,
-                       hipStream_t st);
+                       hipStream_t st, FluidCtl ctl = {});
 // Per-iteration report a kernel writes straight into host memory (fine-grained
 // pinned, so no copy launches): the Fluid loop's Logger sums, maxabs, dt,
 // min Jacobian and status word
@@ -457,7 +487,11 @@ struct FluidReport {
     double sums[2];
     float maxabs, dt, jmin;
     unsigned status;
+    float seq[2];   // the reference's float Logger sums (exact mode)
+    float err;      // the Logger error as the host computes it (logger_error)
+    unsigned flags;  // kFluidBreak, kFluidRegrid; kFluidDone once written
 };
+constexpr unsigned kFluidBreak = 1u, kFluidRegrid = 2u, kFluidDone = 4u;
 // The end of a Fluid iteration's device work: the nb Logger partial pairs
 // reduced as launch_reduce_partials does (same order, same bits), the minimum
 // of the nb Jacobian partials into scal[2], and {sums, scal[0..2], *status}
@@ -465,6 +499,20 @@ struct FluidReport {
 // three copies)
 void launch_fluid_report(const double *lpart, int nb, const float *jpart, float *scal,
                          const unsigned *status, FluidReport *report, hipStream_t st);
+// ... and the iteration's decisions on the device (ImageRegistrationFluid.cpp:
+// 99-124): err from the exact float sums `seq` (the reference's Logger) or from
+// the fp64 sums (seq null), the break (!fixed, err < 0.001f, it > 1: the stop
+// word), the regrid (no break and min Jacobian < 0.5: kFluidRegridWord, and the
+// motion index flips); the report carries them for the host's lines
+void launch_fluid_report_decide(const double *lpart, int nb, const float *jpart, float *scal,
+                                const float *seq, double npx, bool fixed, FluidReport *report,
+                                hipStream_t st, FluidCtl ctl);
+// the regrid of an iteration that decided one (kFluidRegridWord; a no-op
+// otherwise): motion[mcur'] <- accumulate(motion[1 - mcur'], est) with mcur'
+// the flipped index, Iaux <- warp2d(Imov, new motion); est is left as it is
+// (the next iteration reads it as zero and as the Logger's prev)
+void launch_regrid_if(float2 *m0, float2 *m1, const float2 *est, const float *Imov, float *Iaux,
+                      int dimx, int dimy, int P, hipStream_t st, FluidCtl ctl);
 void launch_logger(const float4 *vb, float2 *u, float2 *prev, int dimx, int dimy, int P,
                    double *partial, hipStream_t st);
 

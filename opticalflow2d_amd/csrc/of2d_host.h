@@ -97,13 +97,17 @@ struct DevArray {
     }
 };
 
+// the Fluid loop's report ring (iterations enqueued ahead of the host's read)
+constexpr int kFluidReports = 8;
+// iterations the Fluid loop enqueues beyond the one whose report it reads
+constexpr int kFluidAhead = 3;
 // Pinned host scratch for the per-chunk read-back
 struct HostScratch {
     double *sums = nullptr;
     unsigned *status = nullptr;
     float *flt = nullptr;
     float *seqh = nullptr;  // coherent, mapped: seqnorm_decide's copy of the exact sums
-    FluidReport *report = nullptr;  // hipHostMallocCoherent
+    FluidReport *report = nullptr;  // [kFluidReports], hipHostMallocCoherent
     int cap = 0;
     void ensure(int n);
     ~HostScratch();
@@ -240,7 +244,9 @@ class Registration {
     bool exact_norms() const { return !fixed_ && !logger_fp64_; }
     // enqueue the exact norms of one Logger update into d_seq_[2t], [2t + 1]
     // (synchronous loops: Elastic, Fluid; workspace 0, on st_)
-    void seqnorm(const Level &L, const float2 *cur, const float2 *prev, int t);
+    // (stop, t0: the batch returns at once when *stop < t0, Fluid's loop)
+    void seqnorm(const Level &L, const float2 *cur, const float2 *prev, int t,
+                 const int *stop = nullptr, int t0 = 0);
     // run_chunked with the reference's float norms (single steps in groups of
     // up to three into a ring, each group's norms as one batch on the norm
     // streams); with step3m, run_exact_pipelined

@@ -48,7 +48,7 @@ void HostScratch::ensure(int n) {
     if (seqh) (void)hipHostFree(seqh);
     if (!status) OF2D_HIP(hipHostMalloc(&status, 64 * sizeof(unsigned)));
     if (!report)
-        OF2D_HIP(hipHostMalloc(&report, sizeof(FluidReport),
+        OF2D_HIP(hipHostMalloc(&report, sizeof(FluidReport) * kFluidReports,
                                hipHostMallocCoherent | hipHostMallocMapped));
     OF2D_HIP(hipHostMalloc(&sums, sizeof(double) * 4 * n));
     OF2D_HIP(hipHostMalloc(&flt, sizeof(float) * 4 * n));
@@ -395,13 +395,32 @@ void Registration::estimate_level(int s) {
     }
 }
 
-void Registration::seqnorm(const Level &L, const float2 *cur, const float2 *prev, int t) {
+void Registration::seqnorm(const Level &L, const float2 *cur, const float2 *prev, int t,
+                           const int *stop, int t0) {
     // the profile of the last call predicts this one when it was on the same grid
     const bool use_prof = seq_dx_[0] == L.dx && seq_dy_[0] == L.dy;
     seq_dx_[0] = L.dx;
     seq_dy_[0] = L.dy;
-    launch_seqnorm(cur, prev, L.dx, L.dy, L.P, d_seqws_[0].p, use_prof, d_seq_.p + 2 * (size_t)t,
-                   nullptr, st_);
+    if (!stop) {
+        launch_seqnorm(cur, prev, L.dx, L.dy, L.P, d_seqws_[0].p, use_prof,
+                       d_seq_.p + 2 * (size_t)t, nullptr, st_);
+        return;
+    }
+    // launch_seqnorm's three stages, each returning at once past the loop's
+    // break (*stop < t0: an iteration the host enqueued ahead of its decision)
+    SeqnormBatch B;
+    B.K = 1;
+    B.u[0] = prev;
+    B.u[1] = cur;
+    B.ws[0] = d_seqws_[0].p;
+    B.use_profile[0] = use_prof;
+    B.stop = stop;
+    B.t0 = t0;
+    launch_seqnorm_pass(B, L.dx, L.dy, L.P, st_);
+    launch_seqnorm_refine(B, L.dx, L.dy, L.P, st_);
+    B.use_profile[0] = false;
+    B.out[0] = d_seq_.p + 2 * (size_t)t;
+    launch_seqnorm_walk(B, L.dx, L.dy, L.P, st_);
 }
 
 // The chunked loop of run_chunked with the reference's float norms for the

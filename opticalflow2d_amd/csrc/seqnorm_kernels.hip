@@ -921,6 +921,11 @@ __global__ __launch_bounds__(kSnChk) void seqnorm_check(unsigned nt, SnJobs J) {
         Pb[n] += off;
     }
     if (!active) return;
+    // the window's low end without a profile: kSnWideLo up to 2^25 terms, then
+    // scaled down with the count to the 1/16 floor (past 2^24 terms the float
+    // sum stagnates further behind the prefix as the grid grows: 8192^2 1/4,
+    // 16384^2 1/16) — a prediction only, the walk is exact either way
+    const double wide_lo = fmax(1.0 / 16, kSnWideLo * fmin(1.0, 8192.0 / (double)nt));
     bool listed = false;
     for (int n = 0; n < 2; n++) {
         if (!(h[n] & (kHdrZero | kHdrNan)) && a[n] < INFINITY && Pb[n] < INFINITY) {
@@ -933,7 +938,7 @@ __global__ __launch_bounds__(kSnChk) void seqnorm_check(unsigned nt, SnJobs J) {
             const double wd = pq == 2 ? 1.0 / 64 : (pq == 1 ? 1.0 / 32 : 1.0 / 16);
             const unsigned want =
                 pq ? cand_window(Pb[n] * d0[n] * (1.0 - wd), (Pb[n] + a[n]) * d1[n] * (1.0 + wd))
-                   : cand_window(Pb[n] * kSnWideLo, (Pb[n] + a[n]) * (1.0 + 1.0 / 16));
+                   : cand_window(Pb[n] * wide_lo, (Pb[n] + a[n]) * (1.0 + 1.0 / 16));
             const int wl = hdr_elo(want), wn = hdr_nc(want), hl = hdr_elo(h[n]), hn = hdr_nc(h[n]);
             unsigned hh = h[n];
             // (a header the pass left pending, its window wider than two

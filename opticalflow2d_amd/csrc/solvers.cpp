@@ -152,99 +152,102 @@ int Registration::loop_demons(Level &L, int niter, int &final_buf) {
 // ImageRegistrationFluid::estimate_motion_at_current_resolution loop body
 // (ImageRegistrationFluid.cpp:94-125) with OpticalFlowFluid::get_update
 // (OpticalFlowFluid.cpp:123-140).  The reference prints a line every
-// iteration and may regrid after any iteration, so this loop takes its
-// decisions per iteration: one small read-back (Logger sums, maxabs, dt,
-// min Jacobian, status) per iteration.
+// iteration and may break or regrid after any iteration; both decisions are
+// taken on the device (launch_fluid_report_decide: the stop word, the regrid
+// word, the motion index) and every kernel of an iteration reads them, so the
+// host enqueues kFluidAhead iterations ahead of the report it reads and prints
+// the lines from the reports afterwards, in order; the GPU never waits for the
+// host between iterations (it did: ~20-28 us per iteration).
+// Iterations enqueued past a break return at once.  After a regrid the next
+// iteration reads its estimate as zero while the buffer keeps the old
+// estimate as the Logger's prev (fluid_zero_est), so no buffer changes role
+// on the device's decision: iteration i reads buf[i & 1] and writes
+// buf[(i + 1) & 1].
 int Registration::loop_fluid(Level &L, int niter) {
     const float mu = params_[0], lambda = params_[1];
     const float omega = params_.size() == 3 ? params_[2] : (float)0.66;  // OpticalFlowFluid.h:10
-    float2 *prev = L.tmp.p;
     L.tmp.zero(st_);  // Logger::prev starts at zero (Logger.cpp:13, new per refine)
     float *scal = d_scalar_ + 8;  // [0] maxabs, [1] dt, [2] min jacobian
     const int nb = increment_nblocks(L.dx, L.dy);
     const double npx = (double)L.dx * L.dy;
     const bool exact = exact_norms();
-    // L.est[0] is the estimate; L.force receives the next one and the two swap
-    // every iteration.  prev_separate: the Logger's previous motion is L.tmp,
-    // not the iteration's input estimate (first iteration, after a regrid);
-    // packed: vb's b already holds the force of the estimate, tagged with the
-    // next epoch (fluid_step of the previous iteration).
-    bool prev_separate = true, packed = false, regridded = false;
-    // one iteration's device work, up to its report in host memory
-    auto enqueue = [&]() {
-        float2 *est = L.est[0].p;
-        // get_force(force, motion) into vb's b, then the SOR sweep of the velocity (v)
+    last_err_.clear();
+    if (niter <= 0) return 0;
+    // control words: no break yet, no regrid, the level's motion index
+    OF2D_HIP(hipMemsetAsync(d_status_ + kStopWord, 0x7f, sizeof(int), st_));
+    OF2D_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(d_status_ + kFluidRegridWord), 0,
+                               1, st_));
+    OF2D_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(d_status_ + kFluidMcurWord),
+                               L.mcur, 1, st_));
+    const int *stop = reinterpret_cast<const int *>(d_status_ + kStopWord);
+    float2 *buf[2] = {L.est[0].p, L.force.p};
+    static_assert(kFluidAhead + 2 <= kFluidReports && kFluidAhead + 2 <= kExactEv, "rings");
+    // iteration i's device work, up to its report in host memory
+    auto enqueue = [&](int i) {
+        const FluidCtl c{d_status_, i};
+        float2 *in = buf[i & 1], *out = buf[(i + 1) & 1];
+        // get_force(force, motion) into vb's b, then the SOR sweep of the
+        // velocity (v): the first iteration packs it, later ones find it packed
+        // by the previous fluid_step (or repacked by the regrid pass)
         const unsigned ep = ++epoch_;
-        if (!packed && regridded)  // gradients of the new warped image + force of est = 0
-            launch_regrid_pack(L.Iref.p, L.Iaux.p, L.dI.p, L.It.p, L.vb.p, L.dx, L.dy, L.P,
-                               L.sorH.p, ep, st_);
-        else if (!packed)
-            launch_sor_pack(L.vb.p, est, L.dI.p, L.It.p, nullptr, L.dx, L.dy, L.P, L.sorH.p, ep,
+        if (i == 0)
+            launch_sor_pack(L.vb.p, in, L.dI.p, L.It.p, nullptr, L.dx, L.dy, L.P, L.sorH.p, ep,
                             st_);
-        regridded = false;
+        else  // after a regrid: gradients of the new warped image + force of est = 0
+            launch_regrid_pack(L.Iref.p, L.Iaux.p, L.dI.p, L.It.p, L.vb.p, L.dx, L.dy, L.P,
+                               L.sorH.p, ep, st_, c);
         if (sor_increment_workers() != 0) {  // the increment rides behind the sweep
             launch_sor_increment(L.vb.p, L.dx, L.dy, L.P, mu, lambda, omega, L.sorH.p, ep,
-                                 L.sorTicket.p, L.sorCtr.p, est, L.increment.p, L.part.p, scal,
-                                 d_status_, st_);
+                                 L.sorTicket.p, L.sorCtr.p, in, L.increment.p, L.part.p, scal,
+                                 d_status_, st_, c);
         } else {
             launch_sor(L.vb.p, L.dx, L.dy, L.P, mu, lambda, omega, L.sorH.p, ep, L.sorTicket.p,
-                       d_status_, st_);
-            launch_increment(est, L.vb.p, L.increment.p, L.dx, L.dy, L.P, L.part.p, scal, st_);
+                       d_status_, st_, c);
+            launch_increment(in, L.vb.p, L.increment.p, L.dx, L.dy, L.P, L.part.p, scal, st_, c);
         }
-        // integrate, Logger, Jacobian and the next iteration's force in one pass
-        launch_fluid_step(est, L.increment.p, L.force.p, prev_separate ? prev : nullptr, scal,
-                          L.dI.p, L.It.p, L.vb.p, L.dx, L.dy, L.P, L.sorH.p, ep + 1, d_partial_,
-                          L.part.p, st_);
-        if (exact) seqnorm(L, L.force.p, prev_separate ? prev : est, 0);
-        std::swap(L.est[0], L.force);
-        prev_separate = false;
-        packed = true;
-        // Logger sums, maxabs, dt, min Jacobian and the status word straight
-        // into host memory: one launch, then the one sync of the iteration
-        launch_fluid_report(d_partial_, nb, L.part.p, scal, d_status_, hs_.report, st_);
-        if (exact)
-            OF2D_HIP(hipMemcpyAsync(hs_.flt, d_seq_.p, 2 * sizeof(float), hipMemcpyDeviceToHost,
-                                    st_));
+        // integrate, Logger, Jacobian and the next iteration's force in one
+        // pass; the Logger's prev is L.tmp (zero) in the first iteration, the
+        // input buffer's content after (the estimate, or after a regrid the
+        // pre-regrid estimate, Logger.cpp:45)
+        launch_fluid_step(in, L.increment.p, out, i == 0 ? L.tmp.p : nullptr, scal, L.dI.p,
+                          L.It.p, L.vb.p, L.dx, L.dy, L.P, L.sorH.p, ep + 1, d_partial_, L.part.p,
+                          st_, c);
+        if (exact) seqnorm(L, out, i == 0 ? L.tmp.p : in, 0, stop, i);
+        // sums, maxabs, dt, min Jacobian, status, the error and the decisions
+        // straight into the host-mapped report; then the regrid if decided
+        launch_fluid_report_decide(d_partial_, nb, L.part.p, scal, exact ? d_seq_.p : nullptr,
+                                   npx, fixed_, hs_.report + i % kFluidReports, st_, c);
+        launch_regrid_if(L.motion[0].p, L.motion[1].p, out, L.Imov.p, L.Iaux.p, L.dx, L.dy, L.P,
+                         st_, c);
+        OF2D_HIP(hipEventRecord(ev_step_[i % kExactEv], st_));
     };
-    last_err_.clear();
-    if (niter > 0) enqueue();
-    int iter;
+    int enq = 0, iter;
     for (iter = 0; iter < niter; iter++) {
-        OF2D_HIP(hipStreamSynchronize(st_));
-        check_reported_status(hs_.report->status);
-        const float maxabs = hs_.report->maxabs, dt = hs_.report->dt, jmin = hs_.report->jmin;
-        const float err = exact ? logger_error(hs_.flt[0], hs_.flt[1], npx)
-                                : logger_error(hs_.report->sums[0], hs_.report->sums[1], npx);
-        const bool brk = !fixed_ && err < 0.001f && iter > 1;
-        const bool regrid = !brk && jmin < 0.5;
-        if (regrid) {  // regridding (ImageRegistrationFluid.cpp:108-124)
-            // the Logger keeps this iteration's motion (the buffers trade places:
-            // L.tmp takes the estimate, the old Logger buffer becomes the
-            // estimate, zeroed by the regrid pass); motion accumulates the
-            // estimate, the moving image is warped by it, and the next
-            // iteration starts with its gradients and force (launch_regrid_pack)
-            std::swap(L.tmp, L.est[0]);
-            prev = L.tmp.p;
-            prev_separate = true;
-            launch_regrid(L.motion[L.mcur].p, L.tmp.p, L.est[0].p, L.motion[1 - L.mcur].p,
-                          L.Imov.p, L.Iaux.p, L.dx, L.dy, L.P, st_);
-            L.mcur ^= 1;
-            packed = false;  // the packed force was of the old estimate and gradients
-            regridded = true;
-        }
-        // the next iteration goes to the GPU before this one's lines are
-        // printed (the report is in host memory: the values stay)
-        if (!brk && iter + 1 < niter) enqueue();
+        while (enq < niter && enq <= iter + kFluidAhead) enqueue(enq++);
+        OF2D_HIP(hipEventSynchronize(ev_step_[iter % kExactEv]));
+        const FluidReport &r = hs_.report[iter % kFluidReports];
+        check_reported_status(r.status);
         print("Dumax: %.3f\tMaxabs increment: %.3f\t Timestep: %.3f\n", (double)0.65f,
-              (double)maxabs, (double)dt);
-        last_err_.push_back(err);
-        if (verbose_) print("Iteration: %d\tError:%.4f\n", iter, (double)err);
-        if (brk) {
+              (double)r.maxabs, (double)r.dt);
+        last_err_.push_back(r.err);
+        if (verbose_) print("Iteration: %d\tError:%.4f\n", iter, (double)r.err);
+        if (r.flags & kFluidBreak) {
             iter++;
             break;
         }
-        if (regrid) print("Regridding on iteration: %d\tMin Jacobian: %.3f\n", iter, (double)jmin);
+        if (r.flags & kFluidRegrid)
+            print("Regridding on iteration: %d\tMin Jacobian: %.3f\n", iter, (double)r.jmin);
     }
+    // the iterations enqueued past a break are no-ops; then the level's state
+    // as the host loop left it: L.est[0] the last estimate (zero after a final
+    // regrid, which the next iteration would have read as zero), L.mcur the
+    // accumulated motion
+    OF2D_HIP(hipMemcpyAsync(hs_.status + 2, d_status_ + kFluidRegridWord, 2 * sizeof(unsigned),
+                            hipMemcpyDeviceToHost, st_));
+    OF2D_HIP(hipStreamSynchronize(st_));
+    if (buf[iter & 1] != L.est[0].p) std::swap(L.est[0], L.force);
+    if (hs_.status[2]) L.est[0].zero(st_);
+    L.mcur = hs_.status[3] ? 1 : 0;
     return iter;
 }
 

@@ -105,6 +105,76 @@ def test_rccl_halo_rehearsal_on_one_rank():
     assert r.stdout.count("SELF-HALO-OK") == 2 and "SELF-HALO-REFUSED" in r.stdout
 
 
+TWO_RANKS = r"""
+import os, sys, time, numpy as np
+sys.path.insert(0, sys.argv[1])
+from opticalflow2d_amd import SlabSolver, lib
+from opticalflow2d_amd import synthetic as S
+from opticalflow2d_amd.slab import rccl_unique_id, halo_rows
+lib()
+rank, d, fixed = int(sys.argv[2]), sys.argv[3], sys.argv[4] == "1"
+n, world = 512, 2
+if rank == 0:
+    open(os.path.join(d, "uid.tmp"), "wb").write(rccl_unique_id())
+    os.rename(os.path.join(d, "uid.tmp"), os.path.join(d, "uid"))
+while not os.path.exists(os.path.join(d, "uid")):
+    time.sleep(0.05)
+uid = open(os.path.join(d, "uid"), "rb").read()
+lo, hi = halo_rows(n, rank, world)
+ref, mov = S.procedural_pair(n, 0, n)  # the one grid's images, sliced
+ref, mov = ref[:, lo:hi], mov[:, lo:hi]
+s = SlabSolver(n, n, 0.1, rank, world, device=rank, unique_id=uid)
+s.set_option("logger_fp64", 0)  # the reference's Logger chained over RCCL
+assert s.info()["logger_reference"] == 1 and s.info()["rccl_ranks"] == 2, s.info()
+s.set_images(ref, mov)
+done = s.run(1000, fixed_iters=fixed)
+np.save(os.path.join(d, f"m{rank}.npy"), s.motion())
+np.save(os.path.join(d, f"e{rank}.npy"), s.errors())
+open(os.path.join(d, f"it{rank}"), "w").write(str(done))
+s.close()
+"""
+
+
+def _device_count():
+    import ctypes
+    from opticalflow2d_amd import lib
+    c = ctypes.c_int(0)
+    lib().of2d_device_count(ctypes.byref(c))
+    return c.value
+
+
+@pytest.mark.parametrize("fixed", [False, True])
+def test_two_rccl_ranks_match_one_grid(tmp_path, fixed):
+    """Two RCCL ranks on two devices (one process each): the halo send / recv
+    between distinct devices and, with logger_fp64 = 0, the reference's Logger
+    chained over RCCL — the break iteration, every error and the motion equal
+    the one-rank grid's.  Needs two GPUs: skipped on a one-GPU box (it is here
+    for the first multi-GPU box)."""
+    if _device_count() < 2:
+        pytest.skip("needs two GPUs")
+    import numpy as np
+    procs = [subprocess.Popen([sys.executable, "-c", TWO_RANKS, ROOT, str(r), str(tmp_path),
+                               "1" if fixed else "0"], stdout=subprocess.PIPE,
+                              stderr=subprocess.PIPE, text=True) for r in range(2)]
+    outs = [p.communicate(timeout=240) for p in procs]
+    for p, (o, e) in zip(procs, outs):
+        assert p.returncode == 0, o[-2000:] + e[-4000:]
+    from opticalflow2d_amd import SlabSolver
+    from opticalflow2d_amd import synthetic as S
+    n = 512
+    ref, mov = S.procedural_pair(n, 0, n)
+    one = SlabSolver(n, n, 0.1, 0, 1, device=0)
+    one.set_images(ref, mov)
+    done = one.run(1000, fixed_iters=fixed)
+    want, werr = one.motion(), one.errors()
+    one.close()
+    got = np.concatenate([np.load(tmp_path / f"m{r}.npy") for r in range(2)], axis=1)
+    for r in range(2):
+        assert int(open(tmp_path / f"it{r}").read()) == done
+        assert np.array_equal(np.load(tmp_path / f"e{r}.npy").view(np.uint32), werr.view(np.uint32))
+    assert np.array_equal(got.view(np.uint64), want.view(np.uint64))
+
+
 def _free_port():
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))

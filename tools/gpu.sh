@@ -13,6 +13,8 @@
 #        DESIGN.md §5), texprof / freshprof (kernel trace of the
 #        texture pair's warm / fresh loops), snbench /
 #        snprof (the Logger-norm harness: stage timings / kernel stats),
+#        fluidtrace / fluidtracealt (config 4's kernel trace with the in-tree
+#        library / tools/lib_alt.so, and its GPU idle time: tools/gpu_idle.py),
 #        mtprobe / mtprobeprof (tools/mt_launch_probe: the slab group's
 #        multi-thread launch pattern without the library, plain / under the
 #        kernel trace; q16: 16 hardware queues, one per stream; serial: the eight
@@ -53,6 +55,8 @@ for s in "$@"; do
         snws) run snws 300 env SNB_WS=1 tools/seqnorm_bench 4096 12 3 0.95 ;;
         sndebug) run sndebug 300 env OF2D_LIB_PATH=tools/ab/sndebug/libof2d.so python -u tools/time_convergence.py 4096 1 ;;  # tools/build_variant.sh sndebug registration.cpp -DOF2D_SN_DEBUG=1
         snprof) run snprof 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/$O/${tag}_snprof" -o k -- "$R/tools/seqnorm_bench" 4096 24 3 ;;
+        fluidtrace) run fluidtrace 300 rocprofv3 --kernel-trace --output-format csv -d "$R/$O/${tag}_fluidtrace" -o k -- python3 -u "$R/bench_configs.py" --configs 4 --no-cpu && python3 tools/gpu_idle.py "$O/${tag}_fluidtrace/k_kernel_trace.csv" sor_strip_kernel | tee -a "$O/${tag}_fluidtrace.log" ;;
+        fluidtracealt) OF2D_LIB_PATH="$R/tools/lib_alt.so" run fluidtracealt 300 rocprofv3 --kernel-trace --output-format csv -d "$R/$O/${tag}_fluidtracealt" -o k -- python3 -u "$R/bench_configs.py" --configs 4 --no-cpu && python3 tools/gpu_idle.py "$O/${tag}_fluidtracealt/k_kernel_trace.csv" sor_strip_kernel | tee -a "$O/${tag}_fluidtracealt.log" ;;
         mtprobe) run mtprobe 120 tools/mt_launch_probe 8 3000 ;;
         mtprobeprofserial) run mtprobeprofserial 180 rocprofv3 --kernel-trace --output-format csv -d "$R/$O/${tag}_mtprobeprofserial" -o k -- "$R/tools/mt_launch_probe" 8 3000 64 serial ;;
         mtprobeprofq16) GPU_MAX_HW_QUEUES=16 run mtprobeprofq16 180 rocprofv3 --kernel-trace --output-format csv -d "$R/$O/${tag}_mtprobeprofq16" -o k -- "$R/tools/mt_launch_probe" 8 3000 ;;
