@@ -833,11 +833,19 @@ __global__ __launch_bounds__(256) void regrid_pack_kernel(
     __syncthreads();  // fo is rewritten by the block's next tile
     }
 }
+// blocks of the device-decided regrid pack (a no-op on most iterations: a
+// smaller grid is a cheaper no-op, a larger one a faster real pack).  One
+// tile per block up to 8192^2: config 4 +0.6-0.7 % against the host-decided
+// loop, where 2048 blocks (16 tiles each at 8192^2) made the real packs 38 %
+// slower and 8192 blocks gained 0.2 % (profiles/r06f_fluid_packcap_ab.log)
+#ifndef OF2D_FLUID_PACK_CAP
+#define OF2D_FLUID_PACK_CAP 32768
+#endif
 void launch_regrid_pack(const float *Iref, const float *Iaux, float2 *dI, float *It, float4 *vb,
                         int dimx, int dimy, int P, void *H, unsigned epoch, hipStream_t st,
                         FluidCtl ctl) {
     const int ntiles = ((dimx + kSkI - 1) / kSkI) * ((dimy + kSkJ - 1) / kSkJ);
-    hipLaunchKernelGGL(regrid_pack_kernel, dim3(ctl.w ? std::min(ntiles, kCappedGrid) : ntiles),
+    hipLaunchKernelGGL(regrid_pack_kernel, dim3(ctl.w ? std::min(ntiles, OF2D_FLUID_PACK_CAP) : ntiles),
                        dim3(64, 4), 0, st, Iref, Iaux, dI, It, vb, dimx, dimy, P, (v4u *)H,
                        epoch, ctl);
     OF2D_HIP(hipGetLastError());

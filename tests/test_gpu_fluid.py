@@ -139,3 +139,40 @@ def test_fluid_timestep_skip_and_integrate(gpu, oracle):
     assert body(gt) == body(ot)
     dts = [float(l.split("Timestep:")[1]) for l in body(gt) if "Timestep:" in l]
     assert any(t >= 65.0 for t in dts) and any(t < 65.0 for t in dts), dts
+
+
+@pytest.mark.parametrize("fp64", [0, 1])
+@pytest.mark.parametrize("case", ["faint", "mid", "tex"])
+def test_fluid_convergence_break_on_device(gpu, oracle, case, fp64):
+    """The Fluid loop takes its break and regrid decisions on the device and
+    enqueues iterations ahead of the host's read (solvers.cpp loop_fluid):
+    texture pairs that converge — 'faint' breaks at iteration 3 with every
+    step skipped (dt >= 65), 'mid' at 5 after one regrid, 'tex' at 27 after 11
+    regrids — with the reference's float Logger and with fp64 sums, two
+    register calls (the velocity and the motion fields carry over), bit for
+    bit with the oracle: iterations, motion, warped image, printed lines."""
+    ref, mov = S.texture_pair(96, seed=5)
+    mov = ref + {"faint": 0.08, "mid": 0.3, "tex": 1.0}[case] * (mov - ref)
+    oracle.lib().oracle_set_logger_fp64(fp64)
+    try:
+        g, w, gt, ot = run_both(gpu, oracle, (96, 96), [60], 0, 5, [0.25, 0.0], 1, ref, mov,
+                                calls=2, logger_fp64=fp64)
+    finally:
+        oracle.lib().oracle_set_logger_fp64(0)
+    assert g["iters"] == w["iters"] and g["iters"][0] < 60, (g["iters"], w["iters"])
+    assert np.array_equal(g["motion"], w["motion"])
+    assert np.array_equal(g["warped"], w["warped"])
+    assert body(gt) == body(ot)
+
+
+def test_fluid_break_and_regrid_pyramid(gpu, oracle):
+    """Breaks on two pyramid levels with regrids before them, then a second
+    register call: the levels' motion indices and the estimate buffers the
+    device decided are the host's state afterwards."""
+    ref, mov = S.texture_pair(128, seed=5)
+    g, w, gt, ot = run_both(gpu, oracle, (128, 128), [60, 60], 1, 5, [0.25, 0.0, 0.9], 1, ref,
+                            mov, calls=2)
+    assert g["iters"] == w["iters"], (g["iters"], w["iters"])
+    assert np.array_equal(g["motion"], w["motion"])
+    assert np.array_equal(g["warped"], w["warped"])
+    assert body(gt) == body(ot)

@@ -53,7 +53,7 @@ for s in "$@"; do
         freshprof) OF2D_CONV_FRESH=1 OF2D_CONV_CASE=texture OF2D_CONV_ONLY=1 run freshprof 300 rocprofv3 --kernel-trace --output-format csv -d "$R/$O/${tag}_freshprof" -o k -- python3 -u "$R/tools/time_convergence.py" 4096 1 ;;
         snbench) run snbench 300 bash -c "tools/seqnorm_bench 4096 12 3 0.95 && tools/seqnorm_bench 4096 12 1 0.95 && tools/seqnorm_bench 4096 12 3 0.8" ;;
         snws) run snws 300 env SNB_WS=1 tools/seqnorm_bench 4096 12 3 0.95 ;;
-        sndebug) run sndebug 300 env OF2D_LIB_PATH=tools/ab/sndebug/libof2d.so python -u tools/time_convergence.py 4096 1 ;;  # tools/build_variant.sh sndebug registration.cpp -DOF2D_SN_DEBUG=1
+        sndebug) OF2D_CONV_FRESH=1 OF2D_CONV_CASE=texture OF2D_CONV_ONLY=1 run sndebug 300 env OF2D_LIB_PATH=tools/abx/sndebug/libof2d.so python -u tools/time_convergence.py 4096 1 ;;  # tools/build_variant.sh sndebug registration.cpp -DOF2D_SN_DEBUG=1
         snprof) run snprof 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/$O/${tag}_snprof" -o k -- "$R/tools/seqnorm_bench" 4096 24 3 ;;
         fluidtrace) run fluidtrace 300 rocprofv3 --kernel-trace --output-format csv -d "$R/$O/${tag}_fluidtrace" -o k -- python3 -u "$R/bench_configs.py" --configs 4 --no-cpu && python3 tools/gpu_idle.py "$O/${tag}_fluidtrace/k_kernel_trace.csv" sor_strip_kernel | tee -a "$O/${tag}_fluidtrace.log" ;;
         fluidtracealt) OF2D_LIB_PATH="$R/tools/lib_alt.so" run fluidtracealt 300 rocprofv3 --kernel-trace --output-format csv -d "$R/$O/${tag}_fluidtracealt" -o k -- python3 -u "$R/bench_configs.py" --configs 4 --no-cpu && python3 tools/gpu_idle.py "$O/${tag}_fluidtracealt/k_kernel_trace.csv" sor_strip_kernel | tee -a "$O/${tag}_fluidtracealt.log" ;;
