@@ -5,7 +5,8 @@
 #   tools/gpu.sh <tag> <step>...
 # steps: tests (pytest -m gpu), sntests (Logger-norm tests), slabtests
 #        (slab group / RCCL / ngpus tests), smoke, bench,
-#        prof (rocprofv3 kernel stats of bench.py), conv (convergence-on
+#        prof (rocprofv3 kernel stats of bench.py), benchdrv / profdrv (the
+#        driver's bench command, and its kernel stats), conv (convergence-on
 #        timings at 4096^2), convprof (their kernel trace + stats),
 #        configs (bench_configs.py), ranks (ngpus timings), ranksprof (their
 #        kernel trace, 8 ranks; ranksprofq16 with 16 hardware queues, which
@@ -43,6 +44,8 @@ for s in "$@"; do
         smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
         bench) run bench 600 python bench.py ;;
         prof) run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/$O/${tag}_prof" -o k -- python3 "$R/bench.py" --no-cpu-baseline ;;
+        benchdrv) run benchdrv 600 python bench.py --gpus 1 --steps 20 --warmup 5 ;;
+        profdrv) run profdrv 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/$O/${tag}_profdrv" -o k -- python3 "$R/bench.py" --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --no-default-semantics ;;
         conv) run conv 600 python -u tools/time_convergence.py 4096 3 ;;
         convprof) run convprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/$O/${tag}_convprof" -o k -- python3 -u "$R/tools/time_convergence.py" 4096 1 ;;
         configs) run configs 900 python -u bench_configs.py ;;
