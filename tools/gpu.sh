@@ -16,6 +16,8 @@
 #        snprof (the Logger-norm harness: stage timings / kernel stats),
 #        fluidtrace / fluidtracealt (config 4's kernel trace with the in-tree
 #        library / tools/lib_alt.so, and its GPU idle time: tools/gpu_idle.py),
+#        convlarge (convergence-on procedural pair at 8192^2 and 16384^2; with
+#        CONV_ALT=<dir> also the library tools/abx/<dir>/libof2d.so),
 #        mtprobe / mtprobeprof (tools/mt_launch_probe: the slab group's
 #        multi-thread launch pattern without the library, plain / under the
 #        kernel trace; q16: 16 hardware queues, one per stream; serial: the eight
@@ -60,6 +62,7 @@ for s in "$@"; do
         snprof) run snprof 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/$O/${tag}_snprof" -o k -- "$R/tools/seqnorm_bench" 4096 24 3 ;;
         fluidtrace) run fluidtrace 300 rocprofv3 --kernel-trace --output-format csv -d "$R/$O/${tag}_fluidtrace" -o k -- python3 -u "$R/bench_configs.py" --configs 4 --no-cpu && python3 tools/gpu_idle.py "$O/${tag}_fluidtrace/k_kernel_trace.csv" sor_strip_kernel | tee -a "$O/${tag}_fluidtrace.log" ;;
         fluidtracealt) OF2D_LIB_PATH="$R/tools/lib_alt.so" run fluidtracealt 300 rocprofv3 --kernel-trace --output-format csv -d "$R/$O/${tag}_fluidtracealt" -o k -- python3 -u "$R/bench_configs.py" --configs 4 --no-cpu && python3 tools/gpu_idle.py "$O/${tag}_fluidtracealt/k_kernel_trace.csv" sor_strip_kernel | tee -a "$O/${tag}_fluidtracealt.log" ;;
+        convlarge) for n in 8192 16384; do for v in tree $CONV_ALT; do lp=""; [ $v != tree ] && lp="$R/tools/abx/$v/libof2d.so"; echo "== $n $v" >> "$O/${tag}_convlarge.log"; OF2D_LIB_PATH=$lp OF2D_CONV_CASE=procedural OF2D_CONV_ONLY=1 timeout -k 10 300 python -u tools/time_convergence.py $n 1 >> "$O/${tag}_convlarge.log" 2>&1 || exit $?; done; done; cat "$O/${tag}_convlarge.log" ;;
         mtprobe) run mtprobe 120 tools/mt_launch_probe 8 3000 ;;
         mtprobeprofserial) run mtprobeprofserial 180 rocprofv3 --kernel-trace --output-format csv -d "$R/$O/${tag}_mtprobeprofserial" -o k -- "$R/tools/mt_launch_probe" 8 3000 64 serial ;;
         mtprobeprofq16) GPU_MAX_HW_QUEUES=16 run mtprobeprofq16 180 rocprofv3 --kernel-trace --output-format csv -d "$R/$O/${tag}_mtprobeprofq16" -o k -- "$R/tools/mt_launch_probe" 8 3000 ;;
